@@ -1,0 +1,220 @@
+"""Headline benchmark: wall-clock seconds per 2048x2048 Gaussian-elimination
+solve (fp64, partial pivoting, forward elimination + back substitution) on
+MI355X, with the 2048^2 fp32 matmul reported alongside.
+
+BASELINE.json metric: "wall-clock sec + speedup-vs-sequential, 2048x2048
+Gauss-elim & matmul".  Reference numbers: Gauss 2048^2 OpenMP
+best 0.509428 s; matmul 2048^2 CUDA V2 end-to-end 0.114906 s.
+
+One step = one complete solve of a fresh random 2048^2 system on every GPU:
+the pristine system is copied into the solver's working buffer (the
+elimination is in place), eliminated with the blocked LU (register-resident
+panel + fp64 MFMA trailing GEMM) and back-substituted, all replayed from one
+hipGraph.  N GPUs = N ranks (torchrun), each solving its own system per step
+(weak scaling, "dp" over independent systems); the step time is the MAX over
+ranks and `value` is that wall time.  Data: synthetic random U[-1,1) matrices
+(b = A (1..n)), generated on device; weights/checkpoints do not apply.
+
+  python bench.py [--gpus N --steps K --warmup W] [--n 2048] [--extras]
+
+Output: ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+BASELINE_GAUSS_S = 0.509428  # OpenMP best, 2048^2 (OpenMP_and_MPI/Report.pdf p.4)
+BASELINE_MATMUL_S = 0.114906  # CUDA V2 end-to-end, 2048^2 (CUDA_and_OpenMP/Report.pdf p.2)
+HOST_SEQ_FILE = ROOT / "profiles" / "host_seq_times.json"
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--n", type=int, default=2048)
+    p.add_argument("--backend", default="hip", choices=["hip", "hip-pivot"])
+    p.add_argument("--no-matmul", action="store_true")
+    p.add_argument("--extras", action="store_true",
+                   help="also time the distributed 8192^2 solve and 16384^2 ring matmul (N>1)")
+    p.add_argument("--measure-seq", action="store_true",
+                   help="time the reference sequential loops on this host (slow)")
+    return p.parse_args()
+
+
+def main() -> None:
+    args = parse()
+    import torch
+
+    import gelim
+    from gelim.parallel import comm as C
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
+    comm = C.init_from_env(timeout_s=300)
+    dev = comm.device
+    rank, N = comm.rank, comm.world_size
+    n = args.n
+
+    # -- Gauss: one independent system per GPU --------------------------------
+    src = gelim.random_system(n, seed=1234 + rank, device=dev)
+    solver = gelim.GaussSolver(n, backend=args.backend, pivot="partial", device=dev)
+    x = None
+    for _ in range(args.warmup):
+        x = solver.solve(src)
+    torch.cuda.synchronize(dev)
+    comm.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        x = solver.solve(src)
+    torch.cuda.synchronize(dev)
+    comm.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    comm.all_reduce(t, "max")
+    step_s = t.item() / args.steps
+    err = torch.tensor([gelim.ops.gauss.error_metric(x)], dtype=torch.float64, device=dev)
+    comm.all_reduce(err, "max")
+    info = solver.info()
+
+    # -- matmul 2048^2 fp32 (reference timer semantics) ------------------------
+    mm = None
+    if not args.no_matmul:
+        A, B = gelim.ops.matmul.reference_inputs(2048)
+        A, B = A.pin_memory(), B.pin_memory()
+        Ch = torch.empty_like(A).pin_memory()
+        model = gelim.MatMul("mfma", dev)
+        for _ in range(2):
+            model.run_reference_style(A, B, Ch)
+        runs = [model.run_reference_style(A, B, Ch) for _ in range(5)]
+        e2e = sorted(r.end_to_end_s for r in runs)[len(runs) // 2]
+        ker = sorted(r.kernel_s for r in runs)[len(runs) // 2]
+        ref = A.double() @ B.double()
+        rel = ((Ch.double() - ref).abs().max() / ref.abs().max()).item()
+        mm = {"n": 2048, "end_to_end_s": e2e, "kernel_s": ker, "kernel_tflops": 2 * 2048 ** 3 / ker * 1e-12,
+              "vs_reference_cuda_v2": BASELINE_MATMUL_S / e2e, "max_rel_err": rel}
+
+    # -- speedup vs the reference's sequential loops on THIS host --------------
+    seq = None
+    if args.measure_seq and rank == 0:
+        seq = measure_host_seq(n)
+    elif HOST_SEQ_FILE.exists():
+        seq = json.loads(HOST_SEQ_FILE.read_text())
+
+    extras = {}
+    if args.extras and N > 1:
+        extras = run_extras(comm, gelim, torch)
+
+    if rank == 0:
+        out = {
+            "metric": "wall-clock sec per 2048x2048 Gauss-elim solve (fp64, partial pivoting, "
+                      "elimination + back-substitution) [BASELINE: wall-clock sec + speedup-vs-sequential, "
+                      "2048x2048 Gauss-elim & matmul]",
+            "value": step_s,
+            "unit": "s",
+            "n_gpus": N,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": step_s * 1e3,
+            "higher_is_better": False,
+            "scaling": "weak",
+            "vs_baseline": step_s / BASELINE_GAUSS_S,
+            "speedup_vs_baseline": BASELINE_GAUSS_S / step_s,
+            "dtype": "fp64 (Gauss, reference precision); fp32 (matmul)",
+            "data": "synthetic random U[-1,1) systems generated on device, b = A(1..n)",
+            "config": {"model": f"gauss_elim_{n}x{n}_partial_pivot_{args.backend}", "global_batch": N,
+                       "seq_len": n, "parallelism": f"dp{N} (one independent system per GPU per step)"},
+            "throughput_solves_per_s": N / step_s,
+            "gflops_per_gpu": (2.0 / 3.0) * n ** 3 / step_s * 1e-9,
+            "max_error": err.item(),
+            "singular": info != 0,
+            "matmul_2048": mm,
+        }
+        if seq:
+            out["host_seq"] = seq
+            if "gauss_2048_s" in seq and n == 2048:
+                out["speedup_vs_seq"] = seq["gauss_2048_s"] / step_s
+            if mm and "matmul_2048_s" in seq:
+                mm["speedup_vs_seq_end_to_end"] = seq["matmul_2048_s"] / mm["end_to_end_s"]
+                mm["speedup_vs_seq_kernel"] = seq["matmul_2048_s"] / mm["kernel_s"]
+        if extras:
+            out["extras"] = extras
+        print(json.dumps(out), flush=True)
+    C.destroy()
+
+
+def measure_host_seq(n: int) -> dict:
+    """The reference's sequential loops on this host (the speedup denominator,
+    SURVEY.md §6 caveat): Gauss internal-style elimination and i-j-k matmul."""
+    import torch
+
+    import gelim
+
+    aug = gelim.random_system(n, seed=1234)
+    A = aug[:, :n].contiguous().clone()
+    b = aug[:, n].contiguous().clone()
+    t0 = time.perf_counter()
+    gelim.ops.gauss.cpu_gauss_(A, b, "seq", "partial")
+    gauss_s = time.perf_counter() - t0
+    Am, Bm = gelim.ops.matmul.reference_inputs(2048)
+    t0 = time.perf_counter()
+    gelim.ops.cpu_matmul(Am, Bm)
+    mm_s = time.perf_counter() - t0
+    res = {"gauss_2048_s": gauss_s, "matmul_2048_s": mm_s, "host": os.uname().nodename,
+           "cpus": os.cpu_count(), "measured_at": time.strftime("%Y-%m-%dT%H:%M:%S")}
+    del torch
+    return res
+
+
+def run_extras(comm, gelim, torch) -> dict:
+    """Distributed configs of BASELINE.json: 8192^2 Gauss (column block-cyclic,
+    RCCL panel broadcast) and 16384^2 fp32 ring matmul (B all-gather
+    overlapped with MFMA compute)."""
+    out = {}
+    try:
+        from gelim.parallel import DistributedGauss, ring_matmul
+
+        n = 8192
+        dg = DistributedGauss(comm, n, block=64)
+        for it in range(2):
+            loc = dg.generate_random(seed=99)
+            torch.cuda.synchronize()
+            comm.barrier()
+            t0 = time.perf_counter()
+            x = dg.solve_(loc)
+            torch.cuda.synchronize()
+            comm.barrier()
+            dt = time.perf_counter() - t0
+        out["dist_gauss_8192"] = {"time_s": dt, "error": gelim.ops.gauss.error_metric(x)}
+        M = K = Nn = 16384
+        P = comm.world_size
+        Aloc = torch.randn(M // P, K, device=comm.device)
+        Bloc = torch.randn(K // P, Nn, device=comm.device)
+        for it in range(2):
+            torch.cuda.synchronize()
+            comm.barrier()
+            t0 = time.perf_counter()
+            ring_matmul(comm, Aloc, Bloc)
+            torch.cuda.synchronize()
+            comm.barrier()
+            dt = time.perf_counter() - t0
+        out["dist_matmul_16384"] = {"time_s": dt, "tflops_total": 2 * M * K * Nn / dt * 1e-12}
+    except Exception as e:  # report, never kill the headline line
+        out["error"] = repr(e)
+    return out
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,116 @@
+// Back substitution U x = y on the GPU (the reference's solveGauss,
+// Pthreads/Version-1/gauss_internal_input.c:212-227, which is a serial O(n^2)
+// loop there).
+//
+// Blocked right-to-left: for each 64-row diagonal block (bottom-up)
+//   diag kernel   : one wave64 solves the 64x64 triangle, the block staged in
+//                   LDS, x_i broadcast across lanes with a shuffle;
+//   update kernel : y[0:i0] -= U[0:i0, blk] x_blk, one wave per row,
+//                   coalesced 512-byte row segments + shuffle reduction.
+// A leading copy kernel gathers y (a strided column of the augmented matrix)
+// into a contiguous work vector and optionally emits the reference's
+// transformed B = y_i / U_ii (printed by VERIFY, P1i:292-295).
+#include <hip/hip_runtime.h>
+
+#include "device_common.h"
+#include "gelim/internal.h"
+
+namespace gelim {
+namespace {
+
+constexpr int kBS = 64;
+
+template <typename T>
+__global__ void copy_y_kernel(const T* __restrict__ U, int64_t ldu, const T* __restrict__ y,
+                              int64_t incy, double* __restrict__ yw, double* __restrict__ bnorm,
+                              int n, int unit) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const double v = (double)y[(int64_t)i * incy];
+  yw[i] = v;
+  if (bnorm) bnorm[i] = unit ? v : v / (double)U[(int64_t)i * ldu + i];
+}
+
+template <typename T>
+__global__ __launch_bounds__(64) void diag_solve_kernel(const T* __restrict__ U, int64_t ldu,
+                                                        double* __restrict__ yw,
+                                                        double* __restrict__ x, int i0, int nb,
+                                                        int unit) {
+  __shared__ double s_U[kBS][kBS + 1];
+  const int l = threadIdx.x;
+  for (int r = 0; r < nb; ++r)
+    if (l < nb) s_U[r][l] = (double)U[(int64_t)(i0 + r) * ldu + i0 + l];
+  __syncthreads();
+  double yv = (l < nb) ? yw[i0 + l] : 0.0;
+  double xv = 0.0;
+  for (int i = nb - 1; i >= 0; --i) {
+    double xi = unit ? yv : yv / s_U[i][i];
+    xi = __shfl(xi, i, dev::kWave);
+    if (l == i) xv = xi;
+    if (l < i) yv -= s_U[l][i] * xi;
+  }
+  if (l < nb) x[i0 + l] = xv;
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void update_kernel(const T* __restrict__ U, int64_t ldu,
+                                                     double* __restrict__ yw,
+                                                     const double* __restrict__ x, int i0,
+                                                     int nb) {
+  const int lane = threadIdx.x & 63;
+  const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int nwaves = (gridDim.x * blockDim.x) >> 6;
+  const double xl = (lane < nb) ? x[i0 + lane] : 0.0;
+  for (int r = wave; r < i0; r += nwaves) {
+    double v = (lane < nb) ? (double)U[(int64_t)r * ldu + i0 + lane] * xl : 0.0;
+    v = dev::wave_sum(v);
+    if (lane == 0) yw[r] -= v;
+  }
+}
+
+template <typename T>
+int backsub_impl(const T* U, int64_t ldu, const T* y, int64_t incy, double* x, double* bnorm,
+                 int64_t n, int unit, double* yw, hipStream_t s) {
+  hipLaunchKernelGGL(copy_y_kernel<T>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, U, ldu,
+                     y, incy, yw, bnorm, (int)n, unit);
+  HIP_TRY(hipGetLastError());
+  for (int64_t i1 = n; i1 > 0; i1 -= kBS) {
+    const int64_t i0 = i1 > kBS ? i1 - kBS : 0;
+    const int nb = (int)(i1 - i0);
+    hipLaunchKernelGGL(diag_solve_kernel<T>, dim3(1), dim3(64), 0, s, U, ldu, yw, x, (int)i0, nb,
+                       unit);
+    HIP_TRY(hipGetLastError());
+    if (i0 > 0) {
+      const int blocks = (int)std::min<int64_t>((i0 + 3) / 4, 1024);
+      hipLaunchKernelGGL(update_kernel<T>, dim3(blocks), dim3(256), 0, s, U, ldu, yw, x,
+                         (int)i0, nb);
+      HIP_TRY(hipGetLastError());
+    }
+  }
+  return GELIM_OK;
+}
+
+}  // namespace
+
+int backsub_f64(const double* U, int64_t ldu, const double* y, int64_t incy, double* x,
+                double* bnorm, int64_t n, int unit, double* yw, hipStream_t s) {
+  return backsub_impl<double>(U, ldu, y, incy, x, bnorm, n, unit, yw, s);
+}
+
+int backsub_f32(const float* U, int64_t ldu, const float* y, int64_t incy, double* x,
+                double* bnorm, int64_t n, int unit, double* yw, hipStream_t s) {
+  return backsub_impl<float>(U, ldu, y, incy, x, bnorm, n, unit, yw, s);
+}
+
+}  // namespace gelim
+
+extern "C" int gelim_gpu_backsub(const double* dU, int64_t ldu, const double* dy, int64_t incy,
+                                 double* dx, double* dbnorm, int64_t n, int unit, void* stream) {
+  if (n <= 0) return GELIM_FAIL(GELIM_E_ARG, "backsub: n <= 0");
+  hipStream_t s = (hipStream_t)stream;
+  double* yw = nullptr;
+  HIP_TRY(hipMallocAsync((void**)&yw, sizeof(double) * n, s));
+  int rc = gelim::backsub_f64(dU, ldu, dy, incy, dx, dbnorm, n, unit, yw, s);
+  HIP_TRY(hipFreeAsync(yw, s));
+  return rc;
+}

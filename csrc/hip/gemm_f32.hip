@@ -1,0 +1,230 @@
+// fp32 matrix multiply C = A * B on MI355X (row-major, C is M x N).
+//
+//  NAIVE_ROW  (K1 parity, CUDA_and_OpenMP/Version-1/cuda_matmul.cu:89-103):
+//             one workgroup per output row, threads stride the columns.
+//  NAIVE_ELEM (K2 parity, CUDA_and_OpenMP/Version-2/cuda_matmul.cu:89-101):
+//             2-D grid, one thread per output element.
+//  MFMA       (K3', absent in the reference): 128x128x16 LDS-tiled GEMM on
+//             the exact-fp32 matrix cores (v_mfma_f32_32x32x2_f32), LDS
+//             double-buffered with one barrier per K-step, XCD-aware tile
+//             order.  4 wave64s per workgroup in a 2x2 arrangement, each wave
+//             owns a 64x64 sub-tile = 2x2 MFMA blocks (64 accumulator VGPRs).
+//             LDS holds A transposed ([k][m]) and B as is ([k][n]) so both
+//             fragment reads are unit-stride across lanes (conflict-free).
+// The naive kernels use 64-bit indexing (the reference's int products
+// overflow for n > 46340).
+#include <hip/hip_runtime.h>
+
+#include "device_common.h"
+#include "gelim/internal.h"
+
+namespace gelim {
+namespace {
+
+struct Mat {
+  const float* A;
+  int64_t lda;
+  const float* B;
+  int64_t ldb;
+  float* C;
+  int64_t ldc;
+  int M, N, K, acc;
+};
+
+__global__ void naive_row_kernel(Mat p) {
+  const int64_t i = blockIdx.x;
+  for (int64_t j = threadIdx.x; j < p.N; j += blockDim.x) {
+    float temp = 0.0f;
+    for (int64_t k = 0; k < p.K; ++k) temp += p.A[i * p.lda + k] * p.B[k * p.ldb + j];
+    float* c = p.C + i * p.ldc + j;
+    *c = p.acc ? *c + temp : temp;
+  }
+}
+
+__global__ void naive_elem_kernel(Mat p) {
+  const int64_t j = threadIdx.x + (int64_t)blockIdx.y * blockDim.x;
+  const int64_t i = blockIdx.x;
+  if (j >= p.N) return;
+  float temp = 0.0f;
+  for (int64_t k = 0, kn = 0; k < p.K; ++k, kn += p.ldb) temp += p.A[i * p.lda + k] * p.B[j + kn];
+  float* c = p.C + i * p.ldc + j;
+  *c = p.acc ? *c + temp : temp;
+}
+
+constexpr int BM = 128, BN = 128, BK = 16;
+constexpr int kMmThreads = 256;
+constexpr int APAD = 4, BPAD = 4;
+
+struct Frag {
+  float4 a[2];  // A tile: 2 float4 per thread (128 rows x 16 k)
+  float4 b[2];  // B tile: 2 float4 per thread (16 k x 128 cols)
+};
+
+template <bool CHECK>
+__device__ __forceinline__ void load_tiles(Frag& f, const Mat& p, int m0, int n0, int k0) {
+  const float* __restrict__ A = p.A;
+  const float* __restrict__ B = p.B;
+  const int M = p.M, N = p.N, K = p.K;
+  const int64_t lda = p.lda, ldb = p.ldb;
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int row = (t >> 2) + 64 * h, kc = (t & 3) * 4;
+    const int gm = m0 + row, gk = k0 + kc;
+    if (!CHECK) {
+      f.a[h] = *reinterpret_cast<const float4*>(A + (int64_t)gm * lda + gk);
+    } else {
+      float v[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = (gm < M && gk + e < K) ? A[(int64_t)gm * lda + gk + e] : 0.f;
+      f.a[h] = make_float4(v[0], v[1], v[2], v[3]);
+    }
+    const int kr = (t >> 5) + 8 * h, nc = (t & 31) * 4;
+    const int gkb = k0 + kr, gn = n0 + nc;
+    if (!CHECK) {
+      f.b[h] = *reinterpret_cast<const float4*>(B + (int64_t)gkb * ldb + gn);
+    } else {
+      float v[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = (gkb < K && gn + e < N) ? B[(int64_t)gkb * ldb + gn + e] : 0.f;
+      f.b[h] = make_float4(v[0], v[1], v[2], v[3]);
+    }
+  }
+}
+
+__device__ __forceinline__ void store_tiles(const Frag& f, float (*As)[BM + APAD],
+                                            float (*Bs)[BN + BPAD]) {
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int row = (t >> 2) + 64 * h, kc = (t & 3) * 4;
+    As[kc + 0][row] = f.a[h].x;
+    As[kc + 1][row] = f.a[h].y;
+    As[kc + 2][row] = f.a[h].z;
+    As[kc + 3][row] = f.a[h].w;
+    const int kr = (t >> 5) + 8 * h, nc = (t & 31) * 4;
+    *reinterpret_cast<float4*>(&Bs[kr][nc]) = f.b[h];
+  }
+}
+
+template <bool CHECK>
+__global__ __launch_bounds__(kMmThreads) void mfma_gemm_kernel(Mat p, int tiles_n, int ntiles) {
+  const int M = p.M, N = p.N, K = p.K;
+  __shared__ __attribute__((aligned(16))) float As[2][BK][BM + APAD];
+  __shared__ __attribute__((aligned(16))) float Bs[2][BK][BN + BPAD];
+
+  // XCD-aware bijective remap: consecutive tiles (sharing A row panels) go to
+  // the same XCD's L2 (cdna_hip_programming.md §5.5 T1).
+  const int orig = blockIdx.x;
+  const int q = ntiles / 8, rem = ntiles % 8, xcd = orig % 8;
+  const int tile = (xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q) + orig / 8;
+  const int m0 = (tile / tiles_n) * BM, n0 = (tile % tiles_n) * BN;
+
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
+  const int l31 = lane & 31, kh = lane >> 5;
+
+  dev::f16x acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  Frag f;
+  load_tiles<CHECK>(f, p, m0, n0, 0);
+  store_tiles(f, As[0], Bs[0]);
+  __syncthreads();
+
+  const int nk = (K + BK - 1) / BK;
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) load_tiles<CHECK>(f, p, m0, n0, (kt + 1) * BK);
+#pragma unroll
+    for (int k = 0; k < BK; k += 2) {
+      const int kk = k + kh;
+      float a0 = As[cur][kk][wm + l31];
+      float a1 = As[cur][kk][wm + 32 + l31];
+      float b0 = Bs[cur][kk][wn + l31];
+      float b1 = Bs[cur][kk][wn + 32 + l31];
+      acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
+      acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
+      acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
+      acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
+    }
+    if (kt + 1 < nk) store_tiles(f, As[cur ^ 1], Bs[cur ^ 1]);
+    __syncthreads();
+  }
+
+  // epilogue: C/D map of 32x32 f32 MFMA: col = l&31, row = (r&3) + 8(r>>2) + 4(l>>5)
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int col = n0 + wn + 32 * j + l31;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = m0 + wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * kh;
+        if (!CHECK || (row < M && col < N)) {
+          float* c = p.C + (int64_t)row * p.ldc + col;
+          *c = p.acc ? *c + acc[i][j][r] : acc[i][j][r];
+        }
+      }
+    }
+}
+
+}  // namespace
+
+int matmul_f32(const float* A, int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc,
+               int64_t M, int64_t N, int64_t K, int accumulate, int kernel, hipStream_t s) {
+  if (M <= 0 || N <= 0 || K <= 0) return GELIM_FAIL(GELIM_E_ARG, "matmul: bad shape");
+  if (M > INT32_MAX || N > INT32_MAX || K > INT32_MAX)
+    return GELIM_FAIL(GELIM_E_ARG, "matmul: dimension exceeds 2^31");
+  if (lda < K || ldb < N || ldc < N) return GELIM_FAIL(GELIM_E_ARG, "matmul: leading dimension too small");
+  Mat p{A, lda, B, ldb, C, ldc, (int)M, (int)N, (int)K, accumulate};
+  switch (kernel) {
+    case GELIM_MM_NAIVE_ROW: {
+      const int threads = (int)std::min<int64_t>(1024, N);
+      hipLaunchKernelGGL(naive_row_kernel, dim3((unsigned)M), dim3(threads), 0, s, p);
+      break;
+    }
+    case GELIM_MM_NAIVE_ELEM: {
+      const int threads = (int)std::min<int64_t>(1024, N);
+      dim3 grid((unsigned)M, (unsigned)((N + 1023) / 1024));
+      hipLaunchKernelGGL(naive_elem_kernel, grid, dim3(threads), 0, s, p);
+      break;
+    }
+    case GELIM_MM_MFMA: {
+      const int tiles_m = (int)((M + BM - 1) / BM), tiles_n = (int)((N + BN - 1) / BN);
+      const int ntiles = tiles_m * tiles_n;
+      const bool aligned = (M % BM == 0) && (N % BN == 0) && (K % BK == 0) && (lda % 4 == 0) &&
+                           (ldb % 4 == 0) && ((uintptr_t)A % 16 == 0) && ((uintptr_t)B % 16 == 0);
+      if (aligned)
+        hipLaunchKernelGGL(mfma_gemm_kernel<false>, dim3(ntiles), dim3(kMmThreads), 0, s, p,
+                           tiles_n, ntiles);
+      else
+        hipLaunchKernelGGL(mfma_gemm_kernel<true>, dim3(ntiles), dim3(kMmThreads), 0, s, p,
+                           tiles_n, ntiles);
+      break;
+    }
+    default:
+      return GELIM_FAIL(GELIM_E_ARG, "matmul: unknown kernel");
+  }
+  HIP_TRY(hipGetLastError());
+  return GELIM_OK;
+}
+
+}  // namespace gelim
+
+extern "C" int gelim_gpu_matmul_f32(const float* dA, const float* dB, float* dC, int64_t M,
+                                    int64_t N, int64_t K, int kernel, void* stream) {
+  return gelim::matmul_f32(dA, K, dB, N, dC, N, M, N, K, 0, kernel, (hipStream_t)stream);
+}
+
+extern "C" int gelim_gpu_matmul_f32_ex(const float* dA, int64_t lda, const float* dB, int64_t ldb,
+                                       float* dC, int64_t ldc, int64_t M, int64_t N, int64_t K,
+                                       int accumulate, int kernel, void* stream) {
+  return gelim::matmul_f32(dA, lda, dB, ldb, dC, ldc, M, N, K, accumulate, kernel,
+                           (hipStream_t)stream);
+}

@@ -1,0 +1,191 @@
+// Gauss solver plan: owns the device working system and orchestrates the
+// kernels of one solve, captured once into a hipGraph and replayed.
+//
+// Why a graph: the per-pivot algorithm is 2n dependent launches and the
+// blocked one ~3n/w; issued eagerly each launch costs ~3-4 us of host time
+// (MI355X_MICROARCH.md price list, graph-replay-floor), so the solve would be
+// host-bound.  Captured, each boundary costs ~1.5 us on the device only.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <string>
+
+#include "gelim/internal.h"
+
+namespace gelim {
+int64_t panel_width_for(int64_t m);
+int panel_factor(double* P, int64_t ldp, int64_t m, int64_t w, int64_t row0, int mode, int* piv,
+                 int* info, hipStream_t s);
+int swap_trsm(double* C, int64_t ldc, int64_t ncols, const double* L, int64_t ldl, int64_t w,
+              const int* piv, double* tmp, hipStream_t s);
+int gemm_update(double* C, int64_t ldc, const double* L, int64_t ldl, const double* U,
+                int64_t ldu, int64_t M, int64_t N, int64_t K, hipStream_t s);
+int backsub_f64(const double* U, int64_t ldu, const double* y, int64_t incy, double* x,
+                double* bnorm, int64_t n, int unit, double* yw, hipStream_t s);
+int backsub_f32(const float* U, int64_t ldu, const float* y, int64_t incy, double* x,
+                double* bnorm, int64_t n, int unit, double* yw, hipStream_t s);
+template <typename T>
+int pivot_elimination(T* A, int64_t lda, int64_t n, int mode, T* mcol, int* info,
+                      hipStream_t s);
+}  // namespace gelim
+
+struct gelim_gauss_plan {
+  int64_t n = 0, lda = 0;
+  int algo = 0, pivot = 0, eb = 8;
+  bool use_graph = true;
+  void* work = nullptr;
+  int* piv = nullptr;
+  int* info = nullptr;
+  double* yw = nullptr;
+  void* mcol = nullptr;
+  double* tmp = nullptr;
+  hipStream_t cap = nullptr;
+  hipGraphExec_t exec = nullptr;
+  const void* k_src = nullptr;
+  int64_t k_ld = 0;
+  void* k_dx = nullptr;
+  void* k_bn = nullptr;
+};
+
+namespace {
+
+int enqueue(gelim_gauss_plan* p, const void* src, int64_t src_ld, void* dx, void* bnorm,
+            hipStream_t s) {
+  using namespace gelim;
+  const int64_t n = p->n, lda = p->lda;
+  if (src)
+    HIP_TRY(hipMemcpy2DAsync(p->work, lda * p->eb, src, src_ld * p->eb, (n + 1) * p->eb, n,
+                             hipMemcpyDeviceToDevice, s));
+  HIP_TRY(hipMemsetAsync(p->info, 0, 16, s));
+  if (p->algo == GELIM_GPU_BLOCKED) {
+    double* A = static_cast<double*>(p->work);
+    for (int64_t k = 0; k < n;) {
+      const int64_t m = n - k;
+      const int64_t w = std::min<int64_t>(panel_width_for(m), m);
+      if (w <= 0) return GELIM_FAIL(GELIM_E_ARG, "matrix too tall for the register panel");
+      GELIM_TRY(panel_factor(A + k * lda + k, lda, m, w, k, p->pivot, p->piv + k, p->info, s));
+      const int64_t ncols = (n + 1) - (k + w);
+      GELIM_TRY(swap_trsm(A + k * lda + k + w, lda, ncols, A + k * lda + k, lda, w, p->piv + k,
+                          p->tmp, s));
+      if (m > w)
+        GELIM_TRY(gemm_update(A + (k + w) * lda + (k + w), lda, A + (k + w) * lda + k, lda,
+                              A + k * lda + k + w, lda, m - w, ncols, w, s));
+      k += w;
+    }
+    return backsub_f64(A, lda, A + n, lda, static_cast<double*>(dx),
+                       static_cast<double*>(bnorm), n, 0, p->yw, s);
+  }
+  if (p->eb == 8) {
+    double* A = static_cast<double*>(p->work);
+    GELIM_TRY(pivot_elimination<double>(A, lda, n, p->pivot, static_cast<double*>(p->mcol),
+                                        p->info, s));
+    return backsub_f64(A, lda, A + n, lda, static_cast<double*>(dx),
+                       static_cast<double*>(bnorm), n, 1, p->yw, s);
+  }
+  float* A = static_cast<float*>(p->work);
+  GELIM_TRY(pivot_elimination<float>(A, lda, n, p->pivot, static_cast<float*>(p->mcol), p->info,
+                                     s));
+  return backsub_f32(A, lda, A + n, lda, static_cast<double*>(dx), static_cast<double*>(bnorm), n,
+                     1, p->yw, s);
+}
+
+}  // namespace
+
+extern "C" gelim_gauss_plan* gelim_gauss_plan_create(int64_t n, int algo, int pivot,
+                                                     int dtype_bytes, int use_graph) {
+  if (n <= 0 || (dtype_bytes != 4 && dtype_bytes != 8) ||
+      (algo != GELIM_GPU_BLOCKED && algo != GELIM_GPU_PIVOT) ||
+      (pivot != GELIM_PIVOT_ZERO && pivot != GELIM_PIVOT_PARTIAL)) {
+    GELIM_FAIL(GELIM_E_ARG, "plan_create: bad arguments");
+    return nullptr;
+  }
+  if (algo == GELIM_GPU_BLOCKED && dtype_bytes != 8) {
+    GELIM_FAIL(GELIM_E_ARG, "blocked LU is fp64 only (fp32 fails saylr4/orsreg_1, SURVEY §4.3)");
+    return nullptr;
+  }
+  if (algo == GELIM_GPU_BLOCKED && gelim::panel_width_for(n) <= 0) {
+    GELIM_FAIL(GELIM_E_ARG, "blocked LU: n > 16384 not supported on one GPU yet");
+    return nullptr;
+  }
+  auto* p = new gelim_gauss_plan;
+  p->n = n;
+  p->algo = algo;
+  p->pivot = pivot;
+  p->eb = dtype_bytes;
+  p->use_graph = use_graph != 0;
+  const int64_t align = 64 / dtype_bytes;  // 64-byte rows
+  p->lda = (n + 1 + align - 1) / align * align;
+  auto fail = [&](const char* what) -> gelim_gauss_plan* {
+    GELIM_FAIL(GELIM_E_NOMEM, std::string("plan_create: ") + what);
+    gelim_gauss_plan_destroy(p);
+    return nullptr;
+  };
+  if (hipMalloc(&p->work, (size_t)(n * p->lda * dtype_bytes)) != hipSuccess) return fail("work");
+  if (hipMalloc((void**)&p->piv, (size_t)(n + 64) * sizeof(int)) != hipSuccess) return fail("piv");
+  if (hipMalloc((void**)&p->info, 16) != hipSuccess) return fail("info");
+  if (hipMalloc((void**)&p->yw, (size_t)n * sizeof(double)) != hipSuccess) return fail("yw");
+  if (hipMalloc(&p->mcol, (size_t)n * dtype_bytes) != hipSuccess) return fail("mcol");
+  if (hipMalloc((void**)&p->tmp, (size_t)2 * 32 * (n + 1) * sizeof(double)) != hipSuccess)
+    return fail("tmp");
+  if (hipStreamCreateWithFlags(&p->cap, hipStreamNonBlocking) != hipSuccess) return fail("stream");
+  (void)hipMemset(p->work, 0, (size_t)(n * p->lda * dtype_bytes));
+  return p;
+}
+
+extern "C" void gelim_gauss_plan_destroy(gelim_gauss_plan* p) {
+  if (!p) return;
+  if (p->exec) (void)hipGraphExecDestroy(p->exec);
+  if (p->cap) (void)hipStreamDestroy(p->cap);
+  (void)hipFree(p->work);
+  (void)hipFree(p->piv);
+  (void)hipFree(p->info);
+  (void)hipFree(p->yw);
+  (void)hipFree(p->mcol);
+  (void)hipFree(p->tmp);
+  delete p;
+}
+
+extern "C" int64_t gelim_gauss_plan_lda(const gelim_gauss_plan* p) { return p ? p->lda : 0; }
+extern "C" void* gelim_gauss_plan_work(gelim_gauss_plan* p) { return p ? p->work : nullptr; }
+
+extern "C" int gelim_gauss_plan_solve(gelim_gauss_plan* p, const void* src, int64_t src_ld,
+                                      void* dx, void* bnorm, void* stream) {
+  if (!p || !dx) return GELIM_FAIL(GELIM_E_ARG, "plan_solve: null plan or x");
+  if (src && src_ld < p->n + 1) return GELIM_FAIL(GELIM_E_ARG, "plan_solve: src_ld < n+1");
+  hipStream_t s = (hipStream_t)stream;
+  if (!p->use_graph) return enqueue(p, src, src_ld, dx, bnorm, s);
+  const bool hit = p->exec && p->k_src == src && p->k_ld == src_ld && p->k_dx == dx &&
+                   p->k_bn == bnorm;
+  if (!hit) {
+    if (p->exec) {
+      HIP_TRY(hipGraphExecDestroy(p->exec));
+      p->exec = nullptr;
+    }
+    hipGraph_t g = nullptr;
+    HIP_TRY(hipStreamBeginCapture(p->cap, hipStreamCaptureModeThreadLocal));
+    int rc = enqueue(p, src, src_ld, dx, bnorm, p->cap);
+    hipError_t e = hipStreamEndCapture(p->cap, &g);
+    if (rc != 0) {
+      if (g) (void)hipGraphDestroy(g);
+      return rc;
+    }
+    HIP_TRY(e);
+    e = hipGraphInstantiate(&p->exec, g, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(g);
+    HIP_TRY(e);
+    p->k_src = src;
+    p->k_ld = src_ld;
+    p->k_dx = dx;
+    p->k_bn = bnorm;
+  }
+  HIP_TRY(hipGraphLaunch(p->exec, s));
+  return GELIM_OK;
+}
+
+extern "C" int gelim_gauss_plan_info(gelim_gauss_plan* p, void* stream) {
+  if (!p) return GELIM_FAIL(GELIM_E_ARG, "plan_info: null plan");
+  int h[4] = {0, 0, 0, 0};
+  HIP_TRY(hipMemcpyAsync(h, p->info, 16, hipMemcpyDeviceToHost, (hipStream_t)stream));
+  HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
+  return h[0];
+}

@@ -1,0 +1,173 @@
+// GPU runtime surface of the C ABI (device selection, buffers, copies) and
+// the device-side initialisers / error metric (L1/L2 on the GPU).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+
+#include "device_common.h"
+#include "gelim/internal.h"
+#include "gelim/rng.h"
+
+namespace gelim {
+namespace {
+
+template <typename T>
+__global__ void init_synthetic_kernel(T* __restrict__ A, int64_t lda, int n) {
+  // A[i][j] = 2*min(i+1, j+1), b[i] = i in column n (P1i:59-69)
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  const int i = blockIdx.y;
+  if (j > n) return;
+  T v = (j == n) ? (T)i : (T)(2 * ((j < i) ? (j + 1) : (i + 1)));
+  A[(int64_t)i * lda + j] = v;
+}
+
+__global__ void init_random_kernel(double* __restrict__ A, int64_t lda, int64_t row0, int64_t col0,
+                                   int ncols, uint64_t seed) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  const int i = blockIdx.y;
+  if (j >= ncols) return;
+  A[(int64_t)i * lda + j] = rng_uniform_pm1(seed, row0 + i, col0 + j);
+}
+
+// R[i] = sum_j A[i][j] * (j+1): one wave per row, result in column n.
+template <typename T>
+__global__ __launch_bounds__(256) void init_rhs_kernel(T* __restrict__ A, int64_t lda, int n) {
+  const int lane = threadIdx.x & 63;
+  const int row = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  if (row >= n) return;
+  const T* a = A + (int64_t)row * lda;
+  double acc = 0.0;
+  for (int j = lane; j < n; j += 64) acc += (double)a[j] * (double)(j + 1);
+  acc = dev::wave_sum(acc);
+  if (lane == 0) A[(int64_t)row * lda + n] = (T)acc;
+}
+
+__global__ __launch_bounds__(1024) void error_kernel(const double* __restrict__ x, int n,
+                                                     double* __restrict__ out) {
+  __shared__ double s[16];
+  double e = 0.0;
+  for (int i = threadIdx.x; i < n; i += 1024) {
+    const double ref = (double)(i + 1);
+    double v = fabs((x[i] - ref) / ref);
+    e = (v > e || v != v) ? v : e;  // NaN propagates
+  }
+  // NaN-propagating max
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    double o = __shfl_xor(e, off, 64);
+    e = (o > e || o != o) ? o : e;
+  }
+  if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = e;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double m = 0.0;
+    for (int w = 0; w < 16; ++w) m = (s[w] > m || s[w] != s[w]) ? s[w] : m;
+    *out = m;
+  }
+}
+
+}  // namespace
+
+int init_synthetic_f64(double* A, int64_t lda, int64_t n, hipStream_t s) {
+  dim3 grid((unsigned)((n + 1 + 255) / 256), (unsigned)n);
+  hipLaunchKernelGGL(init_synthetic_kernel<double>, grid, dim3(256), 0, s, A, lda, (int)n);
+  HIP_TRY(hipGetLastError());
+  return GELIM_OK;
+}
+
+int init_synthetic_f32(float* A, int64_t lda, int64_t n, hipStream_t s) {
+  dim3 grid((unsigned)((n + 1 + 255) / 256), (unsigned)n);
+  hipLaunchKernelGGL(init_synthetic_kernel<float>, grid, dim3(256), 0, s, A, lda, (int)n);
+  HIP_TRY(hipGetLastError());
+  return GELIM_OK;
+}
+
+}  // namespace gelim
+
+extern "C" int gelim_gpu_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+extern "C" int gelim_gpu_set_device(int dev) {
+  HIP_TRY(hipSetDevice(dev));
+  return GELIM_OK;
+}
+
+extern "C" int gelim_gpu_sync(void* stream) {
+  HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
+  return GELIM_OK;
+}
+
+extern "C" void* gelim_gpu_malloc(int64_t bytes) {
+  void* p = nullptr;
+  hipError_t e = hipMalloc(&p, (size_t)bytes);
+  if (e != hipSuccess) {
+    GELIM_FAIL(GELIM_E_NOMEM, std::string("hipMalloc: ") + hipGetErrorString(e));
+    return nullptr;
+  }
+  return p;
+}
+
+extern "C" int gelim_gpu_free(void* p) {
+  HIP_TRY(hipFree(p));
+  return GELIM_OK;
+}
+
+extern "C" int gelim_gpu_memcpy_h2d(void* dst, const void* src, int64_t bytes, void* stream) {
+  HIP_TRY(hipMemcpyAsync(dst, src, (size_t)bytes, hipMemcpyHostToDevice, (hipStream_t)stream));
+  return GELIM_OK;
+}
+
+extern "C" int gelim_gpu_memcpy_d2h(void* dst, const void* src, int64_t bytes, void* stream) {
+  HIP_TRY(hipMemcpyAsync(dst, src, (size_t)bytes, hipMemcpyDeviceToHost, (hipStream_t)stream));
+  return GELIM_OK;
+}
+
+extern "C" int gelim_gpu_init_synthetic(double* dA, int64_t lda, int64_t n, void* stream) {
+  if (n <= 0 || lda < n + 1) return GELIM_FAIL(GELIM_E_ARG, "init_synthetic: lda < n+1");
+  return gelim::init_synthetic_f64(dA, lda, n, (hipStream_t)stream);
+}
+
+extern "C" int gelim_gpu_init_synthetic_f32(float* dA, int64_t lda, int64_t n, void* stream) {
+  if (n <= 0 || lda < n + 1) return GELIM_FAIL(GELIM_E_ARG, "init_synthetic: lda < n+1");
+  return gelim::init_synthetic_f32(dA, lda, n, (hipStream_t)stream);
+}
+
+extern "C" int gelim_gpu_init_random(double* dA, int64_t lda, int64_t n, uint64_t seed,
+                                     void* stream) {
+  if (n <= 0 || lda < n) return GELIM_FAIL(GELIM_E_ARG, "init_random: lda < n");
+  return gelim_gpu_init_random_block(dA, lda, 0, n, 0, n, seed, stream);
+}
+
+extern "C" int gelim_gpu_init_random_block(double* dA, int64_t lda, int64_t row0, int64_t nrows,
+                                           int64_t col0, int64_t ncols, uint64_t seed,
+                                           void* stream) {
+  if (nrows <= 0 || ncols <= 0) return GELIM_OK;
+  if (lda < ncols) return GELIM_FAIL(GELIM_E_ARG, "init_random_block: lda < ncols");
+  for (int64_t r = 0; r < nrows; r += 65535) {  // grid.y limit
+    const int64_t rows = std::min<int64_t>(65535, nrows - r);
+    dim3 grid((unsigned)((ncols + 255) / 256), (unsigned)rows);
+    hipLaunchKernelGGL(gelim::init_random_kernel, grid, dim3(256), 0, (hipStream_t)stream,
+                       dA + r * lda, lda, row0 + r, col0, (int)ncols, seed);
+    HIP_TRY(hipGetLastError());
+  }
+  return GELIM_OK;
+}
+
+extern "C" int gelim_gpu_init_rhs(double* dA, int64_t lda, int64_t n, void* stream) {
+  if (n <= 0 || lda < n + 1) return GELIM_FAIL(GELIM_E_ARG, "init_rhs: lda < n+1");
+  const unsigned blocks = (unsigned)((n * 64 + 255) / 256);
+  hipLaunchKernelGGL(gelim::init_rhs_kernel<double>, dim3(blocks), dim3(256), 0,
+                     (hipStream_t)stream, dA, lda, (int)n);
+  HIP_TRY(hipGetLastError());
+  return GELIM_OK;
+}
+
+extern "C" int gelim_gpu_error_metric(const double* dx, int64_t n, double* d_err, void* stream) {
+  hipLaunchKernelGGL(gelim::error_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, dx,
+                     (int)n, d_err);
+  HIP_TRY(hipGetLastError());
+  return GELIM_OK;
+}

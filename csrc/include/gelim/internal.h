@@ -1,0 +1,35 @@
+// Internal helpers shared by the host-side C++ and HIP translation units.
+#pragma once
+
+#include <cstdint>
+#include <cstdio>
+#include <string>
+
+#include "gelim/gelim.h"
+
+namespace gelim {
+
+// Thread-local error message behind gelim_last_error().
+void set_error(const std::string& msg);
+int fail(int code, const char* file, int line, const std::string& msg);
+
+}  // namespace gelim
+
+#define GELIM_FAIL(code, msg) ::gelim::fail((code), __FILE__, __LINE__, (msg))
+
+// Check a hipError_t; on failure record "file:line: hipGetErrorString" and
+// return GELIM_E_HIP from the enclosing function (every HIP
+// return code is checked — the reference never checks cudaError_t).
+#define HIP_TRY(expr)                                                        \
+  do {                                                                       \
+    hipError_t _e = (expr);                                                  \
+    if (_e != hipSuccess)                                                    \
+      return ::gelim::fail(GELIM_E_HIP, __FILE__, __LINE__,                  \
+                           std::string(#expr ": ") + hipGetErrorString(_e)); \
+  } while (0)
+
+#define GELIM_TRY(expr)      \
+  do {                       \
+    int _rc = (expr);        \
+    if (_rc != 0) return _rc; \
+  } while (0)

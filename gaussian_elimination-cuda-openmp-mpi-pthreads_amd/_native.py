@@ -1,0 +1,121 @@
+"""ctypes binding of libgelim.so (the C++/HIP core, ``csrc/``).
+
+The Python layer never re-implements numerics: every op goes through this
+library, CPU ops included.  Loading is strict — if the shared library is
+missing the import raises, so a GPU run can never silently fall back to an
+eager PyTorch path.  Build it with ``python __graft_entry__.py build`` (or
+``cmake -S csrc -B build -G Ninja && ninja -C build``).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from pathlib import Path
+
+_LIB_DIR = Path(__file__).resolve().parent / "lib"
+_LIB_PATH = _LIB_DIR / "libgelim.so"
+
+# error codes (gelim.h)
+OK, E_ARG, E_IO, E_HIP, E_SINGULAR, E_NOMEM, E_THREAD = 0, -1, -2, -3, -4, -5, -6
+PIVOT_ZERO, PIVOT_PARTIAL = 0, 1
+CPU_SEQ, CPU_OMP, CPU_PTH_V1, CPU_PTH_V2, CPU_PTH_V3 = 0, 1, 2, 3, 4
+GPU_BLOCKED, GPU_PIVOT = 0, 1
+MM_NAIVE_ROW, MM_NAIVE_ELEM, MM_MFMA = 0, 1, 2
+
+
+class GelimError(RuntimeError):
+    """A libgelim call failed; ``code`` is the GELIM_E_* value."""
+
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"[{code}] {msg}")
+        self.code = code
+
+
+class SingularMatrixError(GelimError):
+    """Zero pivot: the reference prints 'The matrix is singular' and exits."""
+
+
+_i64, _i32, _int, _dbl, _vp = C.c_int64, C.c_int32, C.c_int, C.c_double, C.c_void_p
+_u64 = C.c_uint64
+_PROTOS = {
+    "gelim_last_error": (C.c_char_p, []),
+    "gelim_version": (C.c_char_p, []),
+    "gelim_dat_size": (_i64, [C.c_char_p]),
+    "gelim_dat_read": (_int, [C.c_char_p, _vp, _i64, _i64]),
+    "gelim_matrix_gen": (_int, [_i64, C.c_char_p]),
+    "gelim_init_synthetic_f64": (None, [_vp, _i64, _vp, _i64]),
+    "gelim_init_random_f64": (None, [_vp, _i64, _i64, _u64]),
+    "gelim_init_rhs_f64": (None, [_vp, _i64, _vp, _i64]),
+    "gelim_error_metric": (_dbl, [_vp, _i64]),
+    "gelim_cpu_gauss": (_int, [_vp, _i64, _vp, _i64, _int, _int, _int, _int]),
+    "gelim_cpu_max_threads": (_int, []),
+    "gelim_cpu_backsub_unit": (None, [_vp, _i64, _vp, _vp, _i64]),
+    "gelim_cpu_matmul_f32": (None, [_vp, _vp, _vp, _i64, _int, _int]),
+    "gelim_init_matmul_f32": (None, [_vp, _vp, _i64]),
+    "gelim_cpu_panel_factor": (_int, [_vp, _i64, _i64, _i64, _i64, _int, _vp, _vp]),
+    "gelim_cpu_swap_trsm": (_int, [_vp, _i64, _i64, _vp, _i64, _i64, _vp, _i64, _i64]),
+    "gelim_cpu_gemm_update": (_int, [_vp, _i64, _vp, _i64, _vp, _i64, _i64, _i64, _i64]),
+    "gelim_gpu_device_count": (_int, []),
+    "gelim_gpu_set_device": (_int, [_int]),
+    "gelim_gpu_sync": (_int, [_vp]),
+    "gelim_gpu_init_synthetic": (_int, [_vp, _i64, _i64, _vp]),
+    "gelim_gpu_init_synthetic_f32": (_int, [_vp, _i64, _i64, _vp]),
+    "gelim_gpu_init_random": (_int, [_vp, _i64, _i64, _u64, _vp]),
+    "gelim_gpu_init_rhs": (_int, [_vp, _i64, _i64, _vp]),
+    "gelim_gpu_error_metric": (_int, [_vp, _i64, _vp, _vp]),
+    "gelim_gpu_panel_factor": (_int, [_vp, _i64, _i64, _i64, _i64, _int, _vp, _vp, _vp]),
+    "gelim_gpu_panel_max_rows": (_i64, [_i64]),
+    "gelim_gpu_swap_trsm": (_int, [_vp, _i64, _i64, _vp, _i64, _i64, _vp, _i64, _vp]),
+    "gelim_gpu_gemm_update": (_int, [_vp, _i64, _vp, _i64, _vp, _i64, _i64, _i64, _i64, _vp]),
+    "gelim_gpu_backsub": (_int, [_vp, _i64, _vp, _i64, _vp, _vp, _i64, _int, _vp]),
+    "gelim_gauss_plan_create": (_vp, [_i64, _int, _int, _int, _int]),
+    "gelim_gauss_plan_destroy": (None, [_vp]),
+    "gelim_gauss_plan_lda": (_i64, [_vp]),
+    "gelim_gauss_plan_work": (_vp, [_vp]),
+    "gelim_gauss_plan_solve": (_int, [_vp, _vp, _i64, _vp, _vp, _vp]),
+    "gelim_gauss_plan_info": (_int, [_vp, _vp]),
+    "gelim_gpu_matmul_f32": (_int, [_vp, _vp, _vp, _i64, _i64, _i64, _int, _vp]),
+}
+
+_lib: C.CDLL | None = None
+
+
+def library_path() -> Path:
+    return _LIB_PATH
+
+
+def lib() -> C.CDLL:
+    """Load libgelim.so once (raises ImportError with a build hint if absent)."""
+    global _lib
+    if _lib is None:
+        if not _LIB_PATH.exists():
+            raise ImportError(
+                f"libgelim.so not found at {_LIB_PATH}; build it with "
+                "`python __graft_entry__.py build` (cmake -S csrc -B build -G Ninja)"
+            )
+        handle = C.CDLL(os.fspath(_LIB_PATH), mode=C.RTLD_GLOBAL)
+        for name, (res, args) in _PROTOS.items():
+            fn = getattr(handle, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = handle
+    return _lib
+
+
+def last_error() -> str:
+    msg = lib().gelim_last_error()
+    return msg.decode() if msg else ""
+
+
+def check(rc: int, what: str = "") -> int:
+    """Raise on a negative libgelim return code."""
+    if rc is not None and rc < 0:
+        msg = f"{what}: {last_error()}" if what else last_error()
+        if rc == E_SINGULAR:
+            raise SingularMatrixError(rc, msg)
+        raise GelimError(rc, msg)
+    return rc
+
+
+def version() -> str:
+    return lib().gelim_version().decode()

@@ -1,0 +1,158 @@
+"""GaussSolver — the framework's Gaussian-elimination "model": one n x n
+system A x = b, solved by a selectable backend with reference semantics
+(forward elimination + back substitution).
+
+Backends
+  hip / hip-blocked : blocked right-looking LU with partial (or zero) pivoting,
+                      register-resident panel + fp64 MFMA trailing GEMM,
+                      the whole solve replayed from a captured hipGraph (fp64)
+  hip-pivot         : the reference per-pivot algorithm on the GPU
+                      (unit-diagonal elimination, fp64 or fp32)
+  seq / omp / pthreads-v1 / pthreads-v2 / pthreads-v3 : the reference CPU
+                      strategies (csrc/cpu/gauss_cpu.cpp), fp64
+
+Input is an augmented system `aug` (n rows, >= n+1 columns, b in column n),
+as produced by `ops.init.*_system`.  `solve` never modifies `aug`.
+"""
+from __future__ import annotations
+
+import torch
+
+from .. import _native
+from ..ops import gauss as cpu_ops
+from ..ops import lu
+from ..utils.tensors import ptr, row_major_ld, stream_handle
+
+GPU_BACKENDS = {"hip": _native.GPU_BLOCKED, "hip-blocked": _native.GPU_BLOCKED, "hip-pivot": _native.GPU_PIVOT}
+CPU_BACKENDS = tuple(cpu_ops.CPU_BACKENDS)
+BACKENDS = tuple(GPU_BACKENDS) + CPU_BACKENDS
+
+
+class GaussSolver:
+    def __init__(self, n: int, backend: str = "hip", pivot: str = "partial", dtype=torch.float64,
+                 device=None, use_graph: bool = True, threads: int = 0, affinity: bool = True):
+        if backend not in BACKENDS:
+            raise ValueError(f"unknown backend {backend!r}; choose from {BACKENDS}")
+        if pivot not in ("partial", "zero"):
+            raise ValueError("pivot must be 'partial' or 'zero'")
+        self.n, self.backend, self.pivot, self.dtype = n, backend, pivot, dtype
+        self.threads, self.affinity = threads, affinity
+        self._plan = None
+        self.gpu = backend in GPU_BACKENDS
+        if self.gpu:
+            self.device = torch.device(device if device is not None else "cuda")
+            if dtype == torch.float32 and backend != "hip-pivot":
+                raise ValueError("fp32 elimination is only offered by hip-pivot (fp64 is required for "
+                                 "partial-pivoting accuracy on the reference matrices)")
+            eb = 8 if dtype == torch.float64 else 4
+            with torch.cuda.device(self.device):
+                plan = _native.lib().gelim_gauss_plan_create(n, GPU_BACKENDS[backend], lu._pivot_code(pivot), eb,
+                                                             int(use_graph))
+            if not plan:
+                raise _native.GelimError(_native.E_ARG, _native.last_error())
+            self._plan = plan
+        else:
+            if dtype != torch.float64:
+                raise ValueError("CPU backends are fp64 (reference precision)")
+            self.device = torch.device("cpu")
+
+    # -- GPU ---------------------------------------------------------------
+    def _solve_gpu(self, aug: torch.Tensor, want_bnorm: bool):
+        n = self.n
+        if aug.device != self.device or aug.dtype != self.dtype:
+            aug = aug.to(self.device, self.dtype)
+        if aug.shape[0] != n or aug.shape[1] < n + 1 or aug.stride(1) != 1:
+            raise ValueError(f"aug must be a row-major (n, >=n+1) tensor, got {tuple(aug.shape)}")
+        x = torch.empty(n, dtype=torch.float64, device=self.device)
+        bn = torch.empty(n, dtype=torch.float64, device=self.device) if want_bnorm else None
+        rc = _native.lib().gelim_gauss_plan_solve(self._plan, ptr(aug), row_major_ld(aug), ptr(x), ptr(bn),
+                                                  stream_handle(self.device))
+        _native.check(rc, "gauss_plan_solve")
+        return x, bn
+
+    def info(self) -> int:
+        """0 if the last solve was non-singular, else 1 + first zero-pivot column."""
+        if not self.gpu:
+            return 0
+        return _native.check(_native.lib().gelim_gauss_plan_info(self._plan, stream_handle(self.device)),
+                             "plan_info")
+
+    # -- CPU ---------------------------------------------------------------
+    def _solve_cpu(self, aug: torch.Tensor, want_bnorm: bool):
+        n = self.n
+        A = aug[:, :n].to("cpu", torch.float64).contiguous().clone()
+        b = aug[:, n].to("cpu", torch.float64).contiguous().clone()
+        cpu_ops.cpu_gauss_(A, b, self.backend, self.pivot, self.threads, self.affinity)
+        x = cpu_ops.cpu_backsub_unit(A, b)
+        return x, (b if want_bnorm else None)
+
+    def solve(self, aug: torch.Tensor, return_bnorm: bool = False, check: bool = False):
+        """Solve the augmented system; returns x (and the reference's
+        transformed b when return_bnorm).  check=True synchronises and raises
+        SingularMatrixError on a zero pivot."""
+        if self.gpu:
+            x, bn = self._solve_gpu(aug, return_bnorm)
+            if check and self.info() != 0:
+                raise _native.SingularMatrixError(_native.E_SINGULAR,
+                                                  f"The matrix is singular (column {self.info() - 1})")
+        else:
+            x, bn = self._solve_cpu(aug, return_bnorm)
+        return (x, bn) if return_bnorm else x
+
+    __call__ = solve
+
+    def close(self) -> None:
+        if self._plan:
+            _native.lib().gelim_gauss_plan_destroy(self._plan)
+            self._plan = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __repr__(self):
+        return f"GaussSolver(n={self.n}, backend={self.backend!r}, pivot={self.pivot!r}, dtype={self.dtype})"
+
+
+def solve(aug: torch.Tensor, backend: str | None = None, pivot: str = "partial", **kw) -> torch.Tensor:
+    """One-shot solve of an augmented system (backend defaults to the GPU
+    blocked LU for CUDA tensors, the sequential reference loop otherwise)."""
+    if backend is None:
+        backend = "hip" if aug.device.type == "cuda" else "seq"
+    s = GaussSolver(aug.shape[0], backend=backend, pivot=pivot,
+                    device=aug.device if aug.device.type == "cuda" else None, **kw)
+    try:
+        return s.solve(aug, check=True)
+    finally:
+        s.close()
+
+
+def blocked_solve_(aug: torch.Tensor, pivot: str = "partial", width: int | None = None) -> torch.Tensor:
+    """The blocked LU of `plan.hip`, composed from `ops.lu` building blocks
+    (works on CPU and GPU tensors; used by tests and the distributed driver).
+    Destroys `aug`; returns x."""
+    n = aug.shape[0]
+    piv = torch.zeros(n + 64, dtype=torch.int32, device=aug.device)
+    info = torch.zeros(4, dtype=torch.int32, device=aug.device)
+    k = 0
+    while k < n:
+        m = n - k
+        w = width or _default_width(m)
+        w = min(w, m)
+        lu.panel_factor(aug[k:, k:k + w], piv[k:k + w], info, row0=k, pivot=pivot)
+        lu.swap_trsm(aug[k:, k + w:n + 1], aug[k:k + w, k:k + w], piv[k:k + w])
+        if m > w:
+            lu.gemm_update(aug[k + w:, k + w:n + 1], aug[k + w:, k:k + w], aug[k:k + w, k + w:n + 1])
+        k += w
+    if int(info[0].item()) != 0:
+        raise _native.SingularMatrixError(_native.E_SINGULAR, "The matrix is singular")
+    return lu.backsub(aug[:, :n], aug[:, n])
+
+
+def _default_width(m: int) -> int:
+    for w, rows in ((32, 1024), (16, 2048), (8, 4096), (4, 8192), (2, 16384)):
+        if m <= rows:
+            return w
+    raise ValueError("panel too tall")

@@ -1,0 +1,119 @@
+"""Communicator layer (L4 of SURVEY.md §1) — replaces the reference's MPI.
+
+One process per GPU, `torch.distributed` underneath: backend "nccl" is RCCL
+on ROCm (collectives over xGMI), "gloo" is the CPU transport used for tests
+and for CPU-only ranks.  The reference's MPI call sites map as
+(SURVEY.md §2.5):
+
+  MPI_Init/Comm_size/Comm_rank/Finalize  -> init_from_env / destroy
+  MPI_Bcast(pivot row)                    -> broadcast (one PANEL per call)
+  MPI_Send/Isend/Recv/Irecv row blocks    -> none: data stays resident,
+                                             owner-computes
+  MPI_Barrier                             -> barrier (stream-ordered otherwise)
+  (solution assembly)                     -> all_reduce / all_gather
+
+Rendezvous always uses 127.0.0.1 defaults (the container hostname may not
+resolve).
+"""
+from __future__ import annotations
+
+import datetime
+import os
+from dataclasses import dataclass
+
+import torch
+import torch.distributed as dist
+
+
+@dataclass
+class Communicator:
+    rank: int = 0
+    world_size: int = 1
+    device: torch.device = torch.device("cpu")
+    backend: str = "none"
+    group: object = None
+
+    # -- collectives ------------------------------------------------------
+    @property
+    def distributed(self) -> bool:
+        return self.world_size > 1
+
+    def broadcast(self, t: torch.Tensor, src: int) -> torch.Tensor:
+        if self.distributed:
+            dist.broadcast(t, src=self.global_rank(src), group=self.group)
+        return t
+
+    def all_reduce(self, t: torch.Tensor, op: str = "sum") -> torch.Tensor:
+        if self.distributed:
+            rop = {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN}[op]
+            dist.all_reduce(t, op=rop, group=self.group)
+        return t
+
+    def all_gather(self, out: torch.Tensor, t: torch.Tensor) -> torch.Tensor:
+        """out: (world_size * t.numel()) contiguous tensor."""
+        if self.distributed:
+            dist.all_gather_into_tensor(out, t.contiguous(), group=self.group)
+        else:
+            out.view(-1).copy_(t.reshape(-1))
+        return out
+
+    def barrier(self) -> None:
+        if self.distributed:
+            if self.backend == "nccl":
+                dist.barrier(group=self.group, device_ids=[self.device.index])
+            else:
+                dist.barrier(group=self.group)
+
+    def send(self, t: torch.Tensor, dst: int):
+        return dist.isend(t, dst=self.global_rank(dst), group=self.group)
+
+    def recv(self, t: torch.Tensor, src: int):
+        return dist.irecv(t, src=self.global_rank(src), group=self.group)
+
+    def global_rank(self, r: int) -> int:
+        if self.group is None:
+            return r
+        return dist.get_global_rank(self.group, r)
+
+    def subgroup(self, ranks: list[int]) -> "Communicator":
+        """Communicator over a subset of ranks (SUMMA rows/columns).  Must be
+        called by every rank with the same list (torch requirement)."""
+        g = dist.new_group(ranks=ranks, backend=self.backend if self.backend != "none" else None)
+        if self.rank not in ranks:
+            return Communicator(0, 1, self.device, self.backend, None)
+        return Communicator(ranks.index(self.rank), len(ranks), self.device, self.backend, g)
+
+
+def env_world() -> tuple[int, int, int]:
+    """(rank, world_size, local_rank) from the torchrun environment."""
+    return (int(os.environ.get("RANK", 0)), int(os.environ.get("WORLD_SIZE", 1)),
+            int(os.environ.get("LOCAL_RANK", 0)))
+
+
+def init_from_env(backend: str | None = None, device: str | None = None,
+                  timeout_s: float = 600.0) -> Communicator:
+    """Join the job described by RANK/WORLD_SIZE/LOCAL_RANK/MASTER_* (torchrun).
+    backend None -> "nccl" (RCCL) when a GPU is visible, else "gloo"."""
+    rank, world, local = env_world()
+    use_gpu = device != "cpu" and (device is not None or torch.cuda.is_available())
+    if use_gpu:
+        dev = torch.device(device) if device not in (None, "cuda") else torch.device("cuda", local)
+        torch.cuda.set_device(dev)
+    else:
+        dev = torch.device("cpu")
+    if world <= 1:
+        return Communicator(0, 1, dev, "none")
+    backend = backend or ("nccl" if use_gpu else "gloo")
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", "29511")
+    if not dist.is_initialized():
+        kw = dict(backend=backend, rank=rank, world_size=world, timeout=datetime.timedelta(seconds=timeout_s))
+        if backend == "nccl":
+            kw["device_id"] = dev
+        dist.init_process_group(**kw)
+    return Communicator(rank, world, dev, backend)
+
+
+def destroy() -> None:
+    if dist.is_initialized():
+        dist.destroy_process_group()

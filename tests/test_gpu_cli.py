@@ -1,0 +1,49 @@
+"""The native CLIs on the GPU."""
+import re
+
+import pytest
+
+from conftest import BIN, run_cli
+
+pytestmark = pytest.mark.gpu
+
+
+def test_internal_default_gpu(cuda):
+    r = run_cli(BIN / "gauss_internal_input", "-s", "2048", "--verify", "--json")
+    assert r.returncode == 0, r.stderr
+    lines = r.stdout.split("\n")
+    assert lines[1] == "Matrix Size: 2048 ; Threads: 32"
+    assert "Backend: hip-blocked" in r.stdout
+    assert re.search(r"Application time: \d+\.\d{6} Secs", r.stdout)
+    assert "0.00000 -0.50000" in r.stdout and "0.50000 0.50000" in r.stdout
+
+
+@pytest.mark.parametrize("extra", [["--backend=hip-pivot"], ["--backend=hip-pivot", "--dtype=f32"]])
+def test_internal_pivot_gpu(cuda, extra):
+    r = run_cli(BIN / "gauss_internal_input", "-s", "256", "--verify", *extra)
+    assert r.returncode == 0, r.stderr
+    assert "0.00000 -0.50000" in r.stdout
+
+
+def test_external_gpu(tmp_path, gelim, cuda):
+    n, rr, cc, vv = gelim.utils.io.load_coo_npz(gelim.utils.io.fixture_path("sherman3"))
+    p = tmp_path / "sherman3.dat"
+    gelim.utils.io.write_dat(p, rr, cc, vv, n)
+    r = run_cli(BIN / "gauss_external_input", p)
+    assert r.returncode == 0, r.stderr
+    m = re.search(r"Error: (\S+)", r.stdout)
+    assert m and float(m.group(1)) < 1e-11
+
+
+def test_hip_matmul_cli(cuda):
+    r = run_cli(BIN / "hip_matmul", "1024", "--no-seq", "--no-omp", "--verify")
+    assert r.returncode == 0, r.stderr
+    assert re.search(r"GPU Time: \S+", r.stdout) and "(PASS)" in r.stdout
+    for k in ("naive-row", "naive-elem"):
+        r = run_cli(BIN / "hip_matmul", "512", f"--kernel={k}", "--no-seq", "--no-omp", "--verify")
+        assert r.returncode == 0 and "(PASS)" in r.stdout
+
+
+def test_hip_matmul_usage():
+    r = run_cli(BIN / "hip_matmul")
+    assert r.stdout.startswith("Invalid number of arguments: usage")

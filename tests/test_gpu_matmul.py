@@ -1,0 +1,64 @@
+"""fp32 matmul kernels vs an fp64 torch reference."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _check(C, A, B, tol=2e-5):
+    ref = A.double() @ B.double()
+    scale = (A.double().abs() @ B.double().abs()).clamp_min(1e-30)
+    rel = ((C.double() - ref).abs() / scale).max().item()
+    assert rel < tol, rel
+
+
+@pytest.mark.parametrize("kernel", ["mfma", "naive-row", "naive-elem"])
+@pytest.mark.parametrize("M,N,K", [(128, 128, 16), (256, 384, 512), (1, 1, 1), (33, 65, 17),
+                                   (1000, 1100, 300), (2048, 2048, 2048)])
+def test_matmul_kernels(gelim, cuda, kernel, M, N, K):
+    torch.manual_seed(M * 7 + N * 3 + K)
+    A = torch.randn(M, K, device=cuda)
+    B = torch.randn(K, N, device=cuda)
+    C = gelim.ops.gpu_matmul(A, B, kernel=kernel)
+    torch.cuda.synchronize()
+    _check(C, A, B)
+
+
+def test_mfma_asymmetric_identity(gelim, cuda):
+    # A = I with an asymmetric B catches a transposed C/D layout
+    n = 256
+    A = torch.eye(n, device=cuda)
+    B = torch.arange(n * n, dtype=torch.float32, device=cuda).view(n, n)
+    C = gelim.ops.gpu_matmul(A, B)
+    assert torch.equal(C, B)
+    C = gelim.ops.gpu_matmul(B, A)
+    assert torch.equal(C, B)
+
+
+def test_matmul_reference_inputs(gelim, cuda):
+    n = 512
+    A, B = gelim.ops.matmul.reference_inputs(n)
+    C = gelim.ops.gpu_matmul(A.to(cuda), B.to(cuda)).cpu()
+    Cr = gelim.ops.cpu_matmul(A, B, omp=True)
+    rel = ((C - Cr).abs() / Cr.abs()).max().item()
+    assert rel < 1e-4
+
+
+def test_matmul_accumulate_strided(gelim, cuda):
+    from gelim.parallel.dist_matmul import matmul_acc_
+    torch.manual_seed(1)
+    A = torch.randn(200, 300, device=cuda)
+    B = torch.randn(300, 260, device=cuda)
+    C = torch.randn(200, 260, device=cuda)
+    C0 = C.clone()
+    matmul_acc_(C, A[:, 100:228], B[100:228], accumulate=True)
+    _check(C - C0, A[:, 100:228], B[100:228])
+
+
+def test_matmul_model_reference_timing(gelim, cuda):
+    n = 512
+    A, B = gelim.ops.matmul.reference_inputs(n)
+    Ch = torch.empty_like(A)
+    t = gelim.MatMul("mfma", cuda).run_reference_style(A.pin_memory(), B.pin_memory(), Ch)
+    assert t.end_to_end_s >= t.kernel_s > 0
+    _check(Ch.to(cuda), A.to(cuda), B.to(cuda))

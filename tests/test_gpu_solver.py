@@ -1,0 +1,92 @@
+"""GaussSolver on the GPU: accuracy vs torch.linalg.solve (fp64), golden
+reference errors on the `.dat` matrices, VERIFY pattern, singular detection,
+graph re-use."""
+import pytest
+import torch
+
+from conftest import GOLDEN_ERROR
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("backend", ["hip", "hip-pivot"])
+@pytest.mark.parametrize("n", [1, 2, 7, 64, 300, 1025, 2048, 2500])
+def test_random_vs_torch(gelim, cuda, backend, n):
+    aug = gelim.random_system(n, seed=n, device=cuda)
+    x = gelim.GaussSolver(n, backend=backend, device=cuda).solve(aug, check=True)
+    A = aug[:, :n]
+    ref = torch.linalg.solve(A, aug[:, n])
+    torch.cuda.synchronize()
+    assert torch.allclose(x, ref, rtol=1e-8, atol=1e-8 * n)
+    assert gelim.ops.gauss.error_metric(x) < 1e-7
+
+
+@pytest.mark.parametrize("name", list(GOLDEN_ERROR))
+@pytest.mark.parametrize("backend", ["hip", "hip-pivot"])
+def test_golden_errors_gpu(gelim, cuda, name, backend):
+    A = gelim.utils.io.load_fixture(name)
+    n = A.shape[0]
+    aug = gelim.augment_with_rhs(A).to(cuda)
+    x = gelim.GaussSolver(n, backend=backend, device=cuda).solve(aug, check=True)
+    err = gelim.ops.gauss.error_metric(x)
+    golden = GOLDEN_ERROR[name]
+    # different (blocked, FMA) rounding than the reference: same accuracy class
+    assert err <= max(20 * golden, 1e-14), (name, err, golden)
+
+
+@pytest.mark.parametrize("backend,dtype", [("hip", torch.float64), ("hip-pivot", torch.float64),
+                                           ("hip-pivot", torch.float32)])
+@pytest.mark.parametrize("n", [8, 16, 2048])
+def test_internal_verify_pattern_gpu(gelim, cuda, backend, dtype, n):
+    aug = gelim.synthetic_system(n, device=cuda, dtype=dtype)
+    s = gelim.GaussSolver(n, backend=backend, pivot="zero", dtype=dtype, device=cuda)
+    x, bn = s.solve(aug, return_bnorm=True)
+    expect = torch.zeros(n, dtype=torch.float64)
+    expect[0], expect[-1] = -0.5, 0.5
+    eb = torch.full((n,), 0.5, dtype=torch.float64)
+    eb[0] = 0.0
+    tol = 0 if backend == "hip-pivot" else 1e-12
+    assert torch.allclose(x.cpu(), expect, rtol=0, atol=tol)
+    assert torch.allclose(bn.cpu(), eb, rtol=0, atol=max(tol, 1e-12))
+
+
+@pytest.mark.parametrize("backend", ["hip", "hip-pivot"])
+def test_singular_detected(gelim, cuda, backend):
+    n = 64
+    aug = gelim.random_system(n, seed=3, device=cuda)
+    aug[:, 10] = aug[:, 3] * 2.0  # rank deficient
+    aug[:, 20] = 0.0
+    s = gelim.GaussSolver(n, backend=backend, device=cuda)
+    s.solve(aug)
+    assert s.info() > 0
+    with pytest.raises(gelim.SingularMatrixError):
+        s.solve(aug, check=True)
+
+
+def test_graph_replay_and_pointer_change(gelim, cuda):
+    n = 500
+    s = gelim.GaussSolver(n, backend="hip", device=cuda)
+    a1 = gelim.random_system(n, seed=1, device=cuda)
+    a2 = gelim.random_system(n, seed=2, device=cuda)
+    x1 = s.solve(a1).clone()
+    x1b = s.solve(a1).clone()  # graph replay
+    x2 = s.solve(a2).clone()   # new source pointer -> re-capture
+    assert torch.equal(x1, x1b)
+    for x, a in ((x1, a1), (x2, a2)):
+        assert torch.allclose(x, torch.linalg.solve(a[:, :n], a[:, n]), rtol=1e-9, atol=1e-9)
+
+
+def test_no_graph_path(gelim, cuda):
+    n = 200
+    aug = gelim.random_system(n, seed=9, device=cuda)
+    xg = gelim.GaussSolver(n, backend="hip", device=cuda, use_graph=True).solve(aug)
+    xe = gelim.GaussSolver(n, backend="hip", device=cuda, use_graph=False).solve(aug)
+    assert torch.equal(xg, xe)
+
+
+def test_blocked_ops_composition_gpu(gelim, cuda):
+    n = 700
+    aug = gelim.random_system(n, seed=5, device=cuda)
+    ref = gelim.GaussSolver(n, backend="hip", device=cuda).solve(aug)
+    x = gelim.blocked_solve_(aug.clone())
+    assert torch.allclose(x, ref, rtol=1e-10, atol=1e-10)

@@ -36,18 +36,27 @@ __global__ __launch_bounds__(64) void diag_solve_kernel(const T* __restrict__ U,
                                                         double* __restrict__ yw,
                                                         double* __restrict__ x, int i0, int nb,
                                                         int unit) {
-  __shared__ double s_U[kBS][kBS + 1];
+  // lane l keeps row l of the 64x64 block in registers; x_i is broadcast with
+  // v_readlane (i is wave-uniform) — no LDS, no shuffles on the serial chain
   const int l = threadIdx.x;
-  for (int r = 0; r < nb; ++r)
-    if (l < nb) s_U[r][l] = (double)U[(int64_t)(i0 + r) * ldu + i0 + l];
-  __syncthreads();
+  double row[kBS];
+  const T* src = U + (int64_t)(i0 + min(l, nb - 1)) * ldu + i0;
+#pragma unroll
+  for (int c = 0; c < kBS; ++c) row[c] = (l < nb && c < nb) ? (double)src[min(c, nb - 1)] : 0.0;
   double yv = (l < nb) ? yw[i0 + l] : 0.0;
   double xv = 0.0;
-  for (int i = nb - 1; i >= 0; --i) {
-    double xi = unit ? yv : yv / s_U[i][i];
-    xi = __shfl(xi, i, dev::kWave);
-    if (l == i) xv = xi;
-    if (l < i) yv -= s_U[l][i] * xi;
+#pragma unroll
+  for (int i = kBS - 1; i >= 0; --i) {
+    if (i < nb) {
+      const double xi_l = unit ? yv : yv / row[i];  // meaningful in lane i only
+      const double xi = __builtin_bit_cast(
+          double, ((uint64_t)(unsigned)__builtin_amdgcn_readlane(
+                       (int)(__builtin_bit_cast(uint64_t, xi_l) >> 32), i)
+                   << 32) |
+                      (unsigned)__builtin_amdgcn_readlane((int)__builtin_bit_cast(uint64_t, xi_l), i));
+      if (l == i) xv = xi;
+      yv = (l < i) ? fma(-row[i], xi, yv) : yv;
+    }
   }
   if (l < nb) x[i0 + l] = xv;
 }

@@ -54,6 +54,60 @@ __device__ __forceinline__ double wave_max(double v) {
   return v;
 }
 
+// ---- DPP wave reductions (gfx9-family row_shr / row_bcast scans) ---------
+// The classic inclusive-scan ladder: row_shr:1,2,4,8 inside each 16-lane row,
+// then row_bcast:15 and row_bcast:31 across rows; lane 63 ends with the
+// reduction of all 64 lanes and is read with v_readlane into a uniform value.
+// ~6 dependent VALU+DPP steps instead of 6 ds_bpermute round trips per value.
+enum : int {
+  kDppRowShr1 = 0x111,
+  kDppRowShr2 = 0x112,
+  kDppRowShr4 = 0x114,
+  kDppRowShr8 = 0x118,
+  kDppRowBcast15 = 0x142,
+  kDppRowBcast31 = 0x143
+};
+
+template <int CTRL, int ROW_MASK, int BANK_MASK>
+__device__ __forceinline__ unsigned dpp_u32(unsigned identity, unsigned v) {
+  // lanes whose source is out of range (or masked) keep `identity`
+  return (unsigned)__builtin_amdgcn_update_dpp((int)identity, (int)v, CTRL, ROW_MASK, BANK_MASK, false);
+}
+
+// 64-bit unsigned max over the wave (identity 0); result uniform.
+__device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
+  unsigned hi = (unsigned)(v >> 32), lo = (unsigned)v;
+#define GELIM_MAX_STEP(CTRL, RM, BM)                                     \
+  {                                                                      \
+    const unsigned h2 = dpp_u32<CTRL, RM, BM>(0u, hi);                   \
+    const unsigned l2 = dpp_u32<CTRL, RM, BM>(0u, lo);                   \
+    const bool gt = (h2 > hi) || (h2 == hi && l2 > lo);                  \
+    hi = gt ? h2 : hi;                                                   \
+    lo = gt ? l2 : lo;                                                   \
+  }
+  GELIM_MAX_STEP(kDppRowShr1, 0xf, 0xf)
+  GELIM_MAX_STEP(kDppRowShr2, 0xf, 0xf)
+  GELIM_MAX_STEP(kDppRowShr4, 0xf, 0xf)
+  GELIM_MAX_STEP(kDppRowShr8, 0xf, 0xf)
+  GELIM_MAX_STEP(kDppRowBcast15, 0xa, 0xf)
+  GELIM_MAX_STEP(kDppRowBcast31, 0xc, 0xf)
+#undef GELIM_MAX_STEP
+  hi = (unsigned)__builtin_amdgcn_readlane((int)hi, 63);
+  lo = (unsigned)__builtin_amdgcn_readlane((int)lo, 63);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+// 32-bit unsigned min over the wave (identity 0xffffffff); result uniform.
+__device__ __forceinline__ unsigned wave_min_u32(unsigned v) {
+  v = min(v, dpp_u32<kDppRowShr1, 0xf, 0xf>(0xffffffffu, v));
+  v = min(v, dpp_u32<kDppRowShr2, 0xf, 0xf>(0xffffffffu, v));
+  v = min(v, dpp_u32<kDppRowShr4, 0xf, 0xf>(0xffffffffu, v));
+  v = min(v, dpp_u32<kDppRowShr8, 0xf, 0xf>(0xffffffffu, v));
+  v = min(v, dpp_u32<kDppRowBcast15, 0xa, 0xf>(0xffffffffu, v));
+  v = min(v, dpp_u32<kDppRowBcast31, 0xc, 0xf>(0xffffffffu, v));
+  return (unsigned)__builtin_amdgcn_readlane((int)v, 63);
+}
+
 // Pivot key of a candidate row.  PARTIAL: |a| (NaN never wins).  ZERO
 // (reference internal getPivot): the diagonal if non-zero, else the first
 // non-zero row — encoded as 2 for a non-zero diagonal, 1 for any other
@@ -66,6 +120,21 @@ __device__ __forceinline__ double pivot_key(T a, bool is_diag, int mode) {
   }
   if (a == T(0)) return 0.0;
   return is_diag ? 2.0 : 1.0;
+}
+
+// Pivot key as an order-preserving unsigned integer: 0 = no candidate,
+// larger = better.  PARTIAL: bits(|a|)+1 (non-negative doubles order like
+// their bit patterns; NaN never wins); ZERO: 3 diag non-zero, 2 other non-zero,
+// 1 zero.
+template <typename T>
+__device__ __forceinline__ uint64_t pivot_ukey(T a, bool is_diag, int mode) {
+  if (mode == 1) {
+    const double v = fabs((double)a);
+    if (v != v) return 0;
+    return (uint64_t)__double_as_longlong(v) + 1;
+  }
+  if (a == T(0)) return 1;
+  return is_diag ? 3 : 2;
 }
 
 }  // namespace dev

@@ -9,17 +9,22 @@
 // panel, L[r][j] = a[r][j] / a[j][j], rank-1 update of the panel's remaining
 // columns.
 //
-// How (MI355X-first): ONE workgroup of 1024 threads (16 wave64s) holds the
-// whole panel in VGPRs — thread t owns rows t, t+1024, ... (R rows x W
-// columns = 32 doubles = 64 VGPRs per lane) — so every column step is pure
+// How (MI355X-first): ONE workgroup of 256 threads — 4 wave64s, one per SIMD,
+// so each wave owns the SIMD's whole 512-entry VGPR file — holds the panel in
+// registers: thread t owns rows t, t+256, ... (R rows x W columns = up to 128
+// doubles = 256 VGPRs per lane, 256 KiB per CU), so every column step is
 // on-chip work with a SINGLE workgroup barrier:
-//   1. each lane scans its rows, a DPP/shuffle wave arg-max picks the wave's
-//      candidate, the winning lane writes its whole candidate row (W doubles)
-//      into LDS and the owner of row j writes row j;
+//   1. each lane scans its rows; a DPP max-scan of the (order-preserving
+//      integer) key followed by a DPP min-scan of the rows holding it gives
+//      the wave's candidate (ties -> lowest row, like the reference's strict
+//      '>'); the winning lane writes its whole candidate row into LDS and the
+//      owner of row j writes row j;
 //   2. __syncthreads();
-//   3. every wave re-reduces the 16 candidates itself (no second barrier),
-//      reads the pivot row straight from the LDS slot of the winning wave,
-//      exchanges rows j/p in registers and applies the rank-1 update.
+//   3. every wave reduces the 4 wave candidates itself (no second barrier),
+//      reads the pivot row from the LDS slot of the winning wave, exchanges
+//      rows j/p in registers and applies the rank-1 update with fp64 FMAs.
+// Fewer, fatter waves matter: with 16 waves the per-column overhead (reductions,
+// LDS traffic, branches) was issued 4x per SIMD and dominated (4-5 us/column).
 // LDS slots are double-buffered by column parity, which is what makes the
 // single barrier per column race-free.  The panel is read and written exactly
 // once (coalesced 16-byte loads per row).
@@ -33,23 +38,23 @@
 namespace gelim {
 namespace {
 
-constexpr int kThreads = 1024;
+constexpr int kThreads = 256;  // 4 wave64s: one per SIMD, each with the full VGPR file
 constexpr int kWaves = kThreads / dev::kWave;
 
+template <int W>
 struct PanelLds {
   // slots double-buffered by column parity (one barrier per column)
-  template <int W>
-  struct T {
-    double cand_row[2][kWaves][W];
-    double rowj[2][W];
-    double cand_val[2][kWaves];
-    int cand_idx[2][kWaves];
-    int piv[W];
-  };
+  double cand_row[2][kWaves][W];
+  unsigned cand_key[2][kWaves][2];  // {hi, lo} of the wave's winning key
+  unsigned cand_row_idx[2][kWaves];
+  int sel[W];           // physical (original) row chosen at each step
+  int pos_of[2 * W];    // compact row id -> compact position
+  int row_at[2 * W];    // compact position -> compact row id
+  int piv[W];
 };
 
 // Value barrier: stops LLVM from folding a select over register-array
-// elements into a dynamically indexed load/store, which would demote the whole
+// elements into a dynamically indexed access, which would demote the whole
 // array to scratch memory.
 __device__ __forceinline__ double opaque(double x) {
   asm volatile("" : "+v"(x));
@@ -58,99 +63,91 @@ __device__ __forceinline__ double opaque(double x) {
 
 // One column step j = J of the panel (J is a compile-time constant so every
 // register index below is static — a runtime j would spill a[][] to scratch).
+// Rows are never moved during the column loop ("logical pivoting"): a chosen
+// row is retired via the per-lane `chosen` bit mask and keeps its place; the
+// LAPACK interchange sequence is reconstructed once at the end.
 template <int R, int W, int J>
-__device__ __forceinline__ void panel_step(double (&a)[R][W], typename PanelLds::T<W>& sh, int t,
-                                           int lane, int wave, int m, int w, int row0, int mode,
-                                           int* __restrict__ info) {
+__device__ __forceinline__ void panel_step(double (&a)[R][W], uint64_t& chosen, PanelLds<W>& sh,
+                                           int t, int lane, int wave, int m, int w, int row0,
+                                           int mode, int* __restrict__ info) {
   if (J >= w) return;  // uniform across the workgroup
   constexpr int par = J & 1;
 
-  // 1. local + wave arg-max over rows >= J of column J
-  double best = -1.0;
-  int bidx = INT_MAX;
+  // 1. local candidate over this lane's live rows (not yet chosen, < m)
+  uint64_t best = 0;
+  unsigned brow = 0xffffffffu;
 #pragma unroll
   for (int i = 0; i < R; ++i) {
     const int lr = t + i * kThreads;
-    if (lr >= J && lr < m) {
-      const double key = dev::pivot_key(a[i][J], lr == J, mode);
-      if (key > best) {  // rows visited in increasing order: '>' keeps the lowest
-        best = key;
-        bidx = lr;
-      }
-    }
+    const bool ok = !((chosen >> i) & 1) && lr < m;
+    // the reference's diagonal preference (ZERO rule) refers to the row that
+    // currently sits at position J: physically row J unless it was chosen
+    // earlier, in which case no row is "the diagonal" for that rule (a
+    // deliberate, documented difference from a physical-swap run)
+    const uint64_t key = ok ? dev::pivot_ukey(a[i][J], lr == J, mode) : 0;
+    const bool better = key > best;  // increasing rows: '>' keeps the lowest row on ties
+    best = better ? key : best;
+    brow = better ? (unsigned)lr : brow;
   }
-  dev::wave_argmax(best, bidx);
-  if (bidx != INT_MAX && (bidx & (kThreads - 1)) == t) {
-    const int ip = bidx / kThreads;
-    // branchless select keeps every register index static (no scratch)
+  // 2. wave arg-max: DPP max of the key, then DPP min of the rows holding it
+  const uint64_t wkey = dev::wave_max_u64(best);
+  const unsigned wrow = dev::wave_min_u32(best == wkey ? brow : 0xffffffffu);
+  if (wkey != 0 && (int)(wrow & (kThreads - 1)) == t) {
+    const int ip = (int)(wrow / kThreads);
 #pragma unroll
-    for (int c = 0; c < W; ++c) {
-      double v = opaque(a[0][c]);
+    for (int i = 0; i < R; ++i)
+      if (i == ip) {
 #pragma unroll
-      for (int i = 1; i < R; ++i) v = (i == ip) ? opaque(a[i][c]) : v;
-      sh.cand_row[par][wave][c] = v;
-    }
+        for (int c = 0; c < W; ++c) sh.cand_row[par][wave][c] = opaque(a[i][c]);
+      }
   }
   if (lane == 0) {
-    sh.cand_val[par][wave] = best;
-    sh.cand_idx[par][wave] = bidx;
-  }
-  if (t == J) {  // row J lives in thread J, slot 0 (J < W <= 32)
-#pragma unroll
-    for (int c = 0; c < W; ++c) sh.rowj[par][c] = a[0][c];
+    sh.cand_key[par][wave][0] = (unsigned)(wkey >> 32);
+    sh.cand_key[par][wave][1] = (unsigned)wkey;
+    sh.cand_row_idx[par][wave] = wrow;
   }
   __syncthreads();
 
-  // 2. block winner, recomputed by every wave (no second barrier)
-  double gv = (lane < kWaves) ? sh.cand_val[par][lane] : -1.0;
-  int gi = (lane < kWaves) ? sh.cand_idx[par][lane] : INT_MAX;
-  dev::group_argmax(gv, gi, kWaves);
-  gv = __shfl(gv, 0, dev::kWave);
-  const int p = __shfl(gi, 0, dev::kWave);
-  const int pw = (p & (kThreads - 1)) >> 6;  // wave that published the pivot row
-  const double* u = sh.cand_row[par][pw];  // pivot row, read from LDS (broadcast)
+  // 3. block winner from the 4 wave candidates (broadcast LDS reads)
+  uint64_t gkey = 0;
+  unsigned p = 0xffffffffu;
+#pragma unroll
+  for (int q = 0; q < kWaves; ++q) {
+    const uint64_t k = ((uint64_t)sh.cand_key[par][q][0] << 32) | sh.cand_key[par][q][1];
+    const unsigned r = sh.cand_row_idx[par][q];
+    const bool better = k > gkey || (k == gkey && r < p);
+    gkey = better ? k : gkey;
+    p = better ? r : p;
+  }
+  const int pw = (int)((p & (kThreads - 1)) >> 6);  // wave that published the pivot row
+  const double* u = sh.cand_row[par][pw];
   const double d = u[J];
   if (t == 0) {
-    sh.piv[J] = p;
-    if (gv <= 0.0 && info && *info == 0) *info = row0 + J + 1;  // zero pivot
+    sh.sel[J] = (int)p;
+    if (gkey <= 1 && info && *info == 0) *info = row0 + J + 1;  // zero pivot
   }
+  if ((int)(p & (kThreads - 1)) == t) chosen |= 1ull << (p / kThreads);
 
-  // 3. exchange rows J and p in registers (whole panel rows: L moves too)
-  if (p != J) {
-    if (t == J) {
-#pragma unroll
-      for (int c = 0; c < W; ++c) a[0][c] = sh.cand_row[par][pw][c];
-    }
-    if ((p & (kThreads - 1)) == t) {
-      const int ip = p / kThreads;
-#pragma unroll
-      for (int c = 0; c < W; ++c) {
-        const double v = sh.rowj[par][c];
-#pragma unroll
-        for (int i = 0; i < R; ++i) a[i][c] = opaque((i == ip) ? v : opaque(a[i][c]));
-      }
-    }
-  }
-
-  // 4. multipliers + rank-1 update of the rows below J
+  // 4. multipliers + rank-1 update of every live row (retired rows get l = 0)
   const double rd = (d != 0.0) ? 1.0 / d : 0.0;
+  double uc[W];
+#pragma unroll
+  for (int c = J + 1; c < W; ++c) uc[c] = u[c];
 #pragma unroll
   for (int i = 0; i < R; ++i) {
-    const int lr = t + i * kThreads;
-    if (lr > J && lr < m) {
-      const double l = a[i][J] * rd;
-      a[i][J] = l;
+    const bool live = !((chosen >> i) & 1);
+    const double l = live ? a[i][J] * rd : 0.0;
+    a[i][J] = live ? l : a[i][J];
 #pragma unroll
-      for (int c = J + 1; c < W; ++c) a[i][c] -= l * u[c];
-    }
+    for (int c = J + 1; c < W; ++c) a[i][c] = fma(-l, uc[c], a[i][c]);
   }
 }
 
 template <int R, int W, int... J>
-__device__ __forceinline__ void panel_steps(double (&a)[R][W], typename PanelLds::T<W>& sh, int t,
-                                            int lane, int wave, int m, int w, int row0, int mode,
-                                            int* info, std::integer_sequence<int, J...>) {
-  (panel_step<R, W, J>(a, sh, t, lane, wave, m, w, row0, mode, info), ...);
+__device__ __forceinline__ void panel_steps(double (&a)[R][W], uint64_t& chosen, PanelLds<W>& sh,
+                                            int t, int lane, int wave, int m, int w, int row0,
+                                            int mode, int* info, std::integer_sequence<int, J...>) {
+  (panel_step<R, W, J>(a, chosen, sh, t, lane, wave, m, w, row0, mode, info), ...);
 }
 
 template <int R, int W>
@@ -158,7 +155,8 @@ __global__ __launch_bounds__(kThreads) void panel_kernel(double* __restrict__ P,
                                                          int m, int w, int row0, int mode,
                                                          int* __restrict__ piv,
                                                          int* __restrict__ info) {
-  __shared__ typename PanelLds::T<W> sh;
+  static_assert(R <= 64, "chosen mask is 64 bits");
+  __shared__ PanelLds<W> sh;
   const int t = threadIdx.x;
   const int lane = t & (dev::kWave - 1);
   const int wave = t >> 6;
@@ -167,25 +165,64 @@ __global__ __launch_bounds__(kThreads) void panel_kernel(double* __restrict__ P,
 #pragma unroll
   for (int i = 0; i < R; ++i) {
     const int lr = t + i * kThreads;
-    const double* src = P + (int64_t)lr * ldp;
+    const double* src = P + (int64_t)min(lr, m - 1) * ldp;  // clamped: no divergent loads
 #pragma unroll
-    for (int c = 0; c < W; ++c) a[i][c] = (lr < m && c < w) ? src[c] : 0.0;
+    for (int c = 0; c < W; ++c) {
+      const double v = src[min(c, w - 1)];
+      a[i][c] = (lr < m && c < w) ? v : 0.0;
+    }
   }
+  uint64_t chosen = 0;
 
-  panel_steps<R, W>(a, sh, t, lane, wave, m, w, row0, mode, info,
+  panel_steps<R, W>(a, chosen, sh, t, lane, wave, m, w, row0, mode, info,
                     std::make_integer_sequence<int, W>{});
 
+  // Reconstruct LAPACK's sequential interchanges from the selection order.
+  // Compact ids: rows < w keep their index; a chosen row >= w selected at
+  // step j gets id w + j.  Compact positions use the same numbering (the
+  // only positions >= w ever touched are original places of chosen rows).
+  if (t == 0) {
+    for (int x = 0; x < 2 * w; ++x) {
+      sh.pos_of[x] = x;
+      sh.row_at[x] = x;
+    }
+    for (int j = 0; j < w; ++j) {
+      const int p = sh.sel[j];
+      const int idp = p < w ? p : w + j;
+      const int cur = sh.pos_of[idp];
+      const int other = sh.row_at[j];
+      sh.row_at[j] = idp;
+      sh.row_at[cur] = other;
+      sh.pos_of[idp] = j;
+      sh.pos_of[other] = cur;
+      sh.piv[j] = cur < w ? cur : sh.sel[cur - w];
+    }
+  }
+  __syncthreads();
+
+  // write back every physical row to its final position
 #pragma unroll
   for (int i = 0; i < R; ++i) {
     const int lr = t + i * kThreads;
     if (lr < m) {
-      double* dst = P + (int64_t)lr * ldp;
+      int dest = lr;
+      int id = -1;
+      if (lr < w) {
+        id = lr;
+      } else if ((chosen >> i) & 1) {
+        for (int j = 0; j < w; ++j)
+          if (sh.sel[j] == lr) id = w + j;
+      }
+      if (id >= 0) {
+        const int cp = sh.pos_of[id];
+        dest = cp < w ? cp : sh.sel[cp - w];
+      }
+      double* dst = P + (int64_t)dest * ldp;
 #pragma unroll
       for (int c = 0; c < W; ++c)
         if (c < w) dst[c] = a[i][c];
     }
   }
-  __syncthreads();
   if (t < w) piv[t] = sh.piv[t];
 }
 
@@ -200,9 +237,9 @@ int launch_panel(double* P, int64_t ldp, int64_t m, int64_t w, int64_t row0, int
 
 }  // namespace
 
-// Widest register panel that fits 32 doubles per lane for m rows.
+// Widest register panel for m rows: R x W = 128 doubles (256 VGPRs) per lane,
+// 256 lanes -> 256 KiB of panel held on one CU.
 int64_t panel_width_for(int64_t m) {
-  if (m <= 1024) return 32;
   if (m <= 2048) return 16;
   if (m <= 4096) return 8;
   if (m <= 8192) return 4;
@@ -213,11 +250,13 @@ int64_t panel_width_for(int64_t m) {
 int panel_factor(double* P, int64_t ldp, int64_t m, int64_t w, int64_t row0, int mode,
                  int* piv, int* info, hipStream_t s) {
   if (m <= 0 || w <= 0 || w > m) return GELIM_FAIL(GELIM_E_ARG, "panel: bad m/w");
-  if (m <= 1024 && w <= 32) return launch_panel<1, 32>(P, ldp, m, w, row0, mode, piv, info, s);
-  if (m <= 2048 && w <= 16) return launch_panel<2, 16>(P, ldp, m, w, row0, mode, piv, info, s);
-  if (m <= 4096 && w <= 8) return launch_panel<4, 8>(P, ldp, m, w, row0, mode, piv, info, s);
-  if (m <= 8192 && w <= 4) return launch_panel<8, 4>(P, ldp, m, w, row0, mode, piv, info, s);
-  if (m <= 16384 && w <= 2) return launch_panel<16, 2>(P, ldp, m, w, row0, mode, piv, info, s);
+  if (m <= 256 && w <= 16) return launch_panel<1, 16>(P, ldp, m, w, row0, mode, piv, info, s);
+  if (m <= 512 && w <= 16) return launch_panel<2, 16>(P, ldp, m, w, row0, mode, piv, info, s);
+  if (m <= 1024 && w <= 16) return launch_panel<4, 16>(P, ldp, m, w, row0, mode, piv, info, s);
+  if (m <= 2048 && w <= 16) return launch_panel<8, 16>(P, ldp, m, w, row0, mode, piv, info, s);
+  if (m <= 4096 && w <= 8) return launch_panel<16, 8>(P, ldp, m, w, row0, mode, piv, info, s);
+  if (m <= 8192 && w <= 4) return launch_panel<32, 4>(P, ldp, m, w, row0, mode, piv, info, s);
+  if (m <= 16384 && w <= 2) return launch_panel<64, 2>(P, ldp, m, w, row0, mode, piv, info, s);
   return GELIM_FAIL(GELIM_E_ARG, "panel: m=" + std::to_string(m) + " w=" + std::to_string(w) +
                                      " exceeds the register-resident panel");
 }
@@ -230,11 +269,10 @@ extern "C" int gelim_gpu_panel_factor(double* dP, int64_t ldp, int64_t m, int64_
   return gelim::panel_factor(dP, ldp, m, w, row0, pivot, dpiv, dinfo, (hipStream_t)stream);
 }
 
-extern "C" int64_t gelim_gpu_panel_max_rows(int64_t w) {
+extern "C" int64_t gelim_gpu_panel_max_rows(int64_t w) {  // rows per width
   if (w <= 2) return 16384;
   if (w <= 4) return 8192;
   if (w <= 8) return 4096;
   if (w <= 16) return 2048;
-  if (w <= 32) return 1024;
   return 0;
 }

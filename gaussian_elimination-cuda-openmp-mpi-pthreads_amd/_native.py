@@ -75,6 +75,9 @@ _PROTOS = {
     "gelim_gauss_plan_solve": (_int, [_vp, _vp, _i64, _vp, _vp, _vp]),
     "gelim_gauss_plan_info": (_int, [_vp, _vp]),
     "gelim_gpu_matmul_f32": (_int, [_vp, _vp, _vp, _i64, _i64, _i64, _int, _vp]),
+    "gelim_gpu_matmul_f32_ex": (_int, [_vp, _i64, _vp, _i64, _vp, _i64, _i64, _i64, _i64, _int, _int, _vp]),
+    "gelim_init_random_block_f64": (None, [_vp, _i64, _i64, _i64, _i64, _i64, _u64]),
+    "gelim_gpu_init_random_block": (_int, [_vp, _i64, _i64, _i64, _i64, _i64, _u64, _vp]),
 }
 
 _lib: C.CDLL | None = None

@@ -152,7 +152,7 @@ def blocked_solve_(aug: torch.Tensor, pivot: str = "partial", width: int | None 
 
 
 def _default_width(m: int) -> int:
-    for w, rows in ((32, 1024), (16, 2048), (8, 4096), (4, 8192), (2, 16384)):
+    for w, rows in ((16, 2048), (8, 4096), (4, 8192), (2, 16384)):
         if m <= rows:
             return w
     raise ValueError("panel too tall")

@@ -48,7 +48,7 @@ from .comm import Communicator
 def inner_width(m: int, device_type: str) -> int:
     """Sub-panel width the register-resident GPU panel kernel supports for m
     rows (CPU: same partition so CPU and GPU runs agree op for op)."""
-    for w, rows in ((32, 1024), (16, 2048), (8, 4096), (4, 8192), (2, 16384)):
+    for w, rows in ((16, 2048), (8, 4096), (4, 8192), (2, 16384)):
         if m <= rows:
             return w
     raise ValueError(f"panel of {m} rows exceeds the register-resident panel kernel")

@@ -31,6 +31,7 @@
 #include <hip/hip_runtime.h>
 
 #include <utility>
+#include <vector>
 
 #include "device_common.h"
 #include "gelim/internal.h"
@@ -42,7 +43,7 @@ constexpr int kThreads = 256;  // 4 wave64s: one per SIMD, each with the full VG
 constexpr int kWaves = kThreads / dev::kWave;
 
 template <int W>
-struct PanelLds {
+struct alignas(16) PanelLds {
   // slots double-buffered by column parity (one barrier per column)
   double cand_row[2][kWaves][W];
   unsigned cand_key[2][kWaves][2];  // {hi, lo} of the wave's winning key
@@ -91,7 +92,14 @@ __device__ __forceinline__ void panel_step(double (&a)[R][W], uint64_t& chosen, 
   }
   // 2. wave arg-max: DPP max of the key, then DPP min of the rows holding it
   const uint64_t wkey = dev::wave_max_u64(best);
-  const unsigned wrow = dev::wave_min_u32(best == wkey ? brow : 0xffffffffu);
+  // exact ties are rare: one ballot finds the single holder; only a real tie
+  // pays the second (row-min) DPP chain (uniform branch)
+  const uint64_t holders = __ballot(best == wkey);
+  unsigned wrow;
+  if (__popcll(holders) == 1)
+    wrow = (unsigned)__builtin_amdgcn_readlane((int)brow, __ffsll((long long)holders) - 1);
+  else
+    wrow = dev::wave_min_u32(best == wkey ? brow : 0xffffffffu);
   if (wkey != 0 && (int)(wrow & (kThreads - 1)) == t) {
     const int ip = (int)(wrow / kThreads);
 #pragma unroll
@@ -133,14 +141,22 @@ __device__ __forceinline__ void panel_step(double (&a)[R][W], uint64_t& chosen, 
   double uc[W];
 #pragma unroll
   for (int c = J + 1; c < W; ++c) uc[c] = u[c];
+  double l[R];
 #pragma unroll
   for (int i = 0; i < R; ++i) {
     const bool live = !((chosen >> i) & 1);
-    const double l = live ? a[i][J] * rd : 0.0;
-    a[i][J] = live ? l : a[i][J];
-#pragma unroll
-    for (int c = J + 1; c < W; ++c) a[i][c] = fma(-l, uc[c], a[i][c]);
+    l[i] = live ? a[i][J] * rd : 0.0;
+    a[i][J] = live ? l[i] : a[i][J];
   }
+  // column J+1 first: the next step's pivot search depends only on it
+  if constexpr (J + 1 < W) {
+#pragma unroll
+    for (int i = 0; i < R; ++i) a[i][J + 1] = fma(-l[i], uc[J + 1], a[i][J + 1]);
+  }
+#pragma unroll
+  for (int i = 0; i < R; ++i)
+#pragma unroll
+    for (int c = J + 2; c < W; ++c) a[i][c] = fma(-l[i], uc[c], a[i][c]);
 }
 
 template <int R, int W, int... J>
@@ -150,32 +166,128 @@ __device__ __forceinline__ void panel_steps(double (&a)[R][W], uint64_t& chosen,
   (panel_step<R, W, J>(a, chosen, sh, t, lane, wave, m, w, row0, mode, info), ...);
 }
 
+// LDS staging tile for the coalesced panel load/store: 256 rows x W doubles,
+// 16-byte chunks XOR-swizzled by row so that the per-row ds_read_b128 /
+// ds_write_b128 of 16 consecutive lanes hit distinct banks.
+template <int W>
+__device__ __forceinline__ int swz_chunk(int row, int ch) {
+  constexpr int CH = W / 2;
+  return ch ^ (row & (CH - 1));
+}
+
+extern __shared__ __attribute__((aligned(16))) char g_panel_dyn_lds[];
+
 template <int R, int W>
+__device__ __forceinline__ void stage_in(double (&a)[R][W], const double* __restrict__ P,
+                                         int64_t ldp, int m, int t) {
+  constexpr int CH = W / 2;                    // chunks per row
+  constexpr int ROWS_PER_PASS = kThreads / CH;  // rows per coalesced pass
+  double2* tile = reinterpret_cast<double2*>(g_panel_dyn_lds);  // [kThreads][CH]
+#pragma unroll
+  for (int i = 0; i < R; ++i) {
+    // coalesced: lane group of CH lanes reads one row's W doubles
+    const int ch = t % CH;
+#pragma unroll
+    for (int pass = 0; pass < kThreads / ROWS_PER_PASS; ++pass) {
+      const int rl = pass * ROWS_PER_PASS + t / CH;  // row within this slot
+      const int lr = i * kThreads + rl;
+      double2 v = make_double2(0.0, 0.0);
+      if (lr < m) v = *reinterpret_cast<const double2*>(P + (int64_t)lr * ldp + 2 * ch);
+      tile[rl * CH + swz_chunk<W>(rl, ch)] = v;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+      const double2 v = tile[t * CH + swz_chunk<W>(t, c)];
+      a[i][2 * c] = v.x;
+      a[i][2 * c + 1] = v.y;
+    }
+    __syncthreads();
+  }
+}
+
+template <int R, int W>
+__device__ __forceinline__ void stage_out(const double (&a)[R][W], const int (&dest)[R],
+                                          double* __restrict__ P, int64_t ldp, int m, int t) {
+  constexpr int CH = W / 2;
+  constexpr int ROWS_PER_PASS = kThreads / CH;
+  double2* tile = reinterpret_cast<double2*>(g_panel_dyn_lds);
+  int* dst_row = reinterpret_cast<int*>(g_panel_dyn_lds + sizeof(double2) * kThreads * CH);
+#pragma unroll
+  for (int i = 0; i < R; ++i) {
+#pragma unroll
+    for (int c = 0; c < CH; ++c) tile[t * CH + swz_chunk<W>(t, c)] = make_double2(a[i][2 * c], a[i][2 * c + 1]);
+    dst_row[t] = dest[i];
+    __syncthreads();
+    const int ch = t % CH;
+#pragma unroll
+    for (int pass = 0; pass < kThreads / ROWS_PER_PASS; ++pass) {
+      const int rl = pass * ROWS_PER_PASS + t / CH;
+      const int lr = i * kThreads + rl;
+      if (lr < m)
+        *reinterpret_cast<double2*>(P + (int64_t)dst_row[rl] * ldp + 2 * ch) =
+            tile[rl * CH + swz_chunk<W>(rl, ch)];
+    }
+    __syncthreads();
+  }
+}
+
+// Diagnostic stamps (separate build of the same kernel, never used by the
+// solver): thread 0 records s_memtime at phase boundaries into `stamps`.
+__device__ __forceinline__ unsigned long long stamp_now() {
+  unsigned long long t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
+
+template <int R, int W, bool STAMP = false>
 __global__ __launch_bounds__(kThreads) void panel_kernel(double* __restrict__ P, int64_t ldp,
                                                          int m, int w, int row0, int mode,
                                                          int* __restrict__ piv,
-                                                         int* __restrict__ info) {
+                                                         int* __restrict__ info,
+                                                         unsigned long long* __restrict__ stamps = nullptr) {
   static_assert(R <= 64, "chosen mask is 64 bits");
   __shared__ PanelLds<W> sh;
   const int t = threadIdx.x;
   const int lane = t & (dev::kWave - 1);
   const int wave = t >> 6;
 
+  unsigned long long t0 = 0;
+  if constexpr (STAMP) t0 = stamp_now();
   double a[R][W];
+  // full-width panels with 16-byte aligned rows are staged through LDS so
+  // that global loads are coalesced (8 lanes per 128-byte row segment)
+  const bool staged = (w == W) && (W % 2 == 0) && ((((uintptr_t)P) & 15) == 0) && (ldp % 2 == 0);
+  if (staged) {
+    stage_in<R, W>(a, P, ldp, m, t);
+  } else {
 #pragma unroll
-  for (int i = 0; i < R; ++i) {
-    const int lr = t + i * kThreads;
-    const double* src = P + (int64_t)min(lr, m - 1) * ldp;  // clamped: no divergent loads
+    for (int i = 0; i < R; ++i) {
+      const int lr = t + i * kThreads;
+      const double* src = P + (int64_t)min(lr, m - 1) * ldp;  // clamped: no divergent loads
 #pragma unroll
-    for (int c = 0; c < W; ++c) {
-      const double v = src[min(c, w - 1)];
-      a[i][c] = (lr < m && c < w) ? v : 0.0;
+      for (int c = 0; c < W; ++c) {
+        const double v = src[min(c, w - 1)];
+        a[i][c] = (lr < m && c < w) ? v : 0.0;
+      }
     }
   }
   uint64_t chosen = 0;
+  if constexpr (STAMP) {
+    __syncthreads();
+    if (t == 0) {
+      stamps[0] = t0;
+      stamps[1] = stamp_now();
+    }
+  }
 
   panel_steps<R, W>(a, chosen, sh, t, lane, wave, m, w, row0, mode, info,
                     std::make_integer_sequence<int, W>{});
+  if constexpr (STAMP) {
+    if (t == 0) stamps[2] = stamp_now();
+  }
 
   // Reconstruct LAPACK's sequential interchanges from the selection order.
   // Compact ids: rows < w keep their index; a chosen row >= w selected at
@@ -201,36 +313,58 @@ __global__ __launch_bounds__(kThreads) void panel_kernel(double* __restrict__ P,
   __syncthreads();
 
   // write back every physical row to its final position
+  int dest[R];
 #pragma unroll
   for (int i = 0; i < R; ++i) {
     const int lr = t + i * kThreads;
-    if (lr < m) {
-      int dest = lr;
-      int id = -1;
-      if (lr < w) {
-        id = lr;
-      } else if ((chosen >> i) & 1) {
-        for (int j = 0; j < w; ++j)
-          if (sh.sel[j] == lr) id = w + j;
-      }
-      if (id >= 0) {
-        const int cp = sh.pos_of[id];
-        dest = cp < w ? cp : sh.sel[cp - w];
-      }
-      double* dst = P + (int64_t)dest * ldp;
+    int d = lr;
+    int id = -1;
+    if (lr < w) {
+      id = lr;
+    } else if (lr < m && ((chosen >> i) & 1)) {
+      for (int j = 0; j < w; ++j)
+        if (sh.sel[j] == lr) id = w + j;
+    }
+    if (id >= 0) {
+      const int cp = sh.pos_of[id];
+      d = cp < w ? cp : sh.sel[cp - w];
+    }
+    dest[i] = d;
+  }
+  if (staged) {
+    stage_out<R, W>(a, dest, P, ldp, m, t);
+  } else {
 #pragma unroll
-      for (int c = 0; c < W; ++c)
-        if (c < w) dst[c] = a[i][c];
+    for (int i = 0; i < R; ++i) {
+      const int lr = t + i * kThreads;
+      if (lr < m) {
+        double* dst = P + (int64_t)dest[i] * ldp;
+#pragma unroll
+        for (int c = 0; c < W; ++c)
+          if (c < w) dst[c] = a[i][c];
+      }
     }
   }
   if (t < w) piv[t] = sh.piv[t];
+  if constexpr (STAMP) {
+    __syncthreads();
+    if (t == 0) {
+      stamps[3] = stamp_now();
+      stamps[4] = __builtin_amdgcn_s_memrealtime();
+    }
+  }
+}
+
+template <int W>
+constexpr size_t stage_bytes() {
+  return sizeof(double) * kThreads * W + sizeof(int) * kThreads;
 }
 
 template <int R, int W>
 int launch_panel(double* P, int64_t ldp, int64_t m, int64_t w, int64_t row0, int mode,
                  int* piv, int* info, hipStream_t s) {
-  hipLaunchKernelGGL((panel_kernel<R, W>), dim3(1), dim3(kThreads), 0, s, P, ldp, (int)m,
-                     (int)w, (int)row0, mode, piv, info);
+  hipLaunchKernelGGL((panel_kernel<R, W>), dim3(1), dim3(kThreads), stage_bytes<W>(), s, P, ldp,
+                     (int)m, (int)w, (int)row0, mode, piv, info, nullptr);
   HIP_TRY(hipGetLastError());
   return GELIM_OK;
 }
@@ -267,6 +401,37 @@ extern "C" int gelim_gpu_panel_factor(double* dP, int64_t ldp, int64_t m, int64_
                                       int64_t row0, int pivot, int32_t* dpiv, int32_t* dinfo,
                                       void* stream) {
   return gelim::panel_factor(dP, ldp, m, w, row0, pivot, dpiv, dinfo, (hipStream_t)stream);
+}
+
+// Diagnostic: run the stamped panel kernel once on a random m x 16 panel and
+// return {t_load, t_steps, t_store} in shader cycles (plus total).
+extern "C" int gelim_debug_panel_stamps(int64_t m, int64_t w, unsigned long long* out4) {
+  using namespace gelim;
+  double* P = nullptr;
+  int *piv = nullptr, *info = nullptr;
+  unsigned long long* st = nullptr;
+  HIP_TRY(hipMalloc((void**)&P, sizeof(double) * m * 16));
+  HIP_TRY(hipMalloc((void**)&piv, sizeof(int) * 64));
+  HIP_TRY(hipMalloc((void**)&info, 16));
+  HIP_TRY(hipMalloc((void**)&st, 64));
+  std::vector<double> h(m * 16);
+  for (size_t i = 0; i < h.size(); ++i) h[i] = (double)((i * 2654435761u) % 1000) / 997.0 - 0.5;
+  HIP_TRY(hipMemcpy(P, h.data(), h.size() * 8, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemset(info, 0, 16));
+  for (int rep = 0; rep < 3; ++rep) {
+    if (m <= 256) hipLaunchKernelGGL((panel_kernel<1, 16, true>), 1, kThreads, stage_bytes<16>(), 0, P, 16, (int)m, (int)w, 0, 1, piv, info, st);
+    else if (m <= 1024) hipLaunchKernelGGL((panel_kernel<4, 16, true>), 1, kThreads, stage_bytes<16>(), 0, P, 16, (int)m, (int)w, 0, 1, piv, info, st);
+    else hipLaunchKernelGGL((panel_kernel<8, 16, true>), 1, kThreads, stage_bytes<16>(), 0, P, 16, (int)m, (int)w, 0, 1, piv, info, st);
+    HIP_TRY(hipDeviceSynchronize());
+  }
+  unsigned long long hs[8];
+  HIP_TRY(hipMemcpy(hs, st, 64, hipMemcpyDeviceToHost));
+  out4[0] = hs[1] - hs[0];
+  out4[1] = hs[2] - hs[1];
+  out4[2] = hs[3] - hs[2];
+  out4[3] = hs[3] - hs[0];
+  (void)hipFree(P); (void)hipFree(piv); (void)hipFree(info); (void)hipFree(st);
+  return GELIM_OK;
 }
 
 extern "C" int64_t gelim_gpu_panel_max_rows(int64_t w) {  // rows per width

@@ -1,0 +1,70 @@
+"""Worker bodies for the multi-process tests (spawned by tests/test_dist_cpu.py
+and tests/test_gpu_dist.py).  Each worker joins a gloo (CPU) or nccl/RCCL
+(GPU) group on 127.0.0.1 and writes its result to a file."""
+import os
+import sys
+import traceback
+from pathlib import Path
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+
+
+def _init(rank, world, port, device):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK="0" if device == "cuda" else str(rank),
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    from gelim.parallel import comm as C
+
+    return C.init_from_env(device=device if device == "cpu" else "cuda:0", timeout_s=120)
+
+
+def gauss(rank, world, port, outdir, n, block, seed, device, mode):
+    import torch
+
+    import gelim
+    from gelim.parallel import DistributedGauss
+    from gelim.parallel import comm as C
+
+    try:
+        comm = _init(rank, world, port, device)
+        dg = DistributedGauss(comm, n, block=block)
+        if mode == "random":
+            loc = dg.generate_random(seed=seed)
+        else:
+            aug = gelim.utils.io.load_fixture(mode)
+            loc = dg.scatter_from_global(gelim.augment_with_rhs(aug))
+        x = dg.solve_(loc)
+        torch.save(x.cpu(), Path(outdir) / f"x{rank}.pt")
+        C.destroy()
+    except Exception:
+        (Path(outdir) / f"err{rank}.txt").write_text(traceback.format_exc())
+        raise
+
+
+def matmul(rank, world, port, outdir, M, K, N, algo, device):
+    import torch
+
+    from gelim.parallel import comm as C
+    from gelim.parallel.dist_matmul import grid_shape, ring_matmul, summa_matmul
+
+    try:
+        comm = _init(rank, world, port, device)
+        g = torch.Generator().manual_seed(5)
+        A = torch.randn(M, K, generator=g)
+        B = torch.randn(K, N, generator=g)
+        dev = comm.device
+        if algo == "ring":
+            rows = M // world
+            kb = K // world
+            C_loc = ring_matmul(comm, A[rank * rows:(rank + 1) * rows].to(dev).contiguous(),
+                                B[rank * kb:(rank + 1) * kb].to(dev).contiguous())
+        else:
+            pr, pc = grid_shape(world)
+            i, j = divmod(rank, pc)
+            mb, ka, kbr, nb = M // pr, K // pc, K // pr, N // pc
+            C_loc = summa_matmul(comm, A[i * mb:(i + 1) * mb, j * ka:(j + 1) * ka].to(dev).contiguous(),
+                                 B[i * kbr:(i + 1) * kbr, j * nb:(j + 1) * nb].to(dev).contiguous(), (pr, pc))
+        torch.save(C_loc.cpu(), Path(outdir) / f"c{rank}.pt")
+        C.destroy()
+    except Exception:
+        (Path(outdir) / f"err{rank}.txt").write_text(traceback.format_exc())
+        raise

@@ -97,6 +97,17 @@ __device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
   return ((uint64_t)hi << 32) | lo;
 }
 
+// 32-bit unsigned max over the wave (identity 0); result uniform.
+__device__ __forceinline__ unsigned wave_max_u32(unsigned v) {
+  v = max(v, dpp_u32<kDppRowShr1, 0xf, 0xf>(0u, v));
+  v = max(v, dpp_u32<kDppRowShr2, 0xf, 0xf>(0u, v));
+  v = max(v, dpp_u32<kDppRowShr4, 0xf, 0xf>(0u, v));
+  v = max(v, dpp_u32<kDppRowShr8, 0xf, 0xf>(0u, v));
+  v = max(v, dpp_u32<kDppRowBcast15, 0xa, 0xf>(0u, v));
+  v = max(v, dpp_u32<kDppRowBcast31, 0xc, 0xf>(0u, v));
+  return (unsigned)__builtin_amdgcn_readlane((int)v, 63);
+}
+
 // 32-bit unsigned min over the wave (identity 0xffffffff); result uniform.
 __device__ __forceinline__ unsigned wave_min_u32(unsigned v) {
   v = min(v, dpp_u32<kDppRowShr1, 0xf, 0xf>(0xffffffffu, v));
@@ -135,6 +146,20 @@ __device__ __forceinline__ uint64_t pivot_ukey(T a, bool is_diag, int mode) {
   }
   if (a == T(0)) return 1;
   return is_diag ? 3 : 2;
+}
+
+// Branchless pivot key for a compile-time rule (MODE 1 = PARTIAL, 0 = ZERO):
+// 0 = not a candidate.
+template <int MODE>
+__device__ __forceinline__ uint64_t pivot_ukey_t(double a, bool is_diag, bool ok) {
+  if constexpr (MODE == 1) {
+    const uint64_t bits = (uint64_t)__double_as_longlong(a) & 0x7fffffffffffffffull;
+    const bool nan = bits > 0x7ff0000000000000ull;
+    return (ok && !nan) ? bits + 1 : 0;
+  } else {
+    const uint64_t k = (a == 0.0) ? 1 : (is_diag ? 3 : 2);
+    return ok ? k : 0;
+  }
 }
 
 }  // namespace dev

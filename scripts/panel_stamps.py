@@ -13,6 +13,6 @@ f.restype = C.c_int
 print("m w load_cyc steps_cyc store_cyc total_cyc steps_per_col")
 for m in (200, 1000, 2048):
     for w in (1, 2, 4, 8, 16):
-        out = (C.c_ulonglong * 4)()
+        out = (C.c_ulonglong * 9)()
         gelim._native.check(f(m, w, out))
-        print(m, w, out[0], out[1], out[2], out[3], out[1] / w)
+        print(m, w, out[0], out[1], out[2], out[3], out[1] / w, "step4:", list(out[4:9]))

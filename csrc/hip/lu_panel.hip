@@ -274,7 +274,8 @@ template <int NT, int R, int W, int MODE, bool STAMP = false>
 __global__ __launch_bounds__(NT) void panel_kernel(double* __restrict__ P, int64_t ldp, int m,
                                                    int w, int row0, int* __restrict__ piv,
                                                    int* __restrict__ info,
-                                                   unsigned long long* __restrict__ stamps) {
+                                                   unsigned long long* __restrict__ stamps,
+                                                   int* __restrict__ pairs) {
   using K = Panel<NT, R, W, MODE, STAMP>;
   __shared__ PanelLds<W> sh;
   const int t = threadIdx.x;
@@ -333,6 +334,25 @@ __global__ __launch_bounds__(NT) void panel_kernel(double* __restrict__ P, int64
       sh.pos_of[other] = cur;
       sh.piv[j] = cur < w ? cur : sh.sel[cur - w];
     }
+    // net row movement as (dst, src) pairs for the trailing-column kernels:
+    // new_row[dst] = old_row[src] over the <= 2w touched rows
+    if (pairs) {
+      int np = 0;
+      for (int x = 0; x < 2 * w; ++x) {
+        // compact position w+j stands for actual position sel[j] only when
+        // that row lies below the panel top (otherwise it is unused)
+        if (x >= w && sh.sel[x - w] < w) continue;
+        const int ap = x < w ? x : sh.sel[x - w];
+        const int id = sh.row_at[x];
+        const int ar = id < w ? id : sh.sel[id - w];
+        if (ap != ar) {
+          pairs[1 + 2 * np] = ap;
+          pairs[2 + 2 * np] = ar;
+          ++np;
+        }
+      }
+      pairs[0] = np;
+    }
   }
   __syncthreads();
 
@@ -384,14 +404,14 @@ __global__ __launch_bounds__(NT) void panel_kernel(double* __restrict__ P, int64
 
 template <int NT, int R, int W>
 int launch_panel(double* P, int64_t ldp, int64_t m, int64_t w, int64_t row0, int mode, int* piv,
-                 int* info, hipStream_t s) {
+                 int* info, int* pairs, hipStream_t s) {
   constexpr size_t lds = Panel<NT, R, W, 1, false>::stage_bytes();
   if (mode == GELIM_PIVOT_PARTIAL)
     hipLaunchKernelGGL((panel_kernel<NT, R, W, 1>), dim3(1), dim3(NT), lds, s, P, ldp, (int)m,
-                       (int)w, (int)row0, piv, info, nullptr);
+                       (int)w, (int)row0, piv, info, nullptr, pairs);
   else
     hipLaunchKernelGGL((panel_kernel<NT, R, W, 0>), dim3(1), dim3(NT), lds, s, P, ldp, (int)m,
-                       (int)w, (int)row0, piv, info, nullptr);
+                       (int)w, (int)row0, piv, info, nullptr, pairs);
   HIP_TRY(hipGetLastError());
   return GELIM_OK;
 }
@@ -409,14 +429,14 @@ int64_t panel_width_for(int64_t m) {
 }
 
 int panel_factor(double* P, int64_t ldp, int64_t m, int64_t w, int64_t row0, int mode, int* piv,
-                 int* info, hipStream_t s) {
+                 int* info, hipStream_t s, int* pairs) {
   if (m <= 0 || w <= 0 || w > m) return GELIM_FAIL(GELIM_E_ARG, "panel: bad m/w");
-  if (m <= 512 && w <= 16) return launch_panel<512, 1, 16>(P, ldp, m, w, row0, mode, piv, info, s);
-  if (m <= 1024 && w <= 16) return launch_panel<512, 2, 16>(P, ldp, m, w, row0, mode, piv, info, s);
-  if (m <= 2048 && w <= 16) return launch_panel<512, 4, 16>(P, ldp, m, w, row0, mode, piv, info, s);
-  if (m <= 4096 && w <= 8) return launch_panel<512, 8, 8>(P, ldp, m, w, row0, mode, piv, info, s);
-  if (m <= 8192 && w <= 4) return launch_panel<512, 16, 4>(P, ldp, m, w, row0, mode, piv, info, s);
-  if (m <= 16384 && w <= 2) return launch_panel<512, 32, 2>(P, ldp, m, w, row0, mode, piv, info, s);
+  if (m <= 512 && w <= 16) return launch_panel<512, 1, 16>(P, ldp, m, w, row0, mode, piv, info, pairs, s);
+  if (m <= 1024 && w <= 16) return launch_panel<512, 2, 16>(P, ldp, m, w, row0, mode, piv, info, pairs, s);
+  if (m <= 2048 && w <= 16) return launch_panel<512, 4, 16>(P, ldp, m, w, row0, mode, piv, info, pairs, s);
+  if (m <= 4096 && w <= 8) return launch_panel<512, 8, 8>(P, ldp, m, w, row0, mode, piv, info, pairs, s);
+  if (m <= 8192 && w <= 4) return launch_panel<512, 16, 4>(P, ldp, m, w, row0, mode, piv, info, pairs, s);
+  if (m <= 16384 && w <= 2) return launch_panel<512, 32, 2>(P, ldp, m, w, row0, mode, piv, info, pairs, s);
   return GELIM_FAIL(GELIM_E_ARG, "panel: m=" + std::to_string(m) + " w=" + std::to_string(w) +
                                      " exceeds the register-resident panel");
 }
@@ -425,7 +445,7 @@ int panel_factor(double* P, int64_t ldp, int64_t m, int64_t w, int64_t row0, int
 
 extern "C" int gelim_gpu_panel_factor(double* dP, int64_t ldp, int64_t m, int64_t w, int64_t row0,
                                       int pivot, int32_t* dpiv, int32_t* dinfo, void* stream) {
-  return gelim::panel_factor(dP, ldp, m, w, row0, pivot, dpiv, dinfo, (hipStream_t)stream);
+  return gelim::panel_factor(dP, ldp, m, w, row0, pivot, dpiv, dinfo, (hipStream_t)stream, nullptr);
 }
 
 // Diagnostic: run the stamped panel kernel on an m x 16 panel (w columns
@@ -449,13 +469,13 @@ extern "C" int gelim_debug_panel_stamps(int64_t m, int64_t w, unsigned long long
   for (int rep = 0; rep < 3; ++rep) {
     if (m <= 512)
       hipLaunchKernelGGL((panel_kernel<512, 1, 16, 1, true>), 1, 512, lds, 0, P, 16, (int)m,
-                         (int)w, 0, piv, info, st);
+                         (int)w, 0, piv, info, st, nullptr);
     else if (m <= 1024)
       hipLaunchKernelGGL((panel_kernel<512, 2, 16, 1, true>), 1, 512, lds, 0, P, 16, (int)m,
-                         (int)w, 0, piv, info, st);
+                         (int)w, 0, piv, info, st, nullptr);
     else
       hipLaunchKernelGGL((panel_kernel<512, 4, 16, 1, true>), 1, 512, lds, 0, P, 16, (int)m,
-                         (int)w, 0, piv, info, st);
+                         (int)w, 0, piv, info, st, nullptr);
     HIP_TRY(hipDeviceSynchronize());
   }
   unsigned long long hs[32];

@@ -116,6 +116,60 @@ __global__ __launch_bounds__(kSwapThreads) void swap_trsm_kernel(
   }
 }
 
+// Pair-list form used by the solver plan: the panel kernel already emitted
+// the net row movement (pairs[0] = count, then (dst, src) per pair), so there
+// is no per-block reconstruction.  Per column (one thread): every touched
+// source row is loaded before anything is stored, the top w rows are staged
+// in this thread's LDS column for the triangular solve, other destinations
+// are written straight back.
+template <int W>
+__global__ __launch_bounds__(kSwapThreads) void pairs_trsm_kernel(
+    double* __restrict__ C, int64_t ldc, int ncols, const double* __restrict__ L, int64_t ldl,
+    int w, const int* __restrict__ pairs) {
+  __shared__ double s_L[W][W];
+  __shared__ double xs[W][kSwapThreads];
+  __shared__ int s_pair[1 + 4 * W];
+  const int t = threadIdx.x;
+  for (int e = t; e < W * W; e += kSwapThreads) {
+    const int r = e / W, c = e % W;
+    s_L[r][c] = (c < r && r < w) ? L[(int64_t)r * ldl + c] : 0.0;
+  }
+  if (t < 1 + 4 * W) s_pair[t] = (t == 0 || t <= 2 * pairs[0]) ? pairs[t] : 0;
+  __syncthreads();
+  const int np = s_pair[0];
+  const int64_t c = (int64_t)blockIdx.x * kSwapThreads + t;
+  if (c >= ncols) return;
+  double* col = C + c;
+  double g[2 * W];
+#pragma unroll
+  for (int e = 0; e < 2 * W; ++e)
+    g[e] = (e < np) ? col[(int64_t)s_pair[2 + 2 * e] * ldc] : 0.0;
+  const double* pl = col;
+#pragma unroll
+  for (int j = 0; j < W; ++j, pl += ldc) xs[j][t] = (j < w) ? *pl : 0.0;
+#pragma unroll
+  for (int e = 0; e < 2 * W; ++e) {
+    if (e < np) {
+      const int d = s_pair[1 + 2 * e];
+      if (d < w) xs[d][t] = g[e];
+      else col[(int64_t)d * ldc] = g[e];
+    }
+  }
+  double x[W];
+#pragma unroll
+  for (int j = 0; j < W; ++j) x[j] = xs[j][t];
+  double* ps = col;
+#pragma unroll
+  for (int i = 0; i < W; ++i) {
+    __builtin_amdgcn_sched_barrier(0);
+    const double xi = x[i];
+    if (i < w) *ps = xi;  // final U12 row i
+    ps += ldc;
+#pragma unroll
+    for (int j = i + 1; j < W; ++j) x[j] -= s_L[j][i] * xi;
+  }
+}
+
 // ---- fp64 MFMA GEMM: C -= L * U --------------------------------------------
 // Workgroup tile 64x64, 4 waves as 2x2, each wave 32x32 = 2x2 blocks of the
 // 16x16x4 f64 MFMA.  Operand maps (gfx950, f64): A lane l holds
@@ -201,6 +255,23 @@ int swap_trsm(double* C, int64_t ldc, int64_t ncols, const double* L, int64_t ld
   if (w <= 16) return launch_swap_trsm<16>(C, ldc, ncols, L, ldl, w, piv, tmp, s);
   if (w <= 32) return launch_swap_trsm<32>(C, ldc, ncols, L, ldl, w, piv, tmp, s);
   return GELIM_FAIL(GELIM_E_ARG, "swap_trsm: w > 32");
+}
+
+int pairs_trsm(double* C, int64_t ldc, int64_t ncols, const double* L, int64_t ldl, int64_t w,
+               const int* pairs, hipStream_t s) {
+  if (ncols <= 0) return GELIM_OK;
+  const int blocks = (int)((ncols + kSwapThreads - 1) / kSwapThreads);
+#define GELIM_PT(WW)                                                                        \
+  hipLaunchKernelGGL((pairs_trsm_kernel<WW>), dim3(blocks), dim3(kSwapThreads), 0, s, C, ldc, \
+                     (int)ncols, L, ldl, (int)w, pairs)
+  if (w <= 2) GELIM_PT(2);
+  else if (w <= 4) GELIM_PT(4);
+  else if (w <= 8) GELIM_PT(8);
+  else if (w <= 16) GELIM_PT(16);
+  else return GELIM_FAIL(GELIM_E_ARG, "pairs_trsm: w > 16");
+#undef GELIM_PT
+  HIP_TRY(hipGetLastError());
+  return GELIM_OK;
 }
 
 int gemm_update(double* C, int64_t ldc, const double* L, int64_t ldl, const double* U,

@@ -9,13 +9,16 @@
 
 #include <algorithm>
 #include <string>
+#include <vector>
 
 #include "gelim/internal.h"
 
 namespace gelim {
 int64_t panel_width_for(int64_t m);
 int panel_factor(double* P, int64_t ldp, int64_t m, int64_t w, int64_t row0, int mode, int* piv,
-                 int* info, hipStream_t s);
+                 int* info, hipStream_t s, int* pairs);
+int pairs_trsm(double* C, int64_t ldc, int64_t ncols, const double* L, int64_t ldl, int64_t w,
+               const int* pairs, hipStream_t s);
 int swap_trsm(double* C, int64_t ldc, int64_t ncols, const double* L, int64_t ldl, int64_t w,
               const int* piv, double* tmp, hipStream_t s);
 int gemm_update(double* C, int64_t ldc, const double* L, int64_t ldl, const double* U,
@@ -40,6 +43,10 @@ struct gelim_gauss_plan {
   void* mcol = nullptr;
   double* tmp = nullptr;
   hipStream_t cap = nullptr;
+  hipStream_t side = nullptr;            // lookahead: wide trailing updates
+  std::vector<hipEvent_t> ev_panel, ev_wide;
+  std::vector<int64_t> step_k, step_w;   // blocked schedule
+  int* pairs = nullptr;                  // per-step net row movement
   hipGraphExec_t exec = nullptr;
   const void* k_src = nullptr;
   int64_t k_ld = 0;
@@ -48,6 +55,8 @@ struct gelim_gauss_plan {
 };
 
 namespace {
+
+constexpr int64_t kPairSlot = 72;  // 1 + 4*16 ints, padded
 
 int enqueue(gelim_gauss_plan* p, const void* src, int64_t src_ld, void* dx, void* bnorm,
             hipStream_t s) {
@@ -58,20 +67,42 @@ int enqueue(gelim_gauss_plan* p, const void* src, int64_t src_ld, void* dx, void
                              hipMemcpyDeviceToDevice, s));
   HIP_TRY(hipMemsetAsync(p->info, 0, 16, s));
   if (p->algo == GELIM_GPU_BLOCKED) {
+    // Right-looking blocked LU with lookahead 1.  Critical stream s:
+    //   panel(i) -> [wait wide(i-1)] -> narrow(i) -> panel(i+1) -> ...
+    // where narrow(i) applies panel i to the NEXT panel's columns only;
+    // side stream: [wait panel(i)] -> wide(i) = panel i applied to every
+    // column right of the next panel (incl. b).  The wide GEMM of step i
+    // runs under the single-CU panel factorisation of step i+1.
     double* A = static_cast<double*>(p->work);
-    for (int64_t k = 0; k < n;) {
-      const int64_t m = n - k;
-      const int64_t w = std::min<int64_t>(panel_width_for(m), m);
-      if (w <= 0) return GELIM_FAIL(GELIM_E_ARG, "matrix too tall for the register panel");
-      GELIM_TRY(panel_factor(A + k * lda + k, lda, m, w, k, p->pivot, p->piv + k, p->info, s));
-      const int64_t ncols = (n + 1) - (k + w);
-      GELIM_TRY(swap_trsm(A + k * lda + k + w, lda, ncols, A + k * lda + k, lda, w, p->piv + k,
-                          p->tmp, s));
-      if (m > w)
-        GELIM_TRY(gemm_update(A + (k + w) * lda + (k + w), lda, A + (k + w) * lda + k, lda,
-                              A + k * lda + k + w, lda, m - w, ncols, w, s));
-      k += w;
+    const size_t S = p->step_k.size();
+    HIP_TRY(hipEventRecord(p->ev_wide[S], s));  // fork: side joins the stream/capture
+    HIP_TRY(hipStreamWaitEvent(p->side, p->ev_wide[S], 0));
+    for (size_t i = 0; i < S; ++i) {
+      const int64_t k = p->step_k[i], w = p->step_w[i], m = n - k;
+      int* pr = p->pairs + i * kPairSlot;
+      GELIM_TRY(panel_factor(A + k * lda + k, lda, m, w, k, p->pivot, p->piv + k, p->info, s, pr));
+      HIP_TRY(hipEventRecord(p->ev_panel[i], s));
+      const int64_t kn = k + w;                                // next panel's first column
+      const int64_t wn = (i + 1 < S) ? p->step_w[i + 1] : 0;  // next panel's width
+      // side: wide update of columns [kn + wn, n] (b included)
+      HIP_TRY(hipStreamWaitEvent(p->side, p->ev_panel[i], 0));
+      const int64_t wc0 = kn + wn, wcols = (n + 1) - wc0;
+      if (wcols > 0) {
+        GELIM_TRY(pairs_trsm(A + k * lda + wc0, lda, wcols, A + k * lda + k, lda, w, pr, p->side));
+        if (m > w)
+          GELIM_TRY(gemm_update(A + kn * lda + wc0, lda, A + kn * lda + k, lda, A + k * lda + wc0,
+                                lda, m - w, wcols, w, p->side));
+      }
+      HIP_TRY(hipEventRecord(p->ev_wide[i], p->side));
+      // critical: narrow update of the next panel's columns [kn, kn + wn)
+      if (wn > 0) {
+        if (i > 0) HIP_TRY(hipStreamWaitEvent(s, p->ev_wide[i - 1], 0));
+        GELIM_TRY(pairs_trsm(A + k * lda + kn, lda, wn, A + k * lda + k, lda, w, pr, s));
+        GELIM_TRY(gemm_update(A + kn * lda + kn, lda, A + kn * lda + k, lda, A + k * lda + kn, lda,
+                              m - w, wn, w, s));
+      }
     }
+    HIP_TRY(hipStreamWaitEvent(s, p->ev_wide[S - 1], 0));  // join
     return backsub_f64(A, lda, A + n, lda, static_cast<double*>(dx),
                        static_cast<double*>(bnorm), n, 0, p->yw, s);
   }
@@ -128,6 +159,22 @@ extern "C" gelim_gauss_plan* gelim_gauss_plan_create(int64_t n, int algo, int pi
   if (hipMalloc((void**)&p->tmp, (size_t)2 * 32 * (n + 1) * sizeof(double)) != hipSuccess)
     return fail("tmp");
   if (hipStreamCreateWithFlags(&p->cap, hipStreamNonBlocking) != hipSuccess) return fail("stream");
+  if (algo == GELIM_GPU_BLOCKED) {
+    for (int64_t k = 0; k < n;) {
+      const int64_t w = std::min<int64_t>(gelim::panel_width_for(n - k), n - k);
+      p->step_k.push_back(k);
+      p->step_w.push_back(w);
+      k += w;
+    }
+    const size_t S = p->step_k.size();
+    if (hipStreamCreateWithFlags(&p->side, hipStreamNonBlocking) != hipSuccess) return fail("side");
+    p->ev_panel.assign(S, nullptr);
+    p->ev_wide.assign(S + 1, nullptr);
+    for (auto* v : {&p->ev_panel, &p->ev_wide})
+      for (auto& e : *v)
+        if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return fail("event");
+    if (hipMalloc((void**)&p->pairs, sizeof(int) * kPairSlot * S) != hipSuccess) return fail("pairs");
+  }
   (void)hipMemset(p->work, 0, (size_t)(n * p->lda * dtype_bytes));
   return p;
 }
@@ -136,6 +183,11 @@ extern "C" void gelim_gauss_plan_destroy(gelim_gauss_plan* p) {
   if (!p) return;
   if (p->exec) (void)hipGraphExecDestroy(p->exec);
   if (p->cap) (void)hipStreamDestroy(p->cap);
+  if (p->side) (void)hipStreamDestroy(p->side);
+  for (auto* v : {&p->ev_panel, &p->ev_wide})
+    for (auto& e : *v)
+      if (e) (void)hipEventDestroy(e);
+  (void)hipFree(p->pairs);
   (void)hipFree(p->work);
   (void)hipFree(p->piv);
   (void)hipFree(p->info);

@@ -43,6 +43,7 @@ def parse():
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--n", type=int, default=2048)
     p.add_argument("--backend", default="hip", choices=["hip", "hip-pivot"])
+    p.add_argument("--graph", type=int, default=0, help="replay the solve from a hipGraph (1) or launch eagerly (0)")
     p.add_argument("--no-matmul", action="store_true")
     p.add_argument("--extras", action="store_true",
                    help="also time the distributed 8192^2 solve and 16384^2 ring matmul (N>1)")
@@ -68,7 +69,7 @@ def main() -> None:
 
     # -- Gauss: one independent system per GPU --------------------------------
     src = gelim.random_system(n, seed=1234 + rank, device=dev)
-    solver = gelim.GaussSolver(n, backend=args.backend, pivot="partial", device=dev)
+    solver = gelim.GaussSolver(n, backend=args.backend, pivot="partial", device=dev, use_graph=bool(args.graph))
     x = None
     for _ in range(args.warmup):
         x = solver.solve(src)
@@ -114,6 +115,7 @@ def main() -> None:
         seq = json.loads(HOST_SEQ_FILE.read_text())
 
     extras = {}
+    solver.close()
     if args.extras and N > 1:
         extras = run_extras(comm, gelim, torch)
 

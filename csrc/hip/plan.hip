@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <string>
 #include <vector>
 
@@ -47,6 +48,7 @@ struct gelim_gauss_plan {
   std::vector<hipEvent_t> ev_panel, ev_wide;
   std::vector<int64_t> step_k, step_w;   // blocked schedule
   int* pairs = nullptr;                  // per-step net row movement
+  bool lookahead = false;                // GELIM_LOOKAHEAD=1: side-stream wide updates
   hipGraphExec_t exec = nullptr;
   const void* k_src = nullptr;
   int64_t k_ld = 0;
@@ -75,34 +77,38 @@ int enqueue(gelim_gauss_plan* p, const void* src, int64_t src_ld, void* dx, void
     // runs under the single-CU panel factorisation of step i+1.
     double* A = static_cast<double*>(p->work);
     const size_t S = p->step_k.size();
-    HIP_TRY(hipEventRecord(p->ev_wide[S], s));  // fork: side joins the stream/capture
-    HIP_TRY(hipStreamWaitEvent(p->side, p->ev_wide[S], 0));
+    const bool la = p->lookahead;
+    hipStream_t side = la ? p->side : s;
+    if (la) {
+      HIP_TRY(hipEventRecord(p->ev_wide[S], s));  // fork: side joins the stream/capture
+      HIP_TRY(hipStreamWaitEvent(side, p->ev_wide[S], 0));
+    }
     for (size_t i = 0; i < S; ++i) {
       const int64_t k = p->step_k[i], w = p->step_w[i], m = n - k;
       int* pr = p->pairs + i * kPairSlot;
       GELIM_TRY(panel_factor(A + k * lda + k, lda, m, w, k, p->pivot, p->piv + k, p->info, s, pr));
-      HIP_TRY(hipEventRecord(p->ev_panel[i], s));
-      const int64_t kn = k + w;                                // next panel's first column
-      const int64_t wn = (i + 1 < S) ? p->step_w[i + 1] : 0;  // next panel's width
+      if (la) HIP_TRY(hipEventRecord(p->ev_panel[i], s));
+      const int64_t kn = k + w;                                      // next panel's first column
+      const int64_t wn = (la && i + 1 < S) ? p->step_w[i + 1] : 0;  // narrow width (lookahead only)
       // side: wide update of columns [kn + wn, n] (b included)
-      HIP_TRY(hipStreamWaitEvent(p->side, p->ev_panel[i], 0));
+      if (la) HIP_TRY(hipStreamWaitEvent(side, p->ev_panel[i], 0));
       const int64_t wc0 = kn + wn, wcols = (n + 1) - wc0;
       if (wcols > 0) {
-        GELIM_TRY(pairs_trsm(A + k * lda + wc0, lda, wcols, A + k * lda + k, lda, w, pr, p->side));
+        GELIM_TRY(pairs_trsm(A + k * lda + wc0, lda, wcols, A + k * lda + k, lda, w, pr, side));
         if (m > w)
           GELIM_TRY(gemm_update(A + kn * lda + wc0, lda, A + kn * lda + k, lda, A + k * lda + wc0,
-                                lda, m - w, wcols, w, p->side));
+                                lda, m - w, wcols, w, side));
       }
-      HIP_TRY(hipEventRecord(p->ev_wide[i], p->side));
+      if (la) HIP_TRY(hipEventRecord(p->ev_wide[i], side));
       // critical: narrow update of the next panel's columns [kn, kn + wn)
       if (wn > 0) {
-        if (i > 0) HIP_TRY(hipStreamWaitEvent(s, p->ev_wide[i - 1], 0));
+        if (la && i > 0) HIP_TRY(hipStreamWaitEvent(s, p->ev_wide[i - 1], 0));
         GELIM_TRY(pairs_trsm(A + k * lda + kn, lda, wn, A + k * lda + k, lda, w, pr, s));
         GELIM_TRY(gemm_update(A + kn * lda + kn, lda, A + kn * lda + k, lda, A + k * lda + kn, lda,
                               m - w, wn, w, s));
       }
     }
-    HIP_TRY(hipStreamWaitEvent(s, p->ev_wide[S - 1], 0));  // join
+    if (la) HIP_TRY(hipStreamWaitEvent(s, p->ev_wide[S - 1], 0));  // join
     return backsub_f64(A, lda, A + n, lda, static_cast<double*>(dx),
                        static_cast<double*>(bnorm), n, 0, p->yw, s);
   }
@@ -159,6 +165,7 @@ extern "C" gelim_gauss_plan* gelim_gauss_plan_create(int64_t n, int algo, int pi
   if (hipMalloc((void**)&p->tmp, (size_t)2 * 32 * (n + 1) * sizeof(double)) != hipSuccess)
     return fail("tmp");
   if (hipStreamCreateWithFlags(&p->cap, hipStreamNonBlocking) != hipSuccess) return fail("stream");
+  if (const char* e = std::getenv("GELIM_LOOKAHEAD")) p->lookahead = std::atoi(e) != 0;
   if (algo == GELIM_GPU_BLOCKED) {
     for (int64_t k = 0; k < n;) {
       const int64_t w = std::min<int64_t>(gelim::panel_width_for(n - k), n - k);

@@ -107,6 +107,12 @@ class GaussSolver:
             self._plan = None
 
     def __del__(self):
+        # never tear down HIP objects during interpreter shutdown (the HIP
+        # runtime may already be gone); explicit close() is the normal path
+        import sys
+
+        if sys.is_finalizing():
+            return
         try:
             self.close()
         except Exception:

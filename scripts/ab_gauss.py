@@ -1,0 +1,37 @@
+"""A/B timing of GaussSolver variants in ONE process (interleaved rounds)."""
+import os
+import statistics
+import sys
+import time
+from pathlib import Path
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+import torch  # noqa: E402
+
+import gelim  # noqa: E402
+
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 2048
+dev = torch.device("cuda:0")
+src = gelim.random_system(n, seed=1234, device=dev)
+variants = {}
+for la in ("1", "0"):
+    for g in (True, False):
+        os.environ["GELIM_LOOKAHEAD"] = la
+        variants[f"lookahead={la} graph={int(g)}"] = gelim.GaussSolver(n, "hip", device=dev, use_graph=g)
+variants["hip-pivot"] = gelim.GaussSolver(n, "hip-pivot", device=dev)
+res = {k: [] for k in variants}
+for s in variants.values():
+    for _ in range(3):
+        s.solve(src)
+torch.cuda.synchronize()
+for rnd in range(5):
+    for k, s in variants.items():
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(5):
+            x = s.solve(src)
+        torch.cuda.synchronize()
+        res[k].append((time.perf_counter() - t0) / 5)
+        assert gelim.ops.gauss.error_metric(x) < 1e-6, k
+for k, v in res.items():
+    print(f"{k:28s} median {statistics.median(v)*1e3:8.3f} ms  min {min(v)*1e3:8.3f} ms")

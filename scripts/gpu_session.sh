@@ -30,7 +30,7 @@ fi
 if [[ ",$STEPS," == *",prof,"* ]]; then
   export TMPDIR=/tmp
   ( cd /tmp && timeout -k 10 "${PROF_TIMEOUT:-240}" rocprofv3 --kernel-trace --stats --output-format csv \
-      -d "$OUT/prof" -o run -- python3 "$ROOT/bench.py" --steps 5 --warmup 2 --no-matmul > "$OUT/prof.log" 2>&1 )
+      -d "$OUT/prof" -o run -- python3 "$ROOT/bench.py" --steps 5 --warmup 2 --no-matmul ${PROF_BENCH_ARGS:-} > "$OUT/prof.log" 2>&1 )
   rc=$?; echo "rocprof rc=$rc"; tail -3 "$OUT/prof.log"
   find "$OUT/prof" -name "*kernel_stats.csv" | head -3
   if [ $rc -ne 0 ]; then exit $rc; fi

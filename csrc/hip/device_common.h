@@ -149,13 +149,13 @@ __device__ __forceinline__ uint64_t pivot_ukey(T a, bool is_diag, int mode) {
 }
 
 // Branchless pivot key for a compile-time rule (MODE 1 = PARTIAL, 0 = ZERO):
-// 0 = not a candidate.
+// 0 = not a candidate; every live row has a key >= 1 (NaN ranks as zero).
 template <int MODE>
 __device__ __forceinline__ uint64_t pivot_ukey_t(double a, bool is_diag, bool ok) {
   if constexpr (MODE == 1) {
     const uint64_t bits = (uint64_t)__double_as_longlong(a) & 0x7fffffffffffffffull;
-    const bool nan = bits > 0x7ff0000000000000ull;
-    return (ok && !nan) ? bits + 1 : 0;
+    const bool nan = bits > 0x7ff0000000000000ull;  // ranks like zero: a live row always wins
+    return ok ? (nan ? 1 : bits + 1) : 0;
   } else {
     const uint64_t k = (a == 0.0) ? 1 : (is_diag ? 3 : 2);
     return ok ? k : 0;

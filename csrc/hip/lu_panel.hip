@@ -28,6 +28,8 @@
 //  * the panel is read and written once, coalesced, staged through LDS.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <cstdlib>
 #include <utility>
 #include <vector>
 
@@ -41,8 +43,8 @@ constexpr int kMaxWaves = 8;
 
 template <int W>
 struct alignas(16) PanelLds {
-  double cand_row[2][kMaxWaves][W];    // each wave's winning row (parity-buffered)
-  unsigned cand_key[2][kMaxWaves][2];  // {hi, lo} of the wave's winning key
+  double cand_row[2][kMaxWaves][W];       // each wave's winning row (parity-buffered)
+  uint64_t cand_key[2][kMaxWaves];        // the wave's winning key
   unsigned cand_row_idx[2][kMaxWaves];
   int sel[W];         // physical (original) row chosen at each step
   int pos_of[2 * W];  // compact row id -> compact position
@@ -73,11 +75,21 @@ struct StepStamps {
   unsigned long long v[6];
 };
 
+// Exact wave arg-max of (key, row): largest key, lowest row on ties.
+__device__ __forceinline__ void wave_argmax_exact(uint64_t best, unsigned brow, uint64_t& wkey,
+                                                  unsigned& wrow) {
+  wkey = dev::wave_max_u64(best);
+  const uint64_t h2 = __ballot(best == wkey);
+  if (__popcll(h2) == 1)
+    wrow = (unsigned)__builtin_amdgcn_readlane((int)brow, __ffsll((long long)h2) - 1);
+  else
+    wrow = dev::wave_min_u32(best == wkey ? brow : 0xffffffffu);
+}
+
 template <int NT, int R, int W, int MODE, bool STAMP>
 struct Panel {
   static constexpr int kWaves = NT / dev::kWave;
-  static_assert(kWaves <= kMaxWaves, "too many waves");
-  static_assert(R <= 64, "chosen mask is 64 bits");
+  static_assert(kWaves <= kMaxWaves && (kWaves & (kWaves - 1)) == 0, "waves: power of two <= 8");
 
   template <int J>
   static __device__ __forceinline__ void stamp(StepStamps& ss, int slot) {
@@ -87,112 +99,169 @@ struct Panel {
   }
 
   // One column step J (compile time, so every register index is static).
+  // The VALU instruction count per column is what bounds this loop (every
+  // wave executes the whole step; 2 waves share a SIMD at NT = 512), so the
+  // step is written to minimise it: per-slot liveness as lane masks, a
+  // hi-word DPP arg-max with one ballot, a publish of only columns >= J, and
+  // a lane-parallel DPP merge of the per-wave candidates.
   template <int J>
-  static __device__ __forceinline__ void step(double (&a)[R][W], uint64_t& chosen,
-                                              PanelLds<W>& sh, int t, int lane, int wave, int m,
-                                              int w, int row0, int* __restrict__ info,
-                                              StepStamps& ss) {
+  static __device__ __forceinline__ void step(double (&a)[R][W], bool (&live)[R],
+                                              PanelLds<W>& sh, int t, int lane, int wave,
+                                              bool active, int w, int row0,
+                                              int* __restrict__ info, StepStamps& ss) {
     if (J >= w) return;  // uniform across the workgroup
     constexpr int par = J & 1;
     stamp<J>(ss, 0);
 
-    // 1. local candidate over this lane's live rows (not yet chosen, < m)
-    uint64_t best = 0;
-    unsigned brow = 0xffffffffu;
+    uint64_t wkey = 0;
+    unsigned wrow = 0xffffffffu;
+    if (active) {  // uniform per wave: the wave holds panel rows
+      // 1. local candidate over this lane's live rows; its reciprocal is
+      //    computed speculatively (hidden under the DPP ladder) and published
+      //    in place of the pivot value, so no division follows the barrier
+      uint64_t best = 0;
+      unsigned brow = 0xffffffffu;
+      double bval = 0.0;
 #pragma unroll
-    for (int i = 0; i < R; ++i) {
-      const int lr = t + i * NT;
-      const bool ok = !((chosen >> i) & 1) && lr < m;
-      // ZERO rule: the "diagonal" is physical row J (a row chosen earlier is
-      // never the diagonal here — documented difference from a physical-swap
-      // run; PARTIAL pivoting, the accuracy-relevant rule, is exact)
-      const uint64_t key = dev::pivot_ukey_t<MODE>(a[i][J], lr == J, ok);
-      const bool better = key > best;  // increasing rows: '>' keeps the lowest row on ties
-      best = better ? key : best;
-      brow = better ? (unsigned)lr : brow;
-    }
-
-    // 2. wave arg-max: DPP max of the high word, one ballot; exact fallback
-    const unsigned bhi = (unsigned)(best >> 32);
-    const unsigned hmax = dev::wave_max_u32(bhi);
-    const uint64_t holders = __ballot(bhi == hmax);
-    uint64_t wkey;
-    unsigned wrow;
-    if (__popcll(holders) == 1) {
-      const int wl = __ffsll((long long)holders) - 1;
-      wrow = (unsigned)__builtin_amdgcn_readlane((int)brow, wl);
-      wkey = ((uint64_t)hmax << 32) | (unsigned)__builtin_amdgcn_readlane((int)(unsigned)best, wl);
-    } else {
-      wkey = dev::wave_max_u64(best);
-      const uint64_t h2 = __ballot(best == wkey);
-      if (__popcll(h2) == 1)
-        wrow = (unsigned)__builtin_amdgcn_readlane((int)brow, __ffsll((long long)h2) - 1);
-      else
-        wrow = dev::wave_min_u32(best == wkey ? brow : 0xffffffffu);
-    }
-    stamp<J>(ss, 1);
-
-    // the lane holding the wave's winner publishes its row (uniform slot)
-    if (wkey != 0 && (int)(wrow % NT) == t) {
-      const int ip = (int)(wrow / NT);
-#pragma unroll
-      for (int i = 0; i < R; ++i)
-        if (i == ip) {
-#pragma unroll
-          for (int c = 0; c < W; ++c) sh.cand_row[par][wave][c] = opaque(a[i][c]);
+      for (int i = 0; i < R; ++i) {
+        const int lr = t + i * NT;
+        // ZERO rule: the "diagonal" is physical row J (a row chosen earlier is
+        // never the diagonal here — documented difference from a physical-swap
+        // run; PARTIAL pivoting, the accuracy-relevant rule, is exact)
+        const uint64_t key = dev::pivot_ukey_t<MODE>(a[i][J], lr == J, live[i]);
+        const bool better = key > best;  // increasing rows: '>' keeps the lowest row on ties
+        best = better ? key : best;
+        brow = better ? (unsigned)lr : brow;
+        bval = better ? a[i][J] : bval;
+      }
+      const double lrd = (bval != 0.0) ? 1.0 / bval : 0.0;
+      // 2. wave arg-max: DPP max of the high word + one ballot; exact path
+      //    only for high-word ties (or all-zero / denormal columns)
+      if constexpr (MODE == 1) {
+        const unsigned bhi = (unsigned)(best >> 32);
+        const unsigned hmax = dev::wave_max_u32(bhi);
+        const uint64_t holders = __ballot(bhi == hmax);
+        if (hmax != 0 && __popcll(holders) == 1) {
+          const int wl = __ffsll((long long)holders) - 1;
+          wrow = (unsigned)__builtin_amdgcn_readlane((int)brow, wl);
+          wkey = ((uint64_t)hmax << 32) | (unsigned)__builtin_amdgcn_readlane((int)(unsigned)best, wl);
+        } else {
+          wave_argmax_exact(best, brow, wkey, wrow);
         }
+      } else {
+        wave_argmax_exact(best, brow, wkey, wrow);
+      }
+      stamp<J>(ss, 1);
+      // the lane holding the wave's winner publishes columns >= J of its row
+      // (column J carries the reciprocal of the pivot)
+      if (wkey != 0 && (int)(wrow & (NT - 1)) == t) {
+        const int ip = (int)(wrow / NT);
+#pragma unroll
+        for (int i = 0; i < R; ++i)
+          if (i == ip) {
+#pragma unroll
+            for (int c = J & ~1; c < W; c += 2) {
+              // input-only value barrier: keeps one store branch per slot
+              // (a merged select would index a[] dynamically -> scratch)
+              const double x0 = (c == J) ? lrd : a[i][c];
+              const double x1 = (c + 1 == J) ? lrd : a[i][c + 1];
+              asm volatile("" ::"v"(x0), "v"(x1));
+              *reinterpret_cast<double2*>(&sh.cand_row[par][wave][c]) = make_double2(x0, x1);
+            }
+          }
+      }
     }
     if (lane == 0) {
-      sh.cand_key[par][wave][0] = (unsigned)(wkey >> 32);
-      sh.cand_key[par][wave][1] = (unsigned)wkey;
+      sh.cand_key[par][wave] = wkey;
       sh.cand_row_idx[par][wave] = wrow;
     }
     stamp<J>(ss, 2);
     __syncthreads();
     stamp<J>(ss, 3);
 
-    // 3. block winner from the per-wave candidates (broadcast LDS reads)
-    uint64_t gkey = 0;
-    unsigned p = 0xffffffffu;
-#pragma unroll
-    for (int q = 0; q < kWaves; ++q) {
-      const uint64_t k = ((uint64_t)sh.cand_key[par][q][0] << 32) | sh.cand_key[par][q][1];
-      const unsigned r = sh.cand_row_idx[par][q];
-      const bool better = k > gkey || (k == gkey && r < p);
-      gkey = better ? k : gkey;
-      p = better ? r : p;
+    // 3. one LDS round trip: lane q < kWaves reads wave q's key, and every
+    //    lane reads a slice of all candidate rows (LPR lanes per row, DPL
+    //    doubles per lane) — the winner's values are then broadcast with
+    //    v_readlane into SGPRs instead of every wave re-reading the row
+    constexpr int DPL = (W * kWaves >= 128) ? 2 : 1;
+    constexpr int LPR = W / DPL;
+    uint64_t k = sh.cand_key[par][lane & (kWaves - 1)];
+    unsigned r = sh.cand_row_idx[par][lane & (kWaves - 1)];
+    double cv[DPL];
+    {
+      const int q = lane / LPR, c0 = (lane % LPR) * DPL;
+      const int qq = q < kWaves ? q : 0;
+      if constexpr (DPL == 2) {
+        const double2 v = *reinterpret_cast<const double2*>(&sh.cand_row[par][qq][c0]);
+        cv[0] = v.x;
+        cv[1] = v.y;
+      } else {
+        cv[0] = sh.cand_row[par][qq][c0];
+      }
     }
-    const int pw = (int)((p % NT) >> 6);  // wave that published the pivot row
-    const double* u = sh.cand_row[par][pw];
-    const double d = u[J];
-    const double rd = (d != 0.0) ? 1.0 / d : 0.0;
+#pragma unroll
+    for (int sft = 1; sft < kWaves; sft <<= 1) {
+      unsigned khi = (unsigned)(k >> 32), klo = (unsigned)k, k2hi, k2lo, r2;
+      if (sft == 1) {
+        k2hi = dev::dpp_u32<dev::kDppRowShr1, 0xf, 0xf>(0u, khi);
+        k2lo = dev::dpp_u32<dev::kDppRowShr1, 0xf, 0xf>(0u, klo);
+        r2 = dev::dpp_u32<dev::kDppRowShr1, 0xf, 0xf>(0xffffffffu, r);
+      } else if (sft == 2) {
+        k2hi = dev::dpp_u32<dev::kDppRowShr2, 0xf, 0xf>(0u, khi);
+        k2lo = dev::dpp_u32<dev::kDppRowShr2, 0xf, 0xf>(0u, klo);
+        r2 = dev::dpp_u32<dev::kDppRowShr2, 0xf, 0xf>(0xffffffffu, r);
+      } else {
+        k2hi = dev::dpp_u32<dev::kDppRowShr4, 0xf, 0xf>(0u, khi);
+        k2lo = dev::dpp_u32<dev::kDppRowShr4, 0xf, 0xf>(0u, klo);
+        r2 = dev::dpp_u32<dev::kDppRowShr4, 0xf, 0xf>(0xffffffffu, r);
+      }
+      const uint64_t k2 = ((uint64_t)k2hi << 32) | k2lo;
+      const bool better = k2 > k || (k2 == k && r2 < r);
+      k = better ? k2 : k;
+      r = better ? r2 : r;
+    }
+    const uint64_t gkey =
+        ((uint64_t)(unsigned)__builtin_amdgcn_readlane((int)(unsigned)(k >> 32), kWaves - 1) << 32) |
+        (unsigned)__builtin_amdgcn_readlane((int)(unsigned)k, kWaves - 1);
+    const unsigned p = (unsigned)__builtin_amdgcn_readlane((int)r, kWaves - 1);
+    const int pw = (int)((p & (NT - 1)) >> 6);  // wave that published the pivot row
+    auto bcast = [&](int c) -> double {         // u[c] of the pivot row (uniform)
+      const int src = pw * LPR + c / DPL;
+      const uint64_t bits = (uint64_t)__double_as_longlong(cv[c % DPL]);
+      const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(bits >> 32), src);
+      const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)bits, src);
+      return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+    };
+    const double rd = bcast(J);
     double uc[W];
 #pragma unroll
-    for (int c = J + 1; c < W; ++c) uc[c] = u[c];
+    for (int c = J + 1; c < W; ++c) uc[c] = bcast(c);
     if (t == 0) {
       sh.sel[J] = (int)p;
       if (gkey <= 1 && info && *info == 0) *info = row0 + J + 1;  // zero pivot
     }
-    if ((int)(p % NT) == t) chosen |= 1ull << (p / NT);
+#pragma unroll
+    for (int i = 0; i < R; ++i) live[i] = live[i] && (t + i * NT != (int)p);
     stamp<J>(ss, 4);
 
     // 4. multipliers + rank-1 update of every live row (retired rows: l = 0);
     //    column J+1 first — the next step's pivot search depends only on it
-    double l[R];
+    if (active) {
+      double l[R];
 #pragma unroll
-    for (int i = 0; i < R; ++i) {
-      const bool live = !((chosen >> i) & 1);
-      l[i] = live ? a[i][J] * rd : 0.0;
-      a[i][J] = live ? l[i] : a[i][J];
+      for (int i = 0; i < R; ++i) {
+        l[i] = live[i] ? a[i][J] * rd : 0.0;
+        a[i][J] = live[i] ? l[i] : a[i][J];
+      }
+      if constexpr (J + 1 < W) {
+#pragma unroll
+        for (int i = 0; i < R; ++i) a[i][J + 1] = fma(-l[i], uc[J + 1], a[i][J + 1]);
+      }
+#pragma unroll
+      for (int i = 0; i < R; ++i)
+#pragma unroll
+        for (int c = J + 2; c < W; ++c) a[i][c] = fma(-l[i], uc[c], a[i][c]);
     }
-    if constexpr (J + 1 < W) {
-#pragma unroll
-      for (int i = 0; i < R; ++i) a[i][J + 1] = fma(-l[i], uc[J + 1], a[i][J + 1]);
-    }
-#pragma unroll
-    for (int i = 0; i < R; ++i)
-#pragma unroll
-      for (int c = J + 2; c < W; ++c) a[i][c] = fma(-l[i], uc[c], a[i][c]);
     if constexpr (STAMP) {
       if (J == 4) {
         asm volatile("" ::"v"(a[R - 1][W - 1]));
@@ -202,11 +271,11 @@ struct Panel {
   }
 
   template <int... J>
-  static __device__ __forceinline__ void steps(double (&a)[R][W], uint64_t& chosen,
-                                               PanelLds<W>& sh, int t, int lane, int wave, int m,
-                                               int w, int row0, int* info, StepStamps& ss,
-                                               std::integer_sequence<int, J...>) {
-    (step<J>(a, chosen, sh, t, lane, wave, m, w, row0, info, ss), ...);
+  static __device__ __forceinline__ void steps(double (&a)[R][W], bool (&live)[R],
+                                               PanelLds<W>& sh, int t, int lane, int wave,
+                                               bool active, int w, int row0, int* info,
+                                               StepStamps& ss, std::integer_sequence<int, J...>) {
+    (step<J>(a, live, sh, t, lane, wave, active, w, row0, info, ss), ...);
   }
 
   // LDS staging tile: NT rows x W doubles in 16-byte chunks, XOR-swizzled by
@@ -268,16 +337,53 @@ struct Panel {
   }
 
   static constexpr size_t stage_bytes() { return sizeof(double) * NT * W + sizeof(int) * NT; }
+
+  // Direct register IO: every lane moves its own rows with 16-byte accesses;
+  // all R*W/2 requests are in flight at once (one memory latency instead of
+  // R staged passes), at the cost of uncoalesced per-instruction addresses.
+  static __device__ __forceinline__ void load_direct(double (&a)[R][W], const double* __restrict__ P,
+                                                     int64_t ldp, int m, int t) {
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      const int lr = t + i * NT;
+      if (lr < m) {
+        const double2* src = reinterpret_cast<const double2*>(P + (int64_t)lr * ldp);
+#pragma unroll
+        for (int c = 0; c < W / 2; ++c) {
+          const double2 v = src[c];
+          a[i][2 * c] = v.x;
+          a[i][2 * c + 1] = v.y;
+        }
+      } else {
+#pragma unroll
+        for (int c = 0; c < W; ++c) a[i][c] = 0.0;
+      }
+    }
+  }
+
+  static __device__ __forceinline__ void store_direct(const double (&a)[R][W], const int (&dest)[R],
+                                                      double* __restrict__ P, int64_t ldp, int m,
+                                                      int t) {
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      const int lr = t + i * NT;
+      if (lr < m) {
+        double2* dst = reinterpret_cast<double2*>(P + (int64_t)dest[i] * ldp);
+#pragma unroll
+        for (int c = 0; c < W / 2; ++c) dst[c] = make_double2(a[i][2 * c], a[i][2 * c + 1]);
+      }
+    }
+  }
 };
 
-template <int NT, int R, int W, int MODE, bool STAMP = false>
-__global__ __launch_bounds__(NT) void panel_kernel(double* __restrict__ P, int64_t ldp, int m,
-                                                   int w, int row0, int* __restrict__ piv,
-                                                   int* __restrict__ info,
-                                                   unsigned long long* __restrict__ stamps,
-                                                   int* __restrict__ pairs) {
+template <int NT, int R, int W, int MODE, bool STAMP>
+__device__ __forceinline__ void panel_body(double* __restrict__ P, int64_t ldp, int m, int w,
+                                           int row0, int* __restrict__ piv,
+                                           int* __restrict__ info,
+                                           unsigned long long* __restrict__ stamps,
+                                           int* __restrict__ pairs, PanelLds<W>& sh,
+                                           int io = 0) {
   using K = Panel<NT, R, W, MODE, STAMP>;
-  __shared__ PanelLds<W> sh;
   const int t = threadIdx.x;
   const int lane = t & (dev::kWave - 1);
   const int wave = t >> 6;
@@ -288,7 +394,9 @@ __global__ __launch_bounds__(NT) void panel_kernel(double* __restrict__ P, int64
   // full-width panels with 16-byte aligned rows are staged through LDS so the
   // global loads are coalesced (W/2 lanes per row segment)
   const bool staged = (w == W) && (W % 2 == 0) && ((((uintptr_t)P) & 15) == 0) && (ldp % 2 == 0);
-  if (staged) {
+  if (staged && io == 1) {
+    K::load_direct(a, P, ldp, m, t);
+  } else if (staged) {
     K::stage_in(a, P, ldp, m, t);
   } else {
 #pragma unroll
@@ -302,7 +410,10 @@ __global__ __launch_bounds__(NT) void panel_kernel(double* __restrict__ P, int64
       }
     }
   }
-  uint64_t chosen = 0;
+  bool live[R];
+#pragma unroll
+  for (int i = 0; i < R; ++i) live[i] = t + i * NT < m;
+  const bool active = wave * dev::kWave < m;  // the wave holds panel rows
   unsigned long long t1 = 0;
   if constexpr (STAMP) {
     __syncthreads();
@@ -310,7 +421,7 @@ __global__ __launch_bounds__(NT) void panel_kernel(double* __restrict__ P, int64
   }
 
   StepStamps ss{};
-  K::steps(a, chosen, sh, t, lane, wave, m, w, row0, info, ss, std::make_integer_sequence<int, W>{});
+  K::steps(a, live, sh, t, lane, wave, active, w, row0, info, ss, std::make_integer_sequence<int, W>{});
   unsigned long long t2 = 0;
   if constexpr (STAMP) t2 = stamp_now();
 
@@ -365,7 +476,7 @@ __global__ __launch_bounds__(NT) void panel_kernel(double* __restrict__ P, int64
     int id = -1;
     if (lr < w) {
       id = lr;
-    } else if (lr < m && ((chosen >> i) & 1)) {
+    } else if (lr < m && !live[i]) {
       for (int j = 0; j < w; ++j)
         if (sh.sel[j] == lr) id = w + j;
     }
@@ -375,7 +486,9 @@ __global__ __launch_bounds__(NT) void panel_kernel(double* __restrict__ P, int64
     }
     dest[i] = d;
   }
-  if (staged) {
+  if (staged && io == 1) {
+    K::store_direct(a, dest, P, ldp, m, t);
+  } else if (staged) {
     K::stage_out(a, dest, P, ldp, m, t);
   } else {
 #pragma unroll
@@ -400,6 +513,228 @@ __global__ __launch_bounds__(NT) void panel_kernel(double* __restrict__ P, int64
       for (int k = 0; k < 6; ++k) stamps[8 + k] = ss.v[k];
     }
   }
+}
+
+template <int NT, int R, int W, int MODE, bool STAMP = false>
+__global__ __launch_bounds__(NT) void panel_kernel(double* __restrict__ P, int64_t ldp, int m,
+                                                   int w, int row0, int* __restrict__ piv,
+                                                   int* __restrict__ info,
+                                                   unsigned long long* __restrict__ stamps,
+                                                   int* __restrict__ pairs) {
+  __shared__ PanelLds<W> sh;
+  panel_body<NT, R, W, MODE, STAMP>(P, ldp, m, w, row0, piv, info, stamps, pairs, sh);
+}
+
+// ---- fused step kernel -----------------------------------------------------
+// One launch per blocked-LU step j (the right-looking sweep with lookahead
+// folded into a single grid, so no cross-stream events are needed):
+//   workgroup 0      : applies step j-1 (row movement, TRSM, rank-wp GEMM) to
+//                      panel j's own column strip, then factors panel j;
+//   workgroups 1..   : apply step j-1 to one 16-column strip each of the
+//                      columns right of panel j (b included).
+// The wide update of step j-1 therefore runs on ~n/16 CUs underneath the
+// single-CU panel factorisation of step j.  Every workgroup owns whole
+// columns, so the row interchanges need no cross-workgroup ordering.
+constexpr int kStripCols = 16;
+constexpr int kStripMaxW = 16;
+
+struct StepArgs {
+  double* A;
+  int64_t lda;
+  int n;
+  int kp, wp;              // previous step (wp = 0: none)
+  const int* pairs_prev;   // its net row movement (relative to kp)
+  int k, w;                // this step's panel (w = 0: none)
+  int* piv;
+  int* info;
+  int* pairs;              // this step's row movement (out)
+  int wide_c0;             // first column of the wide strips
+  unsigned long long* stamps;  // diagnostics (STAMP builds): realtime per phase
+  int io;                      // panel IO: 0 LDS-staged, 1 direct
+};
+
+// Panel IO of the fused step: 1 (default) direct 16-byte register loads and
+// stores (one memory latency for the whole strip), 0 LDS-staged coalesced
+// passes.  GELIM_PANEL_IO overrides (read per launch, for A/B runs).
+int panel_io_mode() {
+  const char* e = std::getenv("GELIM_PANEL_IO");
+  return e ? std::atoi(e) : 1;
+}
+
+__device__ __forceinline__ unsigned long long realtime_now() {
+  unsigned long long t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
+
+struct alignas(16) StripLds {
+  double g[2 * kStripMaxW][kStripCols];   // gathered source rows
+  double x[kStripMaxW][kStripCols];       // top rows -> U12
+  double l11[kStripMaxW][kStripMaxW];     // unit lower triangle of the previous panel
+  int pr[1 + 4 * kStripMaxW];
+};
+
+// Apply a finished panel (rows [0, m) relative to its top, width wp, net row
+// movement `pairs`) to an ncols <= 16 column strip C: swap, U12 = L11^-1 A12,
+// A22 -= L21 U12 on the fp64 matrix cores.  Whole workgroup (NT = 512).
+template <int NT>
+__device__ __forceinline__ void strip_update(double* __restrict__ C, int64_t ldc, int ncols,
+                                             const double* __restrict__ L, int64_t ldl, int wp,
+                                             int m, const int* __restrict__ pairs, StripLds& sh) {
+  static_assert(NT == 2 * kStripMaxW * kStripCols, "one thread per (pair, column)");
+  const int t = threadIdx.x;
+  const int c = t & (kStripCols - 1);
+  const int e = t >> 4;
+  const bool colok = c < ncols;
+  if (t < 1 + 4 * kStripMaxW) {
+    const int np = pairs[0];
+    sh.pr[t] = (t == 0 || t <= 2 * np) ? pairs[t] : 0;
+  }
+  if (t < kStripMaxW * kStripMaxW) {
+    const int r = t / kStripMaxW, q = t % kStripMaxW;
+    sh.l11[r][q] = (q < r && r < wp) ? L[(int64_t)r * ldl + q] : 0.0;
+  }
+  __syncthreads();
+  const int np = sh.pr[0];
+  // every source and every top row is read before anything is written
+  if (e < np && colok) sh.g[e][c] = C[(int64_t)sh.pr[2 + 2 * e] * ldc + c];
+  if (e < kStripMaxW) sh.x[e][c] = (e < wp && colok) ? C[(int64_t)e * ldc + c] : 0.0;
+  __syncthreads();
+  if (e < np && colok) {
+    const int d = sh.pr[1 + 2 * e];
+    if (d < wp) sh.x[d][c] = sh.g[e][c];
+    else C[(int64_t)d * ldc + c] = sh.g[e][c];
+  }
+  __syncthreads();
+  if (t < kStripCols) {  // forward substitution, one column per lane
+    double x[kStripMaxW];
+#pragma unroll
+    for (int r = 0; r < kStripMaxW; ++r) x[r] = sh.x[r][t];
+#pragma unroll
+    for (int i = 0; i < kStripMaxW; ++i) {
+      asm volatile("" ::: "memory");  // keep the L11 reads per step (no 240-VGPR hoist)
+#pragma unroll
+      for (int j = i + 1; j < kStripMaxW; ++j) x[j] = opaque(fma(-sh.l11[j][i], x[i], x[j]));
+    }
+#pragma unroll
+    for (int r = 0; r < kStripMaxW; ++r) {
+      sh.x[r][t] = x[r];
+      if (r < wp && t < ncols) C[(int64_t)r * ldc + t] = x[r];
+    }
+  }
+  __syncthreads();
+  // rank-wp update of rows [wp, m): v_mfma_f64_16x16x4 per 16-row block,
+  // 4 blocks per wave in flight.  K is permuted so each lane reads 4
+  // consecutive multipliers (two 16-byte loads): MFMA kk, lane group q covers
+  // k = 4q + kk, and the B operand is read with the same permutation.
+  const int lane = t & 63, wave = t >> 6;
+  const int r16 = lane & 15, q = lane >> 4;
+  constexpr int kWaves = NT / 64;
+  constexpr int kBatch = 4;
+  double b[4];
+#pragma unroll
+  for (int kk = 0; kk < 4; ++kk) b[kk] = sh.x[4 * q + kk][r16];
+  const bool ccol = r16 < ncols;
+  const int nblk = (m - wp + 15) >> 4;
+  for (int b0 = wave; b0 < nblk; b0 += kWaves * kBatch) {
+    dev::d4 acc[kBatch];
+    double la[kBatch][4];
+#pragma unroll
+    for (int s = 0; s < kBatch; ++s) {
+      const int blk = b0 + kWaves * s;
+      const int rbase = wp + 16 * blk;
+      const int lrow = rbase + r16;
+      if (blk < nblk && lrow < m && 4 * q + 3 < wp) {
+        const double2* lp = reinterpret_cast<const double2*>(L + (int64_t)lrow * ldl + 4 * q);
+        const double2 v0 = lp[0], v1 = lp[1];
+        la[s][0] = v0.x; la[s][1] = v0.y; la[s][2] = v1.x; la[s][3] = v1.y;
+      } else if (blk < nblk && lrow < m) {  // partial last panel: stay inside the row
+        const double* lp = L + (int64_t)lrow * ldl + 4 * q;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) la[s][e] = (4 * q + e < wp) ? lp[e] : 0.0;
+      } else {
+        la[s][0] = la[s][1] = la[s][2] = la[s][3] = 0.0;
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = rbase + q + 4 * r;
+        acc[s][r] = (blk < nblk && row < m && ccol) ? C[(int64_t)row * ldc + r16] : 0.0;
+      }
+    }
+#pragma unroll
+    for (int s = 0; s < kBatch; ++s)
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) {
+        const double a = (4 * q + kk < wp) ? -la[s][kk] : 0.0;
+        acc[s] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b[kk], acc[s], 0, 0, 0);
+      }
+#pragma unroll
+    for (int s = 0; s < kBatch; ++s) {
+      const int blk = b0 + kWaves * s;
+      const int rbase = wp + 16 * blk;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = rbase + q + 4 * r;
+        if (blk < nblk && row < m && ccol) C[(int64_t)row * ldc + r16] = acc[s][r];
+      }
+    }
+  }
+}
+
+template <int NT, int R, int W, int MODE, bool STAMP = false>
+__global__ __launch_bounds__(NT) void step_kernel(StepArgs g) {
+  __shared__ PanelLds<W> sh;
+  StripLds& ss = *reinterpret_cast<StripLds*>(g_panel_dyn_lds);
+  const bool has_panel = g.w > 0;
+  const int64_t lda = g.lda;
+  unsigned long long t0 = 0, t1 = 0;
+  if constexpr (STAMP) t0 = realtime_now();
+  if (has_panel && blockIdx.x == 0) {
+    if (g.wp > 0) {
+      strip_update<NT>(g.A + (int64_t)g.kp * lda + g.k, lda, g.w, g.A + (int64_t)g.kp * lda + g.kp,
+                       lda, g.wp, g.n - g.kp, g.pairs_prev, ss);
+      __syncthreads();  // strip writes visible to the panel's loads (same CU)
+    }
+    if constexpr (STAMP) t1 = realtime_now();
+    panel_body<NT, R, W, MODE, false>(g.A + (int64_t)g.k * lda + g.k, lda, g.n - g.k, g.w, g.k,
+                                      g.piv + g.k, g.info, nullptr, g.pairs, sh, g.io);
+    if constexpr (STAMP) {
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        g.stamps[0] = t0;
+        g.stamps[1] = t1;
+        g.stamps[2] = realtime_now();
+      }
+    }
+    return;
+  }
+  const int wb = (int)(blockIdx.x - (has_panel ? 1 : 0));
+  const int c0 = g.wide_c0 + kStripCols * wb;
+  const int ncols = min(kStripCols, g.n + 1 - c0);
+  if (ncols <= 0) return;
+  strip_update<NT>(g.A + (int64_t)g.kp * lda + c0, lda, ncols, g.A + (int64_t)g.kp * lda + g.kp,
+                   lda, g.wp, g.n - g.kp, g.pairs_prev, ss);
+  if constexpr (STAMP) {
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      g.stamps[8 + 2 * wb] = t0;
+      g.stamps[9 + 2 * wb] = realtime_now();
+    }
+  }
+}
+
+template <int NT, int R, int W>
+int launch_step(const StepArgs& a, int mode, unsigned blocks, hipStream_t s) {
+  constexpr size_t stage = Panel<NT, R, W, 1, false>::stage_bytes();
+  constexpr size_t lds = stage > sizeof(StripLds) ? stage : sizeof(StripLds);
+  if (mode == GELIM_PIVOT_PARTIAL)
+    hipLaunchKernelGGL((step_kernel<NT, R, W, 1>), dim3(blocks), dim3(NT), lds, s, a);
+  else
+    hipLaunchKernelGGL((step_kernel<NT, R, W, 0>), dim3(blocks), dim3(NT), lds, s, a);
+  HIP_TRY(hipGetLastError());
+  return GELIM_OK;
 }
 
 template <int NT, int R, int W>
@@ -441,6 +776,30 @@ int panel_factor(double* P, int64_t ldp, int64_t m, int64_t w, int64_t row0, int
                                      " exceeds the register-resident panel");
 }
 
+// One fused step of the blocked LU (see step_kernel).  (kp, wp): previous
+// panel (wp = 0 for the first step); (k, w): this step's panel (w = 0 for the
+// closing step that only finishes the previous update).
+int lu_step(double* A, int64_t lda, int64_t n, int64_t kp, int64_t wp, const int* pairs_prev,
+            int64_t k, int64_t w, int mode, int* piv, int* info, int* pairs, hipStream_t s) {
+  if (wp > kStripMaxW || w > 16) return GELIM_FAIL(GELIM_E_ARG, "lu_step: panel wider than 16");
+  StepArgs a{A, lda, (int)n, (int)kp, (int)wp, pairs_prev, (int)k, (int)w, piv, info, pairs, 0,
+             nullptr, panel_io_mode()};
+  const int64_t c0 = (w > 0) ? k + w : n;
+  a.wide_c0 = (int)c0;
+  const int64_t nwide = (wp > 0) ? (n + 1 - c0 + kStripCols - 1) / kStripCols : 0;
+  const unsigned blocks = (unsigned)(nwide + (w > 0 ? 1 : 0));
+  if (blocks == 0) return GELIM_OK;
+  const int64_t m = n - (w > 0 ? k : kp);
+  if (m <= 512 && w <= 16) return launch_step<512, 1, 16>(a, mode, blocks, s);
+  if (m <= 1024 && w <= 16) return launch_step<512, 2, 16>(a, mode, blocks, s);
+  if (m <= 2048 && w <= 16) return launch_step<512, 4, 16>(a, mode, blocks, s);
+  if (m <= 4096 && w <= 8) return launch_step<512, 8, 8>(a, mode, blocks, s);
+  if (m <= 8192 && w <= 4) return launch_step<512, 16, 4>(a, mode, blocks, s);
+  if (m <= 16384 && w <= 2) return launch_step<512, 32, 2>(a, mode, blocks, s);
+  return GELIM_FAIL(GELIM_E_ARG, "lu_step: m=" + std::to_string(m) + " w=" + std::to_string(w) +
+                                     " exceeds the register-resident panel");
+}
+
 }  // namespace gelim
 
 extern "C" int gelim_gpu_panel_factor(double* dP, int64_t ldp, int64_t m, int64_t w, int64_t row0,
@@ -466,8 +825,19 @@ extern "C" int gelim_debug_panel_stamps(int64_t m, int64_t w, unsigned long long
   HIP_TRY(hipMemcpy(P, h.data(), h.size() * 8, hipMemcpyHostToDevice));
   HIP_TRY(hipMemset(info, 0, 16));
   constexpr size_t lds = Panel<512, 4, 16, 1, true>::stage_bytes();
+  const char* e256 = std::getenv("GELIM_NT256");
+  const bool nt256 = e256 && std::atoi(e256) != 0 && m <= 1024;
   for (int rep = 0; rep < 3; ++rep) {
-    if (m <= 512)
+    if (nt256 && m <= 256)
+      hipLaunchKernelGGL((panel_kernel<256, 1, 16, 1, true>), 1, 256, lds, 0, P, 16, (int)m,
+                         (int)w, 0, piv, info, st, nullptr);
+    else if (nt256 && m <= 512)
+      hipLaunchKernelGGL((panel_kernel<256, 2, 16, 1, true>), 1, 256, lds, 0, P, 16, (int)m,
+                         (int)w, 0, piv, info, st, nullptr);
+    else if (nt256)
+      hipLaunchKernelGGL((panel_kernel<256, 4, 16, 1, true>), 1, 256, lds, 0, P, 16, (int)m,
+                         (int)w, 0, piv, info, st, nullptr);
+    else if (m <= 512)
       hipLaunchKernelGGL((panel_kernel<512, 1, 16, 1, true>), 1, 512, lds, 0, P, 16, (int)m,
                          (int)w, 0, piv, info, st, nullptr);
     else if (m <= 1024)
@@ -498,4 +868,62 @@ extern "C" int64_t gelim_gpu_panel_max_rows(int64_t w) {
   if (w <= 8) return 4096;
   if (w <= 16) return 2048;
   return 0;
+}
+
+// Diagnostic: factor a random n x (n+1) system up to step j (fused schedule,
+// 16-wide panels, n <= 2048), then run step j with realtime stamps.  out[0..2]
+// = workgroup 0 {prologue, panel} in 10 ns ticks; out[3] = slowest wide
+// workgroup, out[4] = median wide workgroup, out[5] = wide count.
+extern "C" int gelim_debug_step_stamps(int64_t n, int64_t j, double* out) {
+  using namespace gelim;
+  if (n > 2048 || j < 1 || 16 * j >= n) return GELIM_FAIL(GELIM_E_ARG, "debug_step_stamps: bad n/j");
+  const int64_t lda = (n + 1 + 7) / 8 * 8;
+  double* A = nullptr;
+  int *piv = nullptr, *info = nullptr, *pairs = nullptr;
+  unsigned long long* st = nullptr;
+  HIP_TRY(hipMalloc((void**)&A, sizeof(double) * n * lda));
+  HIP_TRY(hipMalloc((void**)&piv, sizeof(int) * (n + 64)));
+  HIP_TRY(hipMalloc((void**)&info, 16));
+  HIP_TRY(hipMalloc((void**)&pairs, sizeof(int) * 72 * (n / 16 + 2)));
+  HIP_TRY(hipMalloc((void**)&st, sizeof(unsigned long long) * 1024));
+  HIP_TRY(hipMemset(st, 0, sizeof(unsigned long long) * 1024));
+  HIP_TRY(hipMemset(info, 0, 16));
+  std::vector<double> h(n * lda, 0.0);
+  for (int64_t r = 0; r < n; ++r)
+    for (int64_t c = 0; c <= n; ++c)
+      h[r * lda + c] = (double)(((r * 7919 + c * 104729) * 2654435761ull) % 2000) / 1000.0 - 1.0;
+  HIP_TRY(hipMemcpy(A, h.data(), h.size() * 8, hipMemcpyHostToDevice));
+  for (int64_t i = 0; i < j; ++i)
+    GELIM_TRY(lu_step(A, lda, n, i ? 16 * (i - 1) : 0, i ? 16 : 0, i ? pairs + (i - 1) * 72 : nullptr,
+                      16 * i, 16, GELIM_PIVOT_PARTIAL, piv, info, pairs + i * 72, 0));
+  StepArgs a{A, lda, (int)n, (int)(16 * (j - 1)), 16, pairs + (j - 1) * 72, (int)(16 * j), 16,
+             piv, info, pairs + j * 72, (int)(16 * j + 16), st, panel_io_mode()};
+  const int64_t m = n - 16 * j;
+  const unsigned nwide = (unsigned)((n + 1 - (16 * j + 16) + 15) / 16);
+  constexpr size_t lds = Panel<512, 4, 16, 1, false>::stage_bytes();
+  if (m <= 512)
+    hipLaunchKernelGGL((step_kernel<512, 1, 16, 1, true>), nwide + 1, 512, lds, 0, a);
+  else if (m <= 1024)
+    hipLaunchKernelGGL((step_kernel<512, 2, 16, 1, true>), nwide + 1, 512, lds, 0, a);
+  else
+    hipLaunchKernelGGL((step_kernel<512, 4, 16, 1, true>), nwide + 1, 512, lds, 0, a);
+  HIP_TRY(hipDeviceSynchronize());
+  std::vector<unsigned long long> hs(1024);
+  HIP_TRY(hipMemcpy(hs.data(), st, 8 * 1024, hipMemcpyDeviceToHost));
+  const unsigned long long base = hs[0];
+  out[0] = (double)(hs[1] - base);
+  out[1] = (double)(hs[2] - hs[1]);
+  out[2] = (double)(hs[2] - base);
+  std::vector<double> wd;
+  for (unsigned b = 0; b < nwide && 9 + 2 * b < 1024; ++b) wd.push_back((double)(hs[9 + 2 * b] - base));
+  std::sort(wd.begin(), wd.end());
+  out[3] = wd.empty() ? 0 : wd.back();
+  out[4] = wd.empty() ? 0 : wd[wd.size() / 2];
+  out[5] = (double)wd.size();
+  (void)hipFree(A);
+  (void)hipFree(piv);
+  (void)hipFree(info);
+  (void)hipFree(pairs);
+  (void)hipFree(st);
+  return GELIM_OK;
 }

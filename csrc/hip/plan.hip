@@ -18,6 +18,8 @@ namespace gelim {
 int64_t panel_width_for(int64_t m);
 int panel_factor(double* P, int64_t ldp, int64_t m, int64_t w, int64_t row0, int mode, int* piv,
                  int* info, hipStream_t s, int* pairs);
+int lu_step(double* A, int64_t lda, int64_t n, int64_t kp, int64_t wp, const int* pairs_prev,
+            int64_t k, int64_t w, int mode, int* piv, int* info, int* pairs, hipStream_t s);
 int pairs_trsm(double* C, int64_t ldc, int64_t ncols, const double* L, int64_t ldl, int64_t w,
                const int* pairs, hipStream_t s);
 int swap_trsm(double* C, int64_t ldc, int64_t ncols, const double* L, int64_t ldl, int64_t w,
@@ -49,6 +51,7 @@ struct gelim_gauss_plan {
   std::vector<int64_t> step_k, step_w;   // blocked schedule
   int* pairs = nullptr;                  // per-step net row movement
   bool lookahead = false;                // GELIM_LOOKAHEAD=1: side-stream wide updates
+  bool fused = true;                     // GELIM_SCHEDULE=classic: separate update kernels
   hipGraphExec_t exec = nullptr;
   const void* k_src = nullptr;
   int64_t k_ld = 0;
@@ -68,6 +71,23 @@ int enqueue(gelim_gauss_plan* p, const void* src, int64_t src_ld, void* dx, void
     HIP_TRY(hipMemcpy2DAsync(p->work, lda * p->eb, src, src_ld * p->eb, (n + 1) * p->eb, n,
                              hipMemcpyDeviceToDevice, s));
   HIP_TRY(hipMemsetAsync(p->info, 0, 16, s));
+  if (p->algo == GELIM_GPU_BLOCKED && p->fused) {
+    // One fused launch per step (lu_step): workgroup 0 finishes step i-1 on
+    // panel i's columns and factors panel i while the other workgroups apply
+    // step i-1 to the columns right of panel i; a closing launch applies the
+    // last step to b.  S+1 launches, stream-ordered, no events.
+    double* A = static_cast<double*>(p->work);
+    const size_t S = p->step_k.size();
+    for (size_t i = 0; i <= S; ++i) {
+      const int64_t kp = i ? p->step_k[i - 1] : 0, wp = i ? p->step_w[i - 1] : 0;
+      const int64_t k = i < S ? p->step_k[i] : n, w = i < S ? p->step_w[i] : 0;
+      const int* prev = i ? p->pairs + (i - 1) * kPairSlot : nullptr;
+      int* cur = i < S ? p->pairs + i * kPairSlot : nullptr;
+      GELIM_TRY(lu_step(A, lda, n, kp, wp, prev, k, w, p->pivot, p->piv, p->info, cur, s));
+    }
+    return backsub_f64(A, lda, A + n, lda, static_cast<double*>(dx),
+                       static_cast<double*>(bnorm), n, 0, p->yw, s);
+  }
   if (p->algo == GELIM_GPU_BLOCKED) {
     // Right-looking blocked LU with lookahead 1.  Critical stream s:
     //   panel(i) -> [wait wide(i-1)] -> narrow(i) -> panel(i+1) -> ...
@@ -166,6 +186,8 @@ extern "C" gelim_gauss_plan* gelim_gauss_plan_create(int64_t n, int algo, int pi
     return fail("tmp");
   if (hipStreamCreateWithFlags(&p->cap, hipStreamNonBlocking) != hipSuccess) return fail("stream");
   if (const char* e = std::getenv("GELIM_LOOKAHEAD")) p->lookahead = std::atoi(e) != 0;
+  if (const char* e = std::getenv("GELIM_SCHEDULE")) p->fused = std::string(e) != "classic";
+  if (p->lookahead) p->fused = false;
   if (algo == GELIM_GPU_BLOCKED) {
     for (int64_t k = 0; k < n;) {
       const int64_t w = std::min<int64_t>(gelim::panel_width_for(n - k), n - k);

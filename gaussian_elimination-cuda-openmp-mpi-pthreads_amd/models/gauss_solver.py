@@ -16,6 +16,8 @@ as produced by `ops.init.*_system`.  `solve` never modifies `aug`.
 """
 from __future__ import annotations
 
+import sys as _sys
+
 import torch
 
 from .. import _native
@@ -109,9 +111,7 @@ class GaussSolver:
     def __del__(self):
         # never tear down HIP objects during interpreter shutdown (the HIP
         # runtime may already be gone); explicit close() is the normal path
-        import sys
-
-        if sys.is_finalizing():
+        if _sys is None or _sys.is_finalizing():
             return
         try:
             self.close()

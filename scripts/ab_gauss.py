@@ -10,22 +10,32 @@ import torch  # noqa: E402
 
 import gelim  # noqa: E402
 
-n = int(sys.argv[1]) if len(sys.argv) > 1 else 2048
+n = int(sys.argv[1]) if len(sys.argv) > 1 and sys.argv[1].isdigit() else 2048
 dev = torch.device("cuda:0")
 src = gelim.random_system(n, seed=1234, device=dev)
 variants = {}
-for la in ("1", "0"):
-    for g in (True, False):
-        os.environ["GELIM_LOOKAHEAD"] = la
-        variants[f"lookahead={la} graph={int(g)}"] = gelim.GaussSolver(n, "hip", device=dev, use_graph=g)
-variants["hip-pivot"] = gelim.GaussSolver(n, "hip-pivot", device=dev)
+# schedule is read from the environment when a plan is created
+# plans read GELIM_* at creation; GELIM_PANEL_IO is read at every enqueue, so
+# the io variants run eagerly with the variable set around each solve
+VARIANTS = {
+    "fused io=0": {"GELIM_SCHEDULE": "fused", "GELIM_LOOKAHEAD": "0", "GELIM_PANEL_IO": "0"},
+    "fused io=1": {"GELIM_SCHEDULE": "fused", "GELIM_LOOKAHEAD": "0", "GELIM_PANEL_IO": "1"},
+    "classic": {"GELIM_SCHEDULE": "classic", "GELIM_LOOKAHEAD": "0", "GELIM_PANEL_IO": "0"},
+}
+for name, env in VARIANTS.items():
+    os.environ.update(env)
+    variants[name] = gelim.GaussSolver(n, "hip", device=dev, use_graph=False)
+if "--pivot" in sys.argv:
+    variants["hip-pivot"] = gelim.GaussSolver(n, "hip-pivot", device=dev)
 res = {k: [] for k in variants}
 for s in variants.values():
     for _ in range(3):
         s.solve(src)
+os.environ["GELIM_PANEL_IO"] = "0"
 torch.cuda.synchronize()
 for rnd in range(5):
     for k, s in variants.items():
+        os.environ.update(VARIANTS.get(k, {}))
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(5):

@@ -1,0 +1,137 @@
+"""Distributed Gaussian elimination CLI — the MI355X counterpart of the
+reference's MPI programs (OpenMP_and_MPI/gauss_mpi/gauss_internal_input.c and
+gauss_external_input.c), launched with torchrun, one rank per GPU over RCCL
+(gloo + CPU ranks with --device cpu).
+
+Internal mode (no FILE): the synthetic system A[i][j] = 2 min(i+1, j+1),
+b[i] = i (gauss_internal_input.c:53-63), size -s N (default 2048); prints the
+reference's `Application time: %f Secs` on rank 0, timer including the
+initialisation like the reference (MPIi:322-334).
+
+External mode (FILE = .dat or data/*.coo.npz): b = A (1..n)
+(gauss_external_input.c:90-108); prints `Time:  %f seconds` (elimination +
+back substitution, the reference times computeGauss only, MPIe:356-365) and
+`Error: %e` (MPIe:371-378).
+
+Unlike the reference's master/worker scheme (rank 0 ships full rows out and
+back every pivot step), the matrix is resident and
+column block-cyclic: one panel broadcast per block (parallel/dist_gauss.py).
+"""
+from __future__ import annotations
+
+import argparse
+import sys
+import time
+
+import torch
+
+from .. import _native
+from ..ops.gauss import error_metric
+from ..ops.init import augment_with_rhs
+from ..parallel import comm as C
+from ..parallel.dist_gauss import DistributedGauss
+from ..utils import io
+from ..utils.report import json_line
+
+
+def parse(argv=None):
+    p = argparse.ArgumentParser(prog="gelim.cli.dist_gauss", description=__doc__.split("\n\n")[0])
+    p.add_argument("file", nargs="?", help=".dat or .coo.npz matrix (external mode)")
+    p.add_argument("-s", "--size", type=int, default=2048, help="order of the synthetic system (internal mode)")
+    p.add_argument("--block", type=int, default=64, help="column block width D of the block-cyclic layout")
+    p.add_argument("--pivot", default="partial", choices=["partial", "zero"])
+    p.add_argument("--device", default=None, help="cpu | cuda (default: cuda when visible)")
+    p.add_argument("--warmup", type=int, default=0, help="untimed solves before the timed one")
+    p.add_argument("--verify", action="store_true", help="print the max error against the exact solution")
+    p.add_argument("--json", action="store_true", help="also print one JSON result line")
+    return p.parse_args(argv)
+
+
+def load_global(path: str) -> torch.Tensor:
+    if path.endswith(".npz"):
+        n, r, c, v = io.load_coo_npz(path)
+        return io.coo_to_dense(n, r, c, v)
+    return io.read_dat(path)
+
+
+def synthetic_local(dg: DistributedGauss) -> torch.Tensor:
+    """Each rank builds only its own columns of the internal system."""
+    L, n = dg.layout, dg.n
+    loc = dg.empty_local()
+    i = torch.arange(1, n + 1, dtype=torch.float64, device=dg.device).view(n, 1)
+    for g in L.local_blocks(dg.comm.rank):
+        c, w = L.local_col(g), L.width(g)
+        j = torch.arange(g * L.D + 1, g * L.D + w + 1, dtype=torch.float64, device=dg.device).view(1, w)
+        loc[:, c:c + w] = 2.0 * torch.minimum(i, j)
+    loc[:, dg.nloc] = torch.arange(n, dtype=torch.float64, device=dg.device)
+    return loc
+
+
+def main(argv=None) -> int:
+    args = parse(argv)
+    comm = C.init_from_env(device=args.device)
+    dev = comm.device
+
+    def sync():
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+        comm.barrier()
+
+    rc = 0
+    try:
+        if args.file is None:
+            n = args.size
+            dg = DistributedGauss(comm, n, block=args.block, pivot=args.pivot)
+            for _ in range(args.warmup):
+                dg.solve_(synthetic_local(dg))
+            sync()
+            t0 = time.perf_counter()
+            loc = synthetic_local(dg)
+            x = dg.solve_(loc)
+            sync()
+            dt = time.perf_counter() - t0
+            if comm.rank == 0:
+                print(f"Application time: {dt:f} Secs", flush=True)
+                err = None
+                if args.verify:
+                    exact = torch.zeros(n, dtype=torch.float64)
+                    exact[0], exact[-1] = -0.5, 0.5
+                    err = float((x.cpu() - exact).abs().max())
+                    print(f"Max error vs exact solution: {err:e}")
+                if args.json:
+                    print(json_line({"program": "dist_gauss_internal", "n": n, "ranks": comm.world_size,
+                                     "block": args.block, "time_s": dt, "max_abs_error": err,
+                                     "backend": comm.backend, "device": dev.type}))
+        else:
+            A = load_global(args.file)
+            n = A.shape[0]
+            aug = augment_with_rhs(A)
+            dg = DistributedGauss(comm, n, block=args.block, pivot=args.pivot)
+            for _ in range(args.warmup):
+                dg.solve_(dg.scatter_from_global(aug))
+            loc = dg.scatter_from_global(aug)
+            sync()
+            t0 = time.perf_counter()
+            x = dg.solve_(loc)
+            sync()
+            dt = time.perf_counter() - t0
+            if comm.rank == 0:
+                err = error_metric(x)
+                print(f"\nMatrix File: {args.file}; Matrix Size: {n} ; Ranks: {comm.world_size}", flush=True)
+                print(f"Time:  {dt:f} seconds")
+                print(f"Error: {err:e}", flush=True)
+                if args.json:
+                    print(json_line({"program": "dist_gauss_external", "file": args.file, "n": n,
+                                     "ranks": comm.world_size, "block": args.block, "time_s": dt,
+                                     "error": err, "backend": comm.backend, "device": dev.type}))
+    except _native.SingularMatrixError:
+        if comm.rank == 0:
+            print("The matrix is singular", file=sys.stderr)
+        rc = 255  # the reference's exit(-1)
+    finally:
+        C.destroy()
+    return rc
+
+
+if __name__ == "__main__":
+    sys.exit(main())

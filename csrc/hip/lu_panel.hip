@@ -579,11 +579,31 @@ struct alignas(16) StripLds {
 // Apply a finished panel (rows [0, m) relative to its top, width wp, net row
 // movement `pairs`) to an ncols <= 16 column strip C: swap, U12 = L11^-1 A12,
 // A22 -= L21 U12 on the fp64 matrix cores.  Whole workgroup (NT = 512).
-template <int NT>
+// One forward-substitution step of the DPP-row TRSM (see strip_update).
+template <int I>
+__device__ __forceinline__ void trsm_dpp_step(double& x, const double (&lrow)[kStripMaxW], int j) {
+  const uint64_t bits = (uint64_t)__double_as_longlong(x);
+  const unsigned hi = (unsigned)__builtin_amdgcn_update_dpp(0, (int)(unsigned)(bits >> 32), 0x150 + I, 0xf, 0xf, false);
+  const unsigned lo = (unsigned)__builtin_amdgcn_update_dpp(0, (int)(unsigned)bits, 0x150 + I, 0xf, 0xf, false);
+  const double xi = __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+  x = (j > I) ? fma(-lrow[I], xi, x) : x;
+}
+
+template <int... I>
+__device__ __forceinline__ void trsm_dpp_steps(double& x, const double (&lrow)[kStripMaxW], int j,
+                                               std::integer_sequence<int, I...>) {
+  (trsm_dpp_step<I>(x, lrow, j), ...);
+}
+
+template <int NT, bool STAMP = false>
 __device__ __forceinline__ void strip_update(double* __restrict__ C, int64_t ldc, int ncols,
                                              const double* __restrict__ L, int64_t ldl, int wp,
-                                             int m, const int* __restrict__ pairs, StripLds& sh) {
+                                             int m, const int* __restrict__ pairs, StripLds& sh,
+                                             unsigned long long* ts = nullptr) {
   static_assert(NT == 2 * kStripMaxW * kStripCols, "one thread per (pair, column)");
+  auto mark = [&](int i) {
+    if constexpr (STAMP) ts[i] = realtime_now();
+  };
   const int t = threadIdx.x;
   const int c = t & (kStripCols - 1);
   const int e = t >> 4;
@@ -597,34 +617,34 @@ __device__ __forceinline__ void strip_update(double* __restrict__ C, int64_t ldc
     sh.l11[r][q] = (q < r && r < wp) ? L[(int64_t)r * ldl + q] : 0.0;
   }
   __syncthreads();
+  mark(0);
   const int np = sh.pr[0];
   // every source and every top row is read before anything is written
   if (e < np && colok) sh.g[e][c] = C[(int64_t)sh.pr[2 + 2 * e] * ldc + c];
   if (e < kStripMaxW) sh.x[e][c] = (e < wp && colok) ? C[(int64_t)e * ldc + c] : 0.0;
   __syncthreads();
+  mark(1);
   if (e < np && colok) {
     const int d = sh.pr[1 + 2 * e];
     if (d < wp) sh.x[d][c] = sh.g[e][c];
     else C[(int64_t)d * ldc + c] = sh.g[e][c];
   }
   __syncthreads();
-  if (t < kStripCols) {  // forward substitution, one column per lane
-    double x[kStripMaxW];
+  mark(2);
+  if (t < kStripCols * kStripMaxW) {  // forward substitution: DPP row = one column
+    // lane j of 16-lane row c holds x[j][c]; x[i][c] is broadcast to the row
+    // with DPP row_newbcast:i, so the 16-step chain has no LDS round trips
+    const int cc = t >> 4, j = t & 15;
+    double x = sh.x[j][cc];
+    double lrow[kStripMaxW];
 #pragma unroll
-    for (int r = 0; r < kStripMaxW; ++r) x[r] = sh.x[r][t];
-#pragma unroll
-    for (int i = 0; i < kStripMaxW; ++i) {
-      asm volatile("" ::: "memory");  // keep the L11 reads per step (no 240-VGPR hoist)
-#pragma unroll
-      for (int j = i + 1; j < kStripMaxW; ++j) x[j] = opaque(fma(-sh.l11[j][i], x[i], x[j]));
-    }
-#pragma unroll
-    for (int r = 0; r < kStripMaxW; ++r) {
-      sh.x[r][t] = x[r];
-      if (r < wp && t < ncols) C[(int64_t)r * ldc + t] = x[r];
-    }
+    for (int i = 0; i < kStripMaxW; ++i) lrow[i] = sh.l11[j][i];
+    trsm_dpp_steps(x, lrow, j, std::make_integer_sequence<int, kStripMaxW>{});
+    sh.x[j][cc] = x;
+    if (j < wp && cc < ncols) C[(int64_t)j * ldc + cc] = x;
   }
   __syncthreads();
+  mark(3);
   // rank-wp update of rows [wp, m): v_mfma_f64_16x16x4 per 16-row block,
   // 4 blocks per wave in flight.  K is permuted so each lane reads 4
   // consecutive multipliers (two 16-byte loads): MFMA kk, lane group q covers
@@ -681,6 +701,9 @@ __device__ __forceinline__ void strip_update(double* __restrict__ C, int64_t ldc
       }
     }
   }
+  mark(4);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // strip complete before any reader
+  mark(5);
 }
 
 template <int NT, int R, int W, int MODE, bool STAMP = false>
@@ -690,11 +713,13 @@ __global__ __launch_bounds__(NT) void step_kernel(StepArgs g) {
   const bool has_panel = g.w > 0;
   const int64_t lda = g.lda;
   unsigned long long t0 = 0, t1 = 0;
+  __shared__ unsigned long long sts[8];
   if constexpr (STAMP) t0 = realtime_now();
   if (has_panel && blockIdx.x == 0) {
     if (g.wp > 0) {
-      strip_update<NT>(g.A + (int64_t)g.kp * lda + g.k, lda, g.w, g.A + (int64_t)g.kp * lda + g.kp,
-                       lda, g.wp, g.n - g.kp, g.pairs_prev, ss);
+      strip_update<NT, STAMP>(g.A + (int64_t)g.kp * lda + g.k, lda, g.w,
+                              g.A + (int64_t)g.kp * lda + g.kp, lda, g.wp, g.n - g.kp, g.pairs_prev,
+                              ss, sts);
       __syncthreads();  // strip writes visible to the panel's loads (same CU)
     }
     if constexpr (STAMP) t1 = realtime_now();
@@ -706,6 +731,7 @@ __global__ __launch_bounds__(NT) void step_kernel(StepArgs g) {
         g.stamps[0] = t0;
         g.stamps[1] = t1;
         g.stamps[2] = realtime_now();
+        for (int i = 0; i < 6; ++i) g.stamps[600 + i] = sts[i];
       }
     }
     return;
@@ -920,6 +946,7 @@ extern "C" int gelim_debug_step_stamps(int64_t n, int64_t j, double* out) {
   out[3] = wd.empty() ? 0 : wd.back();
   out[4] = wd.empty() ? 0 : wd[wd.size() / 2];
   out[5] = (double)wd.size();
+  for (int i = 0; i < 6; ++i) out[6 + i] = hs[600 + i] ? (double)(hs[600 + i] - base) : 0.0;
   (void)hipFree(A);
   (void)hipFree(piv);
   (void)hipFree(info);

@@ -18,7 +18,8 @@ for j in (1, 2, 8, 32, 64, 65, 96, 97, 120):
     if 16 * j >= n:
         continue
     for rep in range(2):
-        out = (C.c_double * 6)()
+        out = (C.c_double * 12)()
         gelim._native.check(f(n, j, out))
     print(f"{j:4d} {n - 16 * j:5d} | {out[0] / 100:8.2f} {out[1] / 100:8.2f} {out[2] / 100:8.2f} | "
-          f"{out[3] / 100:8.2f} {out[4] / 100:8.2f} {int(out[5])}")
+          f"{out[3] / 100:8.2f} {out[4] / 100:8.2f} {int(out[5])} | prologue phases us: "
+          + " ".join(f"{v / 100:6.2f}" for v in out[6:12]))

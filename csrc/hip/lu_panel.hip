@@ -382,7 +382,13 @@ __device__ __forceinline__ void panel_body(double* __restrict__ P, int64_t ldp, 
                                            int* __restrict__ info,
                                            unsigned long long* __restrict__ stamps,
                                            int* __restrict__ pairs, PanelLds<W>& sh,
-                                           int io = 0) {
+                                           int io = 0, const double* Pin = nullptr,
+                                           int64_t ldin = 0) {
+  // the panel is read from Pin (default: P itself) and written to P
+  if (Pin == nullptr) {
+    Pin = P;
+    ldin = ldp;
+  }
   using K = Panel<NT, R, W, MODE, STAMP>;
   const int t = threadIdx.x;
   const int lane = t & (dev::kWave - 1);
@@ -393,16 +399,17 @@ __device__ __forceinline__ void panel_body(double* __restrict__ P, int64_t ldp, 
   double a[R][W];
   // full-width panels with 16-byte aligned rows are staged through LDS so the
   // global loads are coalesced (W/2 lanes per row segment)
-  const bool staged = (w == W) && (W % 2 == 0) && ((((uintptr_t)P) & 15) == 0) && (ldp % 2 == 0);
+  const bool staged = (w == W) && (W % 2 == 0) && ((((uintptr_t)P) & 15) == 0) && (ldp % 2 == 0) &&
+                      ((((uintptr_t)Pin) & 15) == 0) && (ldin % 2 == 0);
   if (staged && io == 1) {
-    K::load_direct(a, P, ldp, m, t);
+    K::load_direct(a, Pin, ldin, m, t);
   } else if (staged) {
-    K::stage_in(a, P, ldp, m, t);
+    K::stage_in(a, Pin, ldin, m, t);
   } else {
 #pragma unroll
     for (int i = 0; i < R; ++i) {
       const int lr = t + i * NT;
-      const double* src = P + (int64_t)min(lr, m - 1) * ldp;  // clamped: no divergent loads
+      const double* src = Pin + (int64_t)min(lr, m - 1) * ldin;  // clamped: no divergent loads
 #pragma unroll
       for (int c = 0; c < W; ++c) {
         const double v = src[min(c, w - 1)];
@@ -551,7 +558,10 @@ struct StepArgs {
   int wide_c0;             // first column of the wide strips
   unsigned long long* stamps;  // diagnostics (STAMP builds): realtime per phase
   int io;                      // panel IO: 0 LDS-staged, 1 direct
+  const double* buf;           // narrow-kernel output (rows rel kp, ld kBufLd) or null
 };
+
+constexpr int kBufLd = 16;  // row stride of the narrow strip buffer (doubles)
 
 // Panel IO of the fused step: 1 (default) direct 16-byte register loads and
 // stores (one memory latency for the whole strip), 0 LDS-staged coalesced
@@ -715,6 +725,28 @@ __global__ __launch_bounds__(NT) void step_kernel(StepArgs g) {
   unsigned long long t0 = 0, t1 = 0;
   __shared__ unsigned long long sts[8];
   if constexpr (STAMP) t0 = realtime_now();
+  if (has_panel && blockIdx.x == 0 && g.buf != nullptr) {
+    // step j-1 was already applied to this strip by the narrow kernel: its
+    // U12 rows go to A, the panel rows are read straight from the buffer
+    {
+      const int r = threadIdx.x >> 4, c = threadIdx.x & 15;
+      if (r < g.wp && c < g.w)
+        g.A[(int64_t)(g.kp + r) * lda + g.k + c] = g.buf[r * kBufLd + c];
+    }
+    if constexpr (STAMP) t1 = realtime_now();
+    panel_body<NT, R, W, MODE, false>(g.A + (int64_t)g.k * lda + g.k, lda, g.n - g.k, g.w, g.k,
+                                      g.piv + g.k, g.info, nullptr, g.pairs, sh, g.io,
+                                      g.buf + (int64_t)g.wp * kBufLd, kBufLd);
+    if constexpr (STAMP) {
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        g.stamps[0] = t0;
+        g.stamps[1] = t1;
+        g.stamps[2] = realtime_now();
+      }
+    }
+    return;
+  }
   if (has_panel && blockIdx.x == 0) {
     if (g.wp > 0) {
       strip_update<NT, STAMP>(g.A + (int64_t)g.kp * lda + g.k, lda, g.w,
@@ -747,6 +779,122 @@ __global__ __launch_bounds__(NT) void step_kernel(StepArgs g) {
     if (threadIdx.x == 0) {
       g.stamps[8 + 2 * wb] = t0;
       g.stamps[9 + 2 * wb] = realtime_now();
+    }
+  }
+}
+
+// ---- narrow kernel ------------------------------------------------------------
+// Step j applied to the NEXT panel's column strip, spread over ceil(m/256)
+// workgroups (one 256-row slice each) instead of serialising it on the panel
+// workgroup.  A is only read; the updated strip (rows relative to the step-j
+// panel top, U12 rows first) goes to a side buffer that the next panel loads
+// directly, so the row interchanges need no cross-workgroup ordering.
+constexpr int kNarrowRows = 256;
+
+struct NarrowArgs {
+  const double* C;  // strip: A + kp*lda + k (rows relative to kp)
+  int64_t ldc;
+  int ncols;        // strip width (next panel's w)
+  const double* L;  // A + kp*lda + kp
+  int64_t ldl;
+  int wp;           // step-j panel width
+  int m;            // n - kp
+  const int* pairs; // step-j row movement
+  double* out;      // buffer, ld kBufLd
+};
+
+__global__ __launch_bounds__(256) void narrow_kernel(NarrowArgs g) {
+  __shared__ double x[kStripMaxW][kStripCols];
+  __shared__ double l11[kStripMaxW][kStripMaxW];
+  __shared__ int pr[1 + 4 * kStripMaxW];
+  __shared__ int srcmap[kNarrowRows];
+  const int t = threadIdx.x;
+  const int r0 = blockIdx.x * kNarrowRows;
+  const int r1 = min(r0 + kNarrowRows, g.m);
+  const int wp = g.wp, ncols = g.ncols;
+  {
+    const int rr = t >> 4, cc = t & 15;
+    if (t < 1 + 4 * kStripMaxW) {
+      const int np = g.pairs[0];
+      pr[t] = (t == 0 || t <= 2 * np) ? g.pairs[t] : 0;
+    }
+    l11[rr][cc] = (cc < rr && rr < wp) ? g.L[(int64_t)rr * g.ldl + cc] : 0.0;
+    x[rr][cc] = (rr < wp && cc < ncols) ? g.C[(int64_t)rr * g.ldc + cc] : 0.0;
+    srcmap[t] = r0 + t;
+  }
+  __syncthreads();
+  const int np = pr[0];
+  // post-swap top rows; source rows of this slice's permuted rows
+  for (int idx = t; idx < np * kStripCols; idx += 256) {
+    const int e = idx >> 4, cc = idx & 15;
+    const int d = pr[1 + 2 * e];
+    if (d < wp) x[d][cc] = (cc < ncols) ? g.C[(int64_t)pr[2 + 2 * e] * g.ldc + cc] : 0.0;
+  }
+  if (t < np) {
+    const int d = pr[1 + 2 * t];
+    if (d >= r0 && d < r1) srcmap[d - r0] = pr[2 + 2 * t];
+  }
+  __syncthreads();
+  {  // U12 = L11^-1 x: DPP row = one column
+    const int cc = t >> 4, j = t & 15;
+    double xv = x[j][cc];
+    double lrow[kStripMaxW];
+#pragma unroll
+    for (int i = 0; i < kStripMaxW; ++i) lrow[i] = l11[j][i];
+    trsm_dpp_steps(xv, lrow, j, std::make_integer_sequence<int, kStripMaxW>{});
+    x[j][cc] = xv;
+    if (r0 == 0 && j < wp) g.out[j * kBufLd + cc] = xv;
+  }
+  __syncthreads();
+  // rows [max(r0, wp), r1): out[r] = A[src(r)] - L[r] U12 (MFMA, K permuted)
+  const int lane = t & 63, wave = t >> 6;
+  const int r16 = lane & 15, q = lane >> 4;
+  double b[4];
+#pragma unroll
+  for (int kk = 0; kk < 4; ++kk) b[kk] = x[4 * q + kk][r16];
+  const bool ccol = r16 < ncols;
+  const int a0 = max(r0, wp);
+  const int nblk = (r1 - a0 + 15) >> 4;  // <= 16
+  dev::d4 acc[4];
+  double la[4][4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    const int blk = wave + 4 * s;
+    const int rbase = a0 + 16 * blk;
+    const int lrow = rbase + r16;
+    const bool okb = blk < nblk && lrow < r1;
+    if (okb && 4 * q + 3 < wp) {
+      const double2* lp = reinterpret_cast<const double2*>(g.L + (int64_t)lrow * g.ldl + 4 * q);
+      const double2 v0 = lp[0], v1 = lp[1];
+      la[s][0] = v0.x; la[s][1] = v0.y; la[s][2] = v1.x; la[s][3] = v1.y;
+    } else if (okb) {
+      const double* lp = g.L + (int64_t)lrow * g.ldl + 4 * q;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) la[s][e] = (4 * q + e < wp) ? lp[e] : 0.0;
+    } else {
+      la[s][0] = la[s][1] = la[s][2] = la[s][3] = 0.0;
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = rbase + q + 4 * r;
+      acc[s][r] = (blk < nblk && row < r1 && ccol) ? g.C[(int64_t)srcmap[row - r0] * g.ldc + r16] : 0.0;
+    }
+  }
+#pragma unroll
+  for (int s = 0; s < 4; ++s)
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      const double a = (4 * q + kk < wp) ? -la[s][kk] : 0.0;
+      acc[s] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b[kk], acc[s], 0, 0, 0);
+    }
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    const int blk = wave + 4 * s;
+    const int rbase = a0 + 16 * blk;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = rbase + q + 4 * r;
+      if (blk < nblk && row < r1) g.out[(int64_t)row * kBufLd + r16] = acc[s][r];
     }
   }
 }
@@ -806,10 +954,11 @@ int panel_factor(double* P, int64_t ldp, int64_t m, int64_t w, int64_t row0, int
 // panel (wp = 0 for the first step); (k, w): this step's panel (w = 0 for the
 // closing step that only finishes the previous update).
 int lu_step(double* A, int64_t lda, int64_t n, int64_t kp, int64_t wp, const int* pairs_prev,
-            int64_t k, int64_t w, int mode, int* piv, int* info, int* pairs, hipStream_t s) {
+            int64_t k, int64_t w, int mode, int* piv, int* info, int* pairs, hipStream_t s,
+            const double* buf) {
   if (wp > kStripMaxW || w > 16) return GELIM_FAIL(GELIM_E_ARG, "lu_step: panel wider than 16");
   StepArgs a{A, lda, (int)n, (int)kp, (int)wp, pairs_prev, (int)k, (int)w, piv, info, pairs, 0,
-             nullptr, panel_io_mode()};
+             nullptr, panel_io_mode(), (w > 0 && wp > 0) ? buf : nullptr};
   const int64_t c0 = (w > 0) ? k + w : n;
   a.wide_c0 = (int)c0;
   const int64_t nwide = (wp > 0) ? (n + 1 - c0 + kStripCols - 1) / kStripCols : 0;
@@ -824,6 +973,19 @@ int lu_step(double* A, int64_t lda, int64_t n, int64_t kp, int64_t wp, const int
   if (m <= 16384 && w <= 2) return launch_step<512, 32, 2>(a, mode, blocks, s);
   return GELIM_FAIL(GELIM_E_ARG, "lu_step: m=" + std::to_string(m) + " w=" + std::to_string(w) +
                                      " exceeds the register-resident panel");
+}
+
+// Step (kp, wp) applied to the next panel's strip [k, k + w) into buf
+// (rows relative to kp, ld 16).  buf must hold (n - kp) x 16 doubles.
+int lu_narrow(double* A, int64_t lda, int64_t n, int64_t kp, int64_t wp, const int* pairs,
+              int64_t k, int64_t w, double* buf, hipStream_t s) {
+  if (wp > kStripMaxW || w > kStripCols) return GELIM_FAIL(GELIM_E_ARG, "lu_narrow: width > 16");
+  const int64_t m = n - kp;
+  NarrowArgs a{A + kp * lda + k, lda, (int)w, A + kp * lda + kp, lda, (int)wp, (int)m, pairs, buf};
+  hipLaunchKernelGGL(narrow_kernel, dim3((unsigned)((m + kNarrowRows - 1) / kNarrowRows)), dim3(256), 0,
+                     s, a);
+  HIP_TRY(hipGetLastError());
+  return GELIM_OK;
 }
 
 }  // namespace gelim
@@ -921,9 +1083,9 @@ extern "C" int gelim_debug_step_stamps(int64_t n, int64_t j, double* out) {
   HIP_TRY(hipMemcpy(A, h.data(), h.size() * 8, hipMemcpyHostToDevice));
   for (int64_t i = 0; i < j; ++i)
     GELIM_TRY(lu_step(A, lda, n, i ? 16 * (i - 1) : 0, i ? 16 : 0, i ? pairs + (i - 1) * 72 : nullptr,
-                      16 * i, 16, GELIM_PIVOT_PARTIAL, piv, info, pairs + i * 72, 0));
+                      16 * i, 16, GELIM_PIVOT_PARTIAL, piv, info, pairs + i * 72, 0, nullptr));
   StepArgs a{A, lda, (int)n, (int)(16 * (j - 1)), 16, pairs + (j - 1) * 72, (int)(16 * j), 16,
-             piv, info, pairs + j * 72, (int)(16 * j + 16), st, panel_io_mode()};
+             piv, info, pairs + j * 72, (int)(16 * j + 16), st, panel_io_mode(), nullptr};
   const int64_t m = n - 16 * j;
   const unsigned nwide = (unsigned)((n + 1 - (16 * j + 16) + 15) / 16);
   constexpr size_t lds = Panel<512, 4, 16, 1, false>::stage_bytes();

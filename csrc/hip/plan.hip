@@ -19,7 +19,10 @@ int64_t panel_width_for(int64_t m);
 int panel_factor(double* P, int64_t ldp, int64_t m, int64_t w, int64_t row0, int mode, int* piv,
                  int* info, hipStream_t s, int* pairs);
 int lu_step(double* A, int64_t lda, int64_t n, int64_t kp, int64_t wp, const int* pairs_prev,
-            int64_t k, int64_t w, int mode, int* piv, int* info, int* pairs, hipStream_t s);
+            int64_t k, int64_t w, int mode, int* piv, int* info, int* pairs, hipStream_t s,
+            const double* buf);
+int lu_narrow(double* A, int64_t lda, int64_t n, int64_t kp, int64_t wp, const int* pairs,
+              int64_t k, int64_t w, double* buf, hipStream_t s);
 int pairs_trsm(double* C, int64_t ldc, int64_t ncols, const double* L, int64_t ldl, int64_t w,
                const int* pairs, hipStream_t s);
 int swap_trsm(double* C, int64_t ldc, int64_t ncols, const double* L, int64_t ldl, int64_t w,
@@ -52,6 +55,8 @@ struct gelim_gauss_plan {
   int* pairs = nullptr;                  // per-step net row movement
   bool lookahead = false;                // GELIM_LOOKAHEAD=1: side-stream wide updates
   bool fused = true;                     // GELIM_SCHEDULE=classic: separate update kernels
+  bool narrow = true;                    // GELIM_NARROW=0: next strip updated by the panel WG
+  double* sbuf = nullptr;                // narrow-kernel strip buffer ((n + 16) x 16)
   hipGraphExec_t exec = nullptr;
   const void* k_src = nullptr;
   int64_t k_ld = 0;
@@ -76,14 +81,21 @@ int enqueue(gelim_gauss_plan* p, const void* src, int64_t src_ld, void* dx, void
     // panel i's columns and factors panel i while the other workgroups apply
     // step i-1 to the columns right of panel i; a closing launch applies the
     // last step to b.  S+1 launches, stream-ordered, no events.
+    // With narrow (default) a small many-workgroup kernel between the steps
+    // applies step i to panel i+1's strip, so the panel workgroup starts on
+    // an up-to-date strip.
     double* A = static_cast<double*>(p->work);
     const size_t S = p->step_k.size();
+    const bool nar = p->narrow;
     for (size_t i = 0; i <= S; ++i) {
       const int64_t kp = i ? p->step_k[i - 1] : 0, wp = i ? p->step_w[i - 1] : 0;
       const int64_t k = i < S ? p->step_k[i] : n, w = i < S ? p->step_w[i] : 0;
       const int* prev = i ? p->pairs + (i - 1) * kPairSlot : nullptr;
       int* cur = i < S ? p->pairs + i * kPairSlot : nullptr;
-      GELIM_TRY(lu_step(A, lda, n, kp, wp, prev, k, w, p->pivot, p->piv, p->info, cur, s));
+      GELIM_TRY(lu_step(A, lda, n, kp, wp, prev, k, w, p->pivot, p->piv, p->info, cur, s,
+                        nar ? p->sbuf : nullptr));
+      if (nar && i + 1 < S)
+        GELIM_TRY(lu_narrow(A, lda, n, k, w, cur, p->step_k[i + 1], p->step_w[i + 1], p->sbuf, s));
     }
     return backsub_f64(A, lda, A + n, lda, static_cast<double*>(dx),
                        static_cast<double*>(bnorm), n, 0, p->yw, s);
@@ -188,6 +200,7 @@ extern "C" gelim_gauss_plan* gelim_gauss_plan_create(int64_t n, int algo, int pi
   if (const char* e = std::getenv("GELIM_LOOKAHEAD")) p->lookahead = std::atoi(e) != 0;
   if (const char* e = std::getenv("GELIM_SCHEDULE")) p->fused = std::string(e) != "classic";
   if (p->lookahead) p->fused = false;
+  if (const char* e = std::getenv("GELIM_NARROW")) p->narrow = std::atoi(e) != 0;
   if (algo == GELIM_GPU_BLOCKED) {
     for (int64_t k = 0; k < n;) {
       const int64_t w = std::min<int64_t>(gelim::panel_width_for(n - k), n - k);
@@ -203,6 +216,7 @@ extern "C" gelim_gauss_plan* gelim_gauss_plan_create(int64_t n, int algo, int pi
       for (auto& e : *v)
         if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return fail("event");
     if (hipMalloc((void**)&p->pairs, sizeof(int) * kPairSlot * S) != hipSuccess) return fail("pairs");
+    if (hipMalloc((void**)&p->sbuf, sizeof(double) * 16 * (n + 16)) != hipSuccess) return fail("sbuf");
   }
   (void)hipMemset(p->work, 0, (size_t)(n * p->lda * dtype_bytes));
   return p;
@@ -217,6 +231,7 @@ extern "C" void gelim_gauss_plan_destroy(gelim_gauss_plan* p) {
     for (auto& e : *v)
       if (e) (void)hipEventDestroy(e);
   (void)hipFree(p->pairs);
+  (void)hipFree(p->sbuf);
   (void)hipFree(p->work);
   (void)hipFree(p->piv);
   (void)hipFree(p->info);

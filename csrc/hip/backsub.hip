@@ -31,24 +31,29 @@ __global__ void copy_y_kernel(const T* __restrict__ U, int64_t ldu, const T* __r
   if (bnorm) bnorm[i] = unit ? v : v / (double)U[(int64_t)i * ldu + i];
 }
 
+// One wave solves the nb x nb diagonal block at i0: lane l keeps row l in
+// registers; x_i is broadcast with v_readlane (i is wave-uniform) — no LDS,
+// no shuffles on the serial chain.
 template <typename T>
-__global__ __launch_bounds__(64) void diag_solve_kernel(const T* __restrict__ U, int64_t ldu,
-                                                        double* __restrict__ yw,
-                                                        double* __restrict__ x, int i0, int nb,
-                                                        int unit) {
-  // lane l keeps row l of the 64x64 block in registers; x_i is broadcast with
-  // v_readlane (i is wave-uniform) — no LDS, no shuffles on the serial chain
-  const int l = threadIdx.x;
+__device__ __forceinline__ void diag_solve_wave(const T* __restrict__ U, int64_t ldu,
+                                                double* __restrict__ yw, double* __restrict__ x,
+                                                int i0, int nb, int unit) {
+  const int l = threadIdx.x & 63;
   double row[kBS];
   const T* src = U + (int64_t)(i0 + min(l, nb - 1)) * ldu + i0;
 #pragma unroll
   for (int c = 0; c < kBS; ++c) row[c] = (l < nb && c < nb) ? (double)src[min(c, nb - 1)] : 0.0;
-  double yv = (l < nb) ? yw[i0 + l] : 0.0;
+  const int lc = min(l, nb - 1);
+  double yv = dev::load_sel(yw + i0 + lc, l < nb);
+  // reciprocal of every lane's own diagonal, computed in parallel up front:
+  // the serial chain is then mul -> readlane -> fma per step
+  const double dg = dev::load_sel(U + (int64_t)(i0 + lc) * ldu + i0 + lc, l < nb, T(1));
+  const double rinv = unit ? 1.0 : 1.0 / dg;
   double xv = 0.0;
 #pragma unroll
   for (int i = kBS - 1; i >= 0; --i) {
     if (i < nb) {
-      const double xi_l = unit ? yv : yv / row[i];  // meaningful in lane i only
+      const double xi_l = yv * rinv;  // meaningful in lane i only
       const double xi = __builtin_bit_cast(
           double, ((uint64_t)(unsigned)__builtin_amdgcn_readlane(
                        (int)(__builtin_bit_cast(uint64_t, xi_l) >> 32), i)
@@ -59,6 +64,56 @@ __global__ __launch_bounds__(64) void diag_solve_kernel(const T* __restrict__ U,
     }
   }
   if (l < nb) x[i0 + l] = xv;
+}
+
+template <typename T>
+__global__ __launch_bounds__(64) void diag_solve_kernel(const T* __restrict__ U, int64_t ldu,
+                                                        double* __restrict__ yw,
+                                                        double* __restrict__ x, int i0, int nb,
+                                                        int unit) {
+  diag_solve_wave<T>(U, ldu, yw, x, i0, nb, unit);
+}
+
+// One launch per block (fused form of update_kernel + diag_solve_kernel):
+// every workgroup subtracts block [i0, i0+nb)'s solved x from its rows above
+// (wave per row); workgroup 0 owns the 64 rows right above the block and,
+// once they are final, solves that diagonal block too, so the next launch
+// can go on with it.
+template <typename T>
+__global__ __launch_bounds__(256) void backsub_step_kernel(const T* __restrict__ U, int64_t ldu,
+                                                           double* __restrict__ yw,
+                                                           double* __restrict__ x, int i0, int nb,
+                                                           int unit) {
+  const int lane = threadIdx.x & 63;
+  const int wv = threadIdx.x >> 6;
+  const int p0 = i0 > kBS ? i0 - kBS : 0;  // the next diagonal block [p0, i0)
+  const double xl = dev::load_sel(x + i0 + min(lane, nb - 1), lane < nb);
+  if (blockIdx.x == 0) {
+    // the 64 rows [p0, i0): 16 per wave, every load in flight before the sums
+    constexpr int kRows = kBS / 4;
+    double v[kRows];
+#pragma unroll
+    for (int k = 0; k < kRows; ++k) {
+      const int r = p0 + wv * kRows + k;
+      v[k] = dev::load_sel(U + (int64_t)min(r, i0 - 1) * ldu + i0 + min(lane, nb - 1),
+                           lane < nb && r < i0) * xl;
+    }
+#pragma unroll
+    for (int k = 0; k < kRows; ++k) {
+      const int r = p0 + wv * kRows + k;
+      const double sum = dev::wave_sum(v[k]);
+      if (lane == 0 && r < i0) yw[r] -= sum;
+    }
+    __syncthreads();
+    if (wv == 0) diag_solve_wave<T>(U, ldu, yw, x, p0, i0 - p0, unit);
+    return;
+  }
+  const int nw = (gridDim.x - 1) * 4;
+  for (int r = (blockIdx.x - 1) * 4 + wv; r < p0; r += nw) {
+    double v = dev::load_sel(U + (int64_t)r * ldu + i0 + min(lane, nb - 1), lane < nb) * xl;
+    v = dev::wave_sum(v);
+    if (lane == 0) yw[r] -= v;
+  }
 }
 
 template <typename T>
@@ -83,18 +138,19 @@ int backsub_impl(const T* U, int64_t ldu, const T* y, int64_t incy, double* x, d
   hipLaunchKernelGGL(copy_y_kernel<T>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, U, ldu,
                      y, incy, yw, bnorm, (int)n, unit);
   HIP_TRY(hipGetLastError());
-  for (int64_t i1 = n; i1 > 0; i1 -= kBS) {
-    const int64_t i0 = i1 > kBS ? i1 - kBS : 0;
+  // last diagonal block, then one fused launch per block: update the rows
+  // above with its x and solve the next diagonal block
+  int64_t i0 = (n - 1) / kBS * kBS;
+  hipLaunchKernelGGL(diag_solve_kernel<T>, dim3(1), dim3(64), 0, s, U, ldu, yw, x, (int)i0,
+                     (int)(n - i0), unit);
+  HIP_TRY(hipGetLastError());
+  for (int64_t i1 = n; i0 > 0; i1 = i0, i0 -= kBS) {
     const int nb = (int)(i1 - i0);
-    hipLaunchKernelGGL(diag_solve_kernel<T>, dim3(1), dim3(64), 0, s, U, ldu, yw, x, (int)i0, nb,
-                       unit);
+    const int64_t rows = i0 > kBS ? i0 - kBS : 0;  // rows above the next block
+    const int blocks = 1 + (int)std::min<int64_t>((rows + 3) / 4, 1024);
+    hipLaunchKernelGGL(backsub_step_kernel<T>, dim3(blocks), dim3(256), 0, s, U, ldu, yw, x,
+                       (int)i0, nb, unit);
     HIP_TRY(hipGetLastError());
-    if (i0 > 0) {
-      const int blocks = (int)std::min<int64_t>((i0 + 3) / 4, 1024);
-      hipLaunchKernelGGL(update_kernel<T>, dim3(blocks), dim3(256), 0, s, U, ldu, yw, x,
-                         (int)i0, nb);
-      HIP_TRY(hipGetLastError());
-    }
   }
   return GELIM_OK;
 }

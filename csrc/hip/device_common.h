@@ -119,6 +119,17 @@ __device__ __forceinline__ unsigned wave_min_u32(unsigned v) {
   return (unsigned)__builtin_amdgcn_readlane((int)v, 63);
 }
 
+// Masked load without control flow: p must be a valid address (callers
+// clamp their indices), the value is selected afterwards.  Written as
+// `ok ? p[i] : 0`, LLVM turns each masked load into an exec-masked branch
+// that ends in its own s_waitcnt vmcnt(0) — independent loads then run one
+// after another instead of being in flight together.
+template <typename T>
+__device__ __forceinline__ T load_sel(const T* p, bool ok, T dflt = T(0)) {
+  const T v = *p;
+  return ok ? v : dflt;
+}
+
 // Pivot key of a candidate row.  PARTIAL: |a| (NaN never wins).  ZERO
 // (reference internal getPivot): the diagonal if non-zero, else the first
 // non-zero row — encoded as 2 for a non-zero diagonal, 1 for any other

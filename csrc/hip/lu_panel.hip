@@ -345,18 +345,15 @@ struct Panel {
                                                      int64_t ldp, int m, int t) {
 #pragma unroll
     for (int i = 0; i < R; ++i) {
-      const int lr = t + i * NT;
-      if (lr < m) {
-        const double2* src = reinterpret_cast<const double2*>(P + (int64_t)lr * ldp);
+      // rows >= m read row m-1 (never live, values unused): no branch, so
+      // every load of the strip is in flight at once
+      const int lr = min(t + i * NT, m - 1);
+      const double2* src = reinterpret_cast<const double2*>(P + (int64_t)lr * ldp);
 #pragma unroll
-        for (int c = 0; c < W / 2; ++c) {
-          const double2 v = src[c];
-          a[i][2 * c] = v.x;
-          a[i][2 * c + 1] = v.y;
-        }
-      } else {
-#pragma unroll
-        for (int c = 0; c < W; ++c) a[i][c] = 0.0;
+      for (int c = 0; c < W / 2; ++c) {
+        const double2 v = src[c];
+        a[i][2 * c] = v.x;
+        a[i][2 * c + 1] = v.y;
       }
     }
   }
@@ -436,40 +433,48 @@ __device__ __forceinline__ void panel_body(double* __restrict__ P, int64_t ldp, 
   // Compact ids: rows < w keep their index; a chosen row >= w selected at
   // step j gets id w + j.  Compact positions use the same numbering (the
   // only positions >= w ever touched are original places of chosen rows).
-  if (t == 0) {
-    for (int x = 0; x < 2 * w; ++x) {
-      sh.pos_of[x] = x;
-      sh.row_at[x] = x;
-    }
+  // Wave 0 runs the w-step simulation in registers (lane x holds pos_of[x]
+  // and row_at[x]; every index is wave-uniform, so reads are v_readlane and
+  // writes are lane selects) — no serial LDS round trips.
+  if (wave == 0) {
+    const int selv = (lane < w) ? sh.sel[lane] : 0;  // lane j: row chosen at step j
+    int pos = lane, rat = lane, pivv = 0;
     for (int j = 0; j < w; ++j) {
-      const int p = sh.sel[j];
+      const int p = __builtin_amdgcn_readlane(selv, j);
       const int idp = p < w ? p : w + j;
-      const int cur = sh.pos_of[idp];
-      const int other = sh.row_at[j];
-      sh.row_at[j] = idp;
-      sh.row_at[cur] = other;
-      sh.pos_of[idp] = j;
-      sh.pos_of[other] = cur;
-      sh.piv[j] = cur < w ? cur : sh.sel[cur - w];
+      const int cur = __builtin_amdgcn_readlane(pos, idp);
+      const int other = __builtin_amdgcn_readlane(rat, j);
+      rat = (lane == j) ? idp : rat;  // row_at[j] = idp; row_at[cur] = other
+      rat = (lane == cur) ? other : rat;
+      pos = (lane == idp) ? j : pos;  // pos_of[idp] = j; pos_of[other] = cur
+      pos = (lane == other) ? cur : pos;
+      const int pj = cur < w ? cur : __builtin_amdgcn_readlane(selv, cur < w ? 0 : cur - w);
+      pivv = (lane == j) ? pj : pivv;
+    }
+    if (lane < w) sh.piv[lane] = pivv;
+    if (lane < 2 * w) {
+      sh.pos_of[lane] = pos;
+      sh.row_at[lane] = rat;
     }
     // net row movement as (dst, src) pairs for the trailing-column kernels:
     // new_row[dst] = old_row[src] over the <= 2w touched rows
     if (pairs) {
-      int np = 0;
-      for (int x = 0; x < 2 * w; ++x) {
-        // compact position w+j stands for actual position sel[j] only when
-        // that row lies below the panel top (otherwise it is unused)
-        if (x >= w && sh.sel[x - w] < w) continue;
-        const int ap = x < w ? x : sh.sel[x - w];
-        const int id = sh.row_at[x];
-        const int ar = id < w ? id : sh.sel[id - w];
-        if (ap != ar) {
-          pairs[1 + 2 * np] = ap;
-          pairs[2 + 2 * np] = ar;
-          ++np;
-        }
+      // compact position w+j stands for actual position sel[j] only when
+      // that row lies below the panel top (otherwise it is unused)
+      const int xs = (lane >= w && lane < 2 * w) ? lane - w : 0;
+      const int selx = __shfl(selv, xs);
+      const int id = rat;
+      const int selid = __shfl(selv, (id >= w && id < 2 * w) ? id - w : 0);
+      const int ap = lane < w ? lane : selx;
+      const int ar = id < w ? id : selid;
+      const bool emit = lane < 2 * w && !(lane >= w && selx < w) && ap != ar;
+      const uint64_t mask = __ballot(emit);
+      const int k = __popcll(mask & ((1ull << lane) - 1ull));
+      if (emit) {
+        pairs[1 + 2 * k] = ap;
+        pairs[2 + 2 * k] = ar;
       }
-      pairs[0] = np;
+      if (lane == 0) pairs[0] = __popcll(mask);
     }
   }
   __syncthreads();
@@ -618,20 +623,27 @@ __device__ __forceinline__ void strip_update(double* __restrict__ C, int64_t ldc
   const int c = t & (kStripCols - 1);
   const int e = t >> 4;
   const bool colok = c < ncols;
+  const int cc = min(c, ncols - 1);  // clamped column: every load below is unconditional
   if (t < 1 + 4 * kStripMaxW) {
     const int np = pairs[0];
-    sh.pr[t] = (t == 0 || t <= 2 * np) ? pairs[t] : 0;
+    sh.pr[t] = dev::load_sel(pairs + t, t == 0 || t <= 2 * np);
   }
   if (t < kStripMaxW * kStripMaxW) {
     const int r = t / kStripMaxW, q = t % kStripMaxW;
-    sh.l11[r][q] = (q < r && r < wp) ? L[(int64_t)r * ldl + q] : 0.0;
+    const int rc = min(r, wp - 1), qc = min(q, wp - 1);
+    sh.l11[r][q] = dev::load_sel(L + (int64_t)rc * ldl + qc, q < r && r < wp);
   }
+  const double top = dev::load_sel(C + (int64_t)min(e, wp - 1) * ldc + cc, e < wp && colok);
   __syncthreads();
   mark(0);
   const int np = sh.pr[0];
   // every source and every top row is read before anything is written
-  if (e < np && colok) sh.g[e][c] = C[(int64_t)sh.pr[2 + 2 * e] * ldc + c];
-  if (e < kStripMaxW) sh.x[e][c] = (e < wp && colok) ? C[(int64_t)e * ldc + c] : 0.0;
+  {
+    const int src = sh.pr[2 + 2 * min(e, 4 * kStripMaxW / 2 - 1)];  // 0 beyond np: row 0
+    const double gv = C[(int64_t)src * ldc + cc];
+    if (e < np && colok) sh.g[e][c] = gv;
+  }
+  if (e < kStripMaxW) sh.x[e][c] = top;
   __syncthreads();
   mark(1);
   if (e < np && colok) {
@@ -676,21 +688,24 @@ __device__ __forceinline__ void strip_update(double* __restrict__ C, int64_t ldc
       const int blk = b0 + kWaves * s;
       const int rbase = wp + 16 * blk;
       const int lrow = rbase + r16;
-      if (blk < nblk && lrow < m && 4 * q + 3 < wp) {
-        const double2* lp = reinterpret_cast<const double2*>(L + (int64_t)lrow * ldl + 4 * q);
-        const double2 v0 = lp[0], v1 = lp[1];
-        la[s][0] = v0.x; la[s][1] = v0.y; la[s][2] = v1.x; la[s][3] = v1.y;
-      } else if (blk < nblk && lrow < m) {  // partial last panel: stay inside the row
-        const double* lp = L + (int64_t)lrow * ldl + 4 * q;
+      // clamped rows / columns: unconditional loads, selects afterwards
+      const bool okb = blk < nblk && lrow < m;
+      const double* lp = L + (int64_t)min(lrow, m - 1) * ldl;
+      if (wp == kStripMaxW) {  // uniform: full panel, two 16-byte loads
+        const double2 v0 = reinterpret_cast<const double2*>(lp + 4 * q)[0];
+        const double2 v1 = reinterpret_cast<const double2*>(lp + 4 * q)[1];
+        la[s][0] = okb ? v0.x : 0.0; la[s][1] = okb ? v0.y : 0.0;
+        la[s][2] = okb ? v1.x : 0.0; la[s][3] = okb ? v1.y : 0.0;
+      } else {  // partial last panel: stay inside the row
 #pragma unroll
-        for (int e = 0; e < 4; ++e) la[s][e] = (4 * q + e < wp) ? lp[e] : 0.0;
-      } else {
-        la[s][0] = la[s][1] = la[s][2] = la[s][3] = 0.0;
+        for (int e = 0; e < 4; ++e)
+          la[s][e] = dev::load_sel(lp + min(4 * q + e, wp - 1), okb && 4 * q + e < wp);
       }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int row = rbase + q + 4 * r;
-        acc[s][r] = (blk < nblk && row < m && ccol) ? C[(int64_t)row * ldc + r16] : 0.0;
+        acc[s][r] = dev::load_sel(C + (int64_t)min(row, m - 1) * ldc + min(r16, ncols - 1),
+                                  blk < nblk && row < m && ccol);
       }
     }
 #pragma unroll
@@ -816,10 +831,12 @@ __global__ __launch_bounds__(256) void narrow_kernel(NarrowArgs g) {
     const int rr = t >> 4, cc = t & 15;
     if (t < 1 + 4 * kStripMaxW) {
       const int np = g.pairs[0];
-      pr[t] = (t == 0 || t <= 2 * np) ? g.pairs[t] : 0;
+      pr[t] = dev::load_sel(g.pairs + t, t == 0 || t <= 2 * np);
     }
-    l11[rr][cc] = (cc < rr && rr < wp) ? g.L[(int64_t)rr * g.ldl + cc] : 0.0;
-    x[rr][cc] = (rr < wp && cc < ncols) ? g.C[(int64_t)rr * g.ldc + cc] : 0.0;
+    l11[rr][cc] = dev::load_sel(g.L + (int64_t)min(rr, wp - 1) * g.ldl + min(cc, wp - 1),
+                                cc < rr && rr < wp);
+    x[rr][cc] = dev::load_sel(g.C + (int64_t)min(rr, wp - 1) * g.ldc + min(cc, ncols - 1),
+                              rr < wp && cc < ncols);
     srcmap[t] = r0 + t;
   }
   __syncthreads();
@@ -828,7 +845,7 @@ __global__ __launch_bounds__(256) void narrow_kernel(NarrowArgs g) {
   for (int idx = t; idx < np * kStripCols; idx += 256) {
     const int e = idx >> 4, cc = idx & 15;
     const int d = pr[1 + 2 * e];
-    if (d < wp) x[d][cc] = (cc < ncols) ? g.C[(int64_t)pr[2 + 2 * e] * g.ldc + cc] : 0.0;
+    if (d < wp) x[d][cc] = dev::load_sel(g.C + (int64_t)pr[2 + 2 * e] * g.ldc + min(cc, ncols - 1), cc < ncols);
   }
   if (t < np) {
     const int d = pr[1 + 2 * t];
@@ -863,21 +880,23 @@ __global__ __launch_bounds__(256) void narrow_kernel(NarrowArgs g) {
     const int rbase = a0 + 16 * blk;
     const int lrow = rbase + r16;
     const bool okb = blk < nblk && lrow < r1;
-    if (okb && 4 * q + 3 < wp) {
-      const double2* lp = reinterpret_cast<const double2*>(g.L + (int64_t)lrow * g.ldl + 4 * q);
-      const double2 v0 = lp[0], v1 = lp[1];
-      la[s][0] = v0.x; la[s][1] = v0.y; la[s][2] = v1.x; la[s][3] = v1.y;
-    } else if (okb) {
-      const double* lp = g.L + (int64_t)lrow * g.ldl + 4 * q;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) la[s][e] = (4 * q + e < wp) ? lp[e] : 0.0;
+    const double* lp = g.L + (int64_t)min(lrow, r1 - 1) * g.ldl;
+    if (wp == kStripMaxW) {  // uniform: full panel, two 16-byte loads
+      const double2 v0 = reinterpret_cast<const double2*>(lp + 4 * q)[0];
+      const double2 v1 = reinterpret_cast<const double2*>(lp + 4 * q)[1];
+      la[s][0] = okb ? v0.x : 0.0; la[s][1] = okb ? v0.y : 0.0;
+      la[s][2] = okb ? v1.x : 0.0; la[s][3] = okb ? v1.y : 0.0;
     } else {
-      la[s][0] = la[s][1] = la[s][2] = la[s][3] = 0.0;
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        la[s][e] = dev::load_sel(lp + min(4 * q + e, wp - 1), okb && 4 * q + e < wp);
     }
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int row = rbase + q + 4 * r;
-      acc[s][r] = (blk < nblk && row < r1 && ccol) ? g.C[(int64_t)srcmap[row - r0] * g.ldc + r16] : 0.0;
+      const int rowc = min(max(row, r0), r1 - 1);
+      acc[s][r] = dev::load_sel(g.C + (int64_t)srcmap[rowc - r0] * g.ldc + min(r16, ncols - 1),
+                                blk < nblk && row < r1 && ccol);
     }
   }
 #pragma unroll

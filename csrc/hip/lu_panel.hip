@@ -309,6 +309,44 @@ struct Panel {
     }
   }
 
+  // Coalesced loads of EVERY slot issued up front (one memory latency, 8
+  // cache lines per instruction instead of 64), then a swizzled LDS transpose
+  // slot by slot into the row-per-thread layout.  Rows >= m read row m-1.
+  static __device__ __forceinline__ void stage_in_all(double (&a)[R][W], const double* __restrict__ P,
+                                                      int64_t ldp, int m, int t) {
+    constexpr int CH = W / 2;     // 16-byte chunks per row
+    constexpr int RPP = NT / CH;  // rows per coalesced pass
+    double2* tile = reinterpret_cast<double2*>(g_panel_dyn_lds);
+    const int ch = t % CH;
+    // a[i] first holds slot i's coalesced chunks (chunk `ch` of rows
+    // pass*RPP + t/CH), then, after the transpose, this thread's row
+#pragma unroll
+    for (int i = 0; i < R; ++i)
+#pragma unroll
+      for (int pass = 0; pass < CH; ++pass) {
+        const int lr = min(i * NT + pass * RPP + t / CH, m - 1);
+        const double2 v = *reinterpret_cast<const double2*>(P + (int64_t)lr * ldp + 2 * ch);
+        a[i][2 * pass] = v.x;
+        a[i][2 * pass + 1] = v.y;
+      }
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+#pragma unroll
+      for (int pass = 0; pass < CH; ++pass) {
+        const int rl = pass * RPP + t / CH;
+        tile[rl * CH + swz(rl, ch)] = make_double2(a[i][2 * pass], a[i][2 * pass + 1]);
+      }
+      __syncthreads();
+#pragma unroll
+      for (int c = 0; c < CH; ++c) {
+        const double2 v = tile[t * CH + swz(t, c)];
+        a[i][2 * c] = v.x;
+        a[i][2 * c + 1] = v.y;
+      }
+      __syncthreads();
+    }
+  }
+
   static __device__ __forceinline__ void stage_out(const double (&a)[R][W], const int (&dest)[R],
                                                    double* __restrict__ P, int64_t ldp, int m,
                                                    int t) {
@@ -400,6 +438,8 @@ __device__ __forceinline__ void panel_body(double* __restrict__ P, int64_t ldp, 
                       ((((uintptr_t)Pin) & 15) == 0) && (ldin % 2 == 0);
   if (staged && io == 1) {
     K::load_direct(a, Pin, ldin, m, t);
+  } else if (staged && io == 2) {
+    K::stage_in_all(a, Pin, ldin, m, t);
   } else if (staged) {
     K::stage_in(a, Pin, ldin, m, t);
   } else {
@@ -568,12 +608,14 @@ struct StepArgs {
 
 constexpr int kBufLd = 16;  // row stride of the narrow strip buffer (doubles)
 
-// Panel IO of the fused step: 1 (default) direct 16-byte register loads and
-// stores (one memory latency for the whole strip), 0 LDS-staged coalesced
-// passes.  GELIM_PANEL_IO overrides (read per launch, for A/B runs).
+// Panel IO of the fused step: 2 (default) every coalesced load in flight at
+// once + LDS transpose, LDS-staged coalesced stores; 1 direct 16-byte
+// register loads/stores (uncoalesced: 64 cache lines per instruction); 0
+// LDS-staged passes one slot at a time.  GELIM_PANEL_IO overrides (read per
+// launch, for A/B runs).
 int panel_io_mode() {
   const char* e = std::getenv("GELIM_PANEL_IO");
-  return e ? std::atoi(e) : 1;
+  return e ? std::atoi(e) : 2;
 }
 
 __device__ __forceinline__ unsigned long long realtime_now() {
@@ -749,9 +791,9 @@ __global__ __launch_bounds__(NT) void step_kernel(StepArgs g) {
         g.A[(int64_t)(g.kp + r) * lda + g.k + c] = g.buf[r * kBufLd + c];
     }
     if constexpr (STAMP) t1 = realtime_now();
-    panel_body<NT, R, W, MODE, false>(g.A + (int64_t)g.k * lda + g.k, lda, g.n - g.k, g.w, g.k,
-                                      g.piv + g.k, g.info, nullptr, g.pairs, sh, g.io,
-                                      g.buf + (int64_t)g.wp * kBufLd, kBufLd);
+    panel_body<NT, R, W, MODE, STAMP>(g.A + (int64_t)g.k * lda + g.k, lda, g.n - g.k, g.w, g.k,
+                                      g.piv + g.k, g.info, STAMP ? g.stamps + 700 : nullptr,
+                                      g.pairs, sh, g.io, g.buf + (int64_t)g.wp * kBufLd, kBufLd);
     if constexpr (STAMP) {
       __syncthreads();
       if (threadIdx.x == 0) {
@@ -1100,11 +1142,19 @@ extern "C" int gelim_debug_step_stamps(int64_t n, int64_t j, double* out) {
     for (int64_t c = 0; c <= n; ++c)
       h[r * lda + c] = (double)(((r * 7919 + c * 104729) * 2654435761ull) % 2000) / 1000.0 - 1.0;
   HIP_TRY(hipMemcpy(A, h.data(), h.size() * 8, hipMemcpyHostToDevice));
-  for (int64_t i = 0; i < j; ++i)
+  double* sbuf = nullptr;
+  HIP_TRY(hipMalloc((void**)&sbuf, sizeof(double) * 16 * (n + 16)));
+  const char* en = std::getenv("GELIM_NARROW");
+  const bool nar = !en || std::atoi(en) != 0;
+  for (int64_t i = 0; i < j; ++i) {
     GELIM_TRY(lu_step(A, lda, n, i ? 16 * (i - 1) : 0, i ? 16 : 0, i ? pairs + (i - 1) * 72 : nullptr,
-                      16 * i, 16, GELIM_PIVOT_PARTIAL, piv, info, pairs + i * 72, 0, nullptr));
+                      16 * i, 16, GELIM_PIVOT_PARTIAL, piv, info, pairs + i * 72, 0,
+                      nar ? sbuf : nullptr));
+    if (nar) GELIM_TRY(lu_narrow(A, lda, n, 16 * i, 16, pairs + i * 72, 16 * (i + 1), 16, sbuf, 0));
+  }
   StepArgs a{A, lda, (int)n, (int)(16 * (j - 1)), 16, pairs + (j - 1) * 72, (int)(16 * j), 16,
-             piv, info, pairs + j * 72, (int)(16 * j + 16), st, panel_io_mode(), nullptr};
+             piv, info, pairs + j * 72, (int)(16 * j + 16), st, panel_io_mode(),
+             nar ? sbuf : nullptr};
   const int64_t m = n - 16 * j;
   const unsigned nwide = (unsigned)((n + 1 - (16 * j + 16) + 15) / 16);
   constexpr size_t lds = Panel<512, 4, 16, 1, false>::stage_bytes();
@@ -1128,6 +1178,11 @@ extern "C" int gelim_debug_step_stamps(int64_t n, int64_t j, double* out) {
   out[4] = wd.empty() ? 0 : wd[wd.size() / 2];
   out[5] = (double)wd.size();
   for (int i = 0; i < 6; ++i) out[6 + i] = hs[600 + i] ? (double)(hs[600 + i] - base) : 0.0;
+  // panel internals (s_memtime cycles -> 10 ns ticks at 2.4 GHz): load, steps, store
+  out[12] = (double)(hs[701] - hs[700]) / 24.0;
+  out[13] = (double)(hs[702] - hs[701]) / 24.0;
+  out[14] = (double)(hs[703] - hs[702]) / 24.0;
+  (void)hipFree(sbuf);
   (void)hipFree(A);
   (void)hipFree(piv);
   (void)hipFree(info);

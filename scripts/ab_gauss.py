@@ -18,7 +18,9 @@ variants = {}
 # plans read GELIM_* at creation; GELIM_PANEL_IO is read at every enqueue, so
 # the io variants run eagerly with the variable set around each solve
 VARIANTS = {
-    "fused+narrow": {"GELIM_SCHEDULE": "fused", "GELIM_LOOKAHEAD": "0", "GELIM_PANEL_IO": "1", "GELIM_NARROW": "1"},
+    "fused+narrow io=2": {"GELIM_SCHEDULE": "fused", "GELIM_LOOKAHEAD": "0", "GELIM_PANEL_IO": "2", "GELIM_NARROW": "1"},
+    "fused+narrow io=1": {"GELIM_SCHEDULE": "fused", "GELIM_LOOKAHEAD": "0", "GELIM_PANEL_IO": "1", "GELIM_NARROW": "1"},
+    "fused+narrow io=0": {"GELIM_SCHEDULE": "fused", "GELIM_LOOKAHEAD": "0", "GELIM_PANEL_IO": "0", "GELIM_NARROW": "1"},
     "fused prologue": {"GELIM_SCHEDULE": "fused", "GELIM_LOOKAHEAD": "0", "GELIM_PANEL_IO": "1", "GELIM_NARROW": "0"},
     "classic": {"GELIM_SCHEDULE": "classic", "GELIM_LOOKAHEAD": "0", "GELIM_PANEL_IO": "0", "GELIM_NARROW": "0"},
 }

@@ -1,15 +1,26 @@
 // Back substitution U x = y on the GPU (the reference's solveGauss,
-// Pthreads/Version-1/gauss_internal_input.c:212-227, which is a serial O(n^2)
-// loop there).
+// Pthreads/Version-1/gauss_internal_input.c:212-227, a serial O(n^2) loop
+// there).
 //
-// Blocked right-to-left: for each 64-row diagonal block (bottom-up)
-//   diag kernel   : one wave64 solves the 64x64 triangle, the block staged in
-//                   LDS, x_i broadcast across lanes with a shuffle;
-//   update kernel : y[0:i0] -= U[0:i0, blk] x_blk, one wave per row,
-//                   coalesced 512-byte row segments + shuffle reduction.
-// A leading copy kernel gathers y (a strided column of the augmented matrix)
-// into a contiguous work vector and optionally emits the reference's
-// transformed B = y_i / U_ii (printed by VERIFY, P1i:292-295).
+// Default: ONE persistent launch (backsub_persist_kernel).  Row block b (64
+// equations) belongs to workgroup b and x is produced bottom-up.  Every
+// workgroup preloads its 64x64 diagonal triangle into wave 0's registers,
+// then takes the solved x blocks below it in order (last block first): for
+// each it prefetches the matching 64x64 block of U BEFORE polling that
+// block's flag, so after the hand-off only x_c (512 B) is read, and
+// subtracts U[b, c] x_c (wave per row, shuffle sums).  After the last one,
+// wave 0 solves the triangle (rows in lanes, x_i broadcast with v_readlane:
+// mul -> readlane -> fma per step) and publishes x_b (sc1 stores, drain,
+// flag).  The critical path per block is one hand-off + one block mat-vec +
+// the 64-step chain, instead of one dependent kernel launch per block.
+// Spins are bounded (200 ms) and report through an error word.
+//
+// Rows may be indirect: perm[i] is the row of U (and of y) that holds
+// equation i -- the resident LU (rlu.hip) leaves U rows at their physical
+// positions.  Without perm, row i is equation i.
+//
+// Fallback when the blocks cannot all be resident (more than 256 blocks,
+// n > 16384): one launch per block (backsub_step_kernel).
 #include <hip/hip_runtime.h>
 
 #include "device_common.h"
@@ -19,68 +30,162 @@ namespace gelim {
 namespace {
 
 constexpr int kBS = 64;
+constexpr int kMaxPersistBlocks = 256;
+constexpr unsigned long long kSpinTicks = 20000000ull;  // 200 ms at 100 MHz
+
+__device__ __forceinline__ int rowof(const int* perm, int i) { return perm ? perm[i] : i; }
+
+__device__ __forceinline__ unsigned long long rtc() {
+  unsigned long long t;
+  asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  return t;
+}
 
 template <typename T>
 __global__ void copy_y_kernel(const T* __restrict__ U, int64_t ldu, const T* __restrict__ y,
-                              int64_t incy, double* __restrict__ yw, double* __restrict__ bnorm,
-                              int n, int unit) {
+                              int64_t incy, const int* __restrict__ perm, double* __restrict__ yw,
+                              double* __restrict__ bnorm, int n, int unit) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const double v = (double)y[(int64_t)i * incy];
+  const int r = rowof(perm, i);
+  const double v = (double)y[(int64_t)r * incy];
   yw[i] = v;
-  if (bnorm) bnorm[i] = unit ? v : v / (double)U[(int64_t)i * ldu + i];
+  if (bnorm) bnorm[i] = unit ? v : v / (double)U[(int64_t)r * ldu + i];
 }
 
-// One wave solves the nb x nb diagonal block at i0: lane l keeps row l in
-// registers; x_i is broadcast with v_readlane (i is wave-uniform) — no LDS,
-// no shuffles on the serial chain.
+// Wave 0's copy of a diagonal block: lane l keeps equation i0+l's row
+// (columns i0..i0+nb) and the reciprocal of its diagonal.
 template <typename T>
-__device__ __forceinline__ void diag_solve_wave(const T* __restrict__ U, int64_t ldu,
-                                                double* __restrict__ yw, double* __restrict__ x,
-                                                int i0, int nb, int unit) {
+__device__ __forceinline__ void load_diag(const T* __restrict__ U, int64_t ldu, const int* perm, int i0,
+                                          int nb, int unit, double (&row)[kBS], double& rinv) {
   const int l = threadIdx.x & 63;
-  double row[kBS];
-  const T* src = U + (int64_t)(i0 + min(l, nb - 1)) * ldu + i0;
-#pragma unroll
-  for (int c = 0; c < kBS; ++c) row[c] = (l < nb && c < nb) ? (double)src[min(c, nb - 1)] : 0.0;
   const int lc = min(l, nb - 1);
-  double yv = dev::load_sel(yw + i0 + lc, l < nb);
-  // reciprocal of every lane's own diagonal, computed in parallel up front:
-  // the serial chain is then mul -> readlane -> fma per step
-  const double dg = dev::load_sel(U + (int64_t)(i0 + lc) * ldu + i0 + lc, l < nb, T(1));
-  const double rinv = unit ? 1.0 : 1.0 / dg;
+  const T* src = U + (int64_t)rowof(perm, i0 + lc) * ldu + i0;
+#pragma unroll
+  for (int c = 0; c < kBS; ++c) row[c] = dev::load_sel(src + min(c, nb - 1), l < nb && c < nb);
+  rinv = unit ? 1.0 : 1.0 / (double)src[lc];
+}
+
+// One wave solves the nb x nb triangle: x_i broadcast with v_readlane (i is
+// wave-uniform), so the serial chain is mul -> readlane -> fma per step.
+__device__ __forceinline__ double solve_diag(const double (&row)[kBS], double rinv, double yv, int nb) {
+  const int l = threadIdx.x & 63;
   double xv = 0.0;
 #pragma unroll
   for (int i = kBS - 1; i >= 0; --i) {
     if (i < nb) {
       const double xi_l = yv * rinv;  // meaningful in lane i only
+      const uint64_t b = __builtin_bit_cast(uint64_t, xi_l);
       const double xi = __builtin_bit_cast(
-          double, ((uint64_t)(unsigned)__builtin_amdgcn_readlane(
-                       (int)(__builtin_bit_cast(uint64_t, xi_l) >> 32), i)
-                   << 32) |
-                      (unsigned)__builtin_amdgcn_readlane((int)__builtin_bit_cast(uint64_t, xi_l), i));
+          double, ((uint64_t)(unsigned)__builtin_amdgcn_readlane((int)(b >> 32), i) << 32) |
+                      (unsigned)__builtin_amdgcn_readlane((int)b, i));
       if (l == i) xv = xi;
       yv = (l < i) ? fma(-row[i], xi, yv) : yv;
     }
   }
-  if (l < nb) x[i0 + l] = xv;
+  return xv;
 }
+
+template <typename T>
+__global__ __launch_bounds__(256) void backsub_persist_kernel(const T* __restrict__ U, int64_t ldu,
+                                                              const T* __restrict__ y, int64_t incy,
+                                                              const int* __restrict__ perm,
+                                                              double* __restrict__ x,
+                                                              double* __restrict__ bnorm, int n,
+                                                              int unit, unsigned* flags, int* err) {
+  __shared__ double acc[kBS];
+  __shared__ int prow[kBS];
+  __shared__ int ok[2];
+  const int b = blockIdx.x, nb = gridDim.x;
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int r0 = b * kBS, rows = min(kBS, n - r0);
+  if (t < kBS) {
+    const int i = r0 + min(t, rows - 1);
+    const int pr = rowof(perm, i);
+    prow[t] = pr;
+    const double v = (double)y[(int64_t)pr * incy];
+    acc[t] = v;
+    if (bnorm && t < rows) bnorm[i] = unit ? v : v / (double)U[(int64_t)pr * ldu + i];
+  }
+  double drow[kBS];
+  double rinv = 1.0;
+  if (wv == 0) load_diag<T>(U, ldu, perm, r0, rows, unit, drow, rinv);
+  __syncthreads();
+  // this wave's 16 equations of the block: their physical rows
+  int pr16[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) pr16[k] = prow[min(wv * 16 + k, rows - 1)];
+  int it = 0;
+  for (int c = nb - 1; c > b; --c, ++it) {
+    const int c0 = c * kBS, cw = min(kBS, n - c0);
+    const int cl = c0 + min(lane, cw - 1);
+    // U[b rows, block c] does not depend on x: in flight before the wait
+    double uv[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) uv[k] = (double)U[(int64_t)pr16[k] * ldu + cl];
+    if (t == 0) {
+      int good = 1;
+      if (__hip_atomic_load(&flags[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
+        const unsigned long long t0 = rtc();
+        while (__hip_atomic_load(&flags[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
+          if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0 ||
+              rtc() - t0 > kSpinTicks) {
+            __hip_atomic_store(err, 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            good = 0;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+        }
+      }
+      ok[it & 1] = good;
+    }
+    __syncthreads();
+    if (!ok[it & 1]) return;
+    // x_c was stored write-through by its producer: agent-scope loads
+    const double xl = lane < cw
+                          ? __builtin_bit_cast(double, __hip_atomic_load(reinterpret_cast<unsigned long long*>(x + c0 + lane),
+                                                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+                          : 0.0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const double v = dev::wave_sum(uv[k] * xl);
+      if (lane == 0 && wv * 16 + k < rows) acc[wv * 16 + k] -= v;
+    }
+  }
+  __syncthreads();
+  if (wv == 0) {
+    const double xv = solve_diag(drow, rinv, acc[min(lane, rows - 1)], rows);
+    if (lane < rows)
+      __hip_atomic_store(reinterpret_cast<unsigned long long*>(x + r0 + lane), __builtin_bit_cast(unsigned long long, xv),
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (t == 0) __hip_atomic_store(&flags[b], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// ---- fallback: one launch per block ----------------------------------------
 
 template <typename T>
 __global__ __launch_bounds__(64) void diag_solve_kernel(const T* __restrict__ U, int64_t ldu,
+                                                        const int* __restrict__ perm,
                                                         double* __restrict__ yw,
                                                         double* __restrict__ x, int i0, int nb,
                                                         int unit) {
-  diag_solve_wave<T>(U, ldu, yw, x, i0, nb, unit);
+  double row[kBS];
+  double rinv;
+  load_diag<T>(U, ldu, perm, i0, nb, unit, row, rinv);
+  const int l = threadIdx.x & 63;
+  const double xv = solve_diag(row, rinv, dev::load_sel(yw + i0 + min(l, nb - 1), l < nb), nb);
+  if (l < nb) x[i0 + l] = xv;
 }
 
-// One launch per block (fused form of update_kernel + diag_solve_kernel):
-// every workgroup subtracts block [i0, i0+nb)'s solved x from its rows above
+// Every workgroup subtracts block [i0, i0+nb)'s solved x from its rows above
 // (wave per row); workgroup 0 owns the 64 rows right above the block and,
-// once they are final, solves that diagonal block too, so the next launch
-// can go on with it.
+// once they are final, solves that diagonal block too.
 template <typename T>
 __global__ __launch_bounds__(256) void backsub_step_kernel(const T* __restrict__ U, int64_t ldu,
+                                                           const int* __restrict__ perm,
                                                            double* __restrict__ yw,
                                                            double* __restrict__ x, int i0, int nb,
                                                            int unit) {
@@ -89,13 +194,12 @@ __global__ __launch_bounds__(256) void backsub_step_kernel(const T* __restrict__
   const int p0 = i0 > kBS ? i0 - kBS : 0;  // the next diagonal block [p0, i0)
   const double xl = dev::load_sel(x + i0 + min(lane, nb - 1), lane < nb);
   if (blockIdx.x == 0) {
-    // the 64 rows [p0, i0): 16 per wave, every load in flight before the sums
     constexpr int kRows = kBS / 4;
     double v[kRows];
 #pragma unroll
     for (int k = 0; k < kRows; ++k) {
       const int r = p0 + wv * kRows + k;
-      v[k] = dev::load_sel(U + (int64_t)min(r, i0 - 1) * ldu + i0 + min(lane, nb - 1),
+      v[k] = dev::load_sel(U + (int64_t)rowof(perm, min(r, i0 - 1)) * ldu + i0 + min(lane, nb - 1),
                            lane < nb && r < i0) * xl;
     }
 #pragma unroll
@@ -105,28 +209,19 @@ __global__ __launch_bounds__(256) void backsub_step_kernel(const T* __restrict__
       if (lane == 0 && r < i0) yw[r] -= sum;
     }
     __syncthreads();
-    if (wv == 0) diag_solve_wave<T>(U, ldu, yw, x, p0, i0 - p0, unit);
+    if (wv == 0) {
+      double row[kBS];
+      double rinv;
+      load_diag<T>(U, ldu, perm, p0, i0 - p0, unit, row, rinv);
+      const int l = lane;
+      const double xv = solve_diag(row, rinv, dev::load_sel(yw + p0 + min(l, i0 - p0 - 1), l < i0 - p0), i0 - p0);
+      if (l < i0 - p0) x[p0 + l] = xv;
+    }
     return;
   }
   const int nw = (gridDim.x - 1) * 4;
   for (int r = (blockIdx.x - 1) * 4 + wv; r < p0; r += nw) {
-    double v = dev::load_sel(U + (int64_t)r * ldu + i0 + min(lane, nb - 1), lane < nb) * xl;
-    v = dev::wave_sum(v);
-    if (lane == 0) yw[r] -= v;
-  }
-}
-
-template <typename T>
-__global__ __launch_bounds__(256) void update_kernel(const T* __restrict__ U, int64_t ldu,
-                                                     double* __restrict__ yw,
-                                                     const double* __restrict__ x, int i0,
-                                                     int nb) {
-  const int lane = threadIdx.x & 63;
-  const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const int nwaves = (gridDim.x * blockDim.x) >> 6;
-  const double xl = (lane < nb) ? x[i0 + lane] : 0.0;
-  for (int r = wave; r < i0; r += nwaves) {
-    double v = (lane < nb) ? (double)U[(int64_t)r * ldu + i0 + lane] * xl : 0.0;
+    double v = dev::load_sel(U + (int64_t)rowof(perm, r) * ldu + i0 + min(lane, nb - 1), lane < nb) * xl;
     v = dev::wave_sum(v);
     if (lane == 0) yw[r] -= v;
   }
@@ -134,21 +229,34 @@ __global__ __launch_bounds__(256) void update_kernel(const T* __restrict__ U, in
 
 template <typename T>
 int backsub_impl(const T* U, int64_t ldu, const T* y, int64_t incy, double* x, double* bnorm,
-                 int64_t n, int unit, double* yw, hipStream_t s) {
-  hipLaunchKernelGGL(copy_y_kernel<T>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, U, ldu,
-                     y, incy, yw, bnorm, (int)n, unit);
+                 int64_t n, int unit, double* yw, hipStream_t s, const int* perm, int* err) {
+  const int64_t nblk = (n + kBS - 1) / kBS;
+  if (nblk <= kMaxPersistBlocks) {
+    // flags (+ the error word when the caller has none) live in yw
+    unsigned* flags = reinterpret_cast<unsigned*>(yw);
+    int* e = err ? err : reinterpret_cast<int*>(flags + nblk);
+    // (nblk + 1) words always fit in yw's n doubles; round to 16 bytes when
+    // that still fits (a 16-byte multiple is the fast memset path)
+    const size_t bytes = ((size_t)nblk + 1) * 4;
+    const size_t rounded = (bytes + 15) / 16 * 16;
+    HIP_TRY(hipMemsetAsync(flags, 0, rounded <= (size_t)n * sizeof(double) ? rounded : bytes, s));
+    hipLaunchKernelGGL(backsub_persist_kernel<T>, dim3((unsigned)nblk), dim3(256), 0, s, U, ldu, y, incy,
+                       perm, x, bnorm, (int)n, unit, flags, e);
+    HIP_TRY(hipGetLastError());
+    return GELIM_OK;
+  }
+  hipLaunchKernelGGL(copy_y_kernel<T>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, U, ldu, y, incy,
+                     perm, yw, bnorm, (int)n, unit);
   HIP_TRY(hipGetLastError());
-  // last diagonal block, then one fused launch per block: update the rows
-  // above with its x and solve the next diagonal block
   int64_t i0 = (n - 1) / kBS * kBS;
-  hipLaunchKernelGGL(diag_solve_kernel<T>, dim3(1), dim3(64), 0, s, U, ldu, yw, x, (int)i0,
+  hipLaunchKernelGGL(diag_solve_kernel<T>, dim3(1), dim3(64), 0, s, U, ldu, perm, yw, x, (int)i0,
                      (int)(n - i0), unit);
   HIP_TRY(hipGetLastError());
   for (int64_t i1 = n; i0 > 0; i1 = i0, i0 -= kBS) {
     const int nb = (int)(i1 - i0);
     const int64_t rows = i0 > kBS ? i0 - kBS : 0;  // rows above the next block
     const int blocks = 1 + (int)std::min<int64_t>((rows + 3) / 4, 1024);
-    hipLaunchKernelGGL(backsub_step_kernel<T>, dim3(blocks), dim3(256), 0, s, U, ldu, yw, x,
+    hipLaunchKernelGGL(backsub_step_kernel<T>, dim3(blocks), dim3(256), 0, s, U, ldu, perm, yw, x,
                        (int)i0, nb, unit);
     HIP_TRY(hipGetLastError());
   }
@@ -158,13 +266,15 @@ int backsub_impl(const T* U, int64_t ldu, const T* y, int64_t incy, double* x, d
 }  // namespace
 
 int backsub_f64(const double* U, int64_t ldu, const double* y, int64_t incy, double* x,
-                double* bnorm, int64_t n, int unit, double* yw, hipStream_t s) {
-  return backsub_impl<double>(U, ldu, y, incy, x, bnorm, n, unit, yw, s);
+                double* bnorm, int64_t n, int unit, double* yw, hipStream_t s, const int* perm,
+                int* err) {
+  return backsub_impl<double>(U, ldu, y, incy, x, bnorm, n, unit, yw, s, perm, err);
 }
 
 int backsub_f32(const float* U, int64_t ldu, const float* y, int64_t incy, double* x,
-                double* bnorm, int64_t n, int unit, double* yw, hipStream_t s) {
-  return backsub_impl<float>(U, ldu, y, incy, x, bnorm, n, unit, yw, s);
+                double* bnorm, int64_t n, int unit, double* yw, hipStream_t s, const int* perm,
+                int* err) {
+  return backsub_impl<float>(U, ldu, y, incy, x, bnorm, n, unit, yw, s, perm, err);
 }
 
 }  // namespace gelim
@@ -174,8 +284,8 @@ extern "C" int gelim_gpu_backsub(const double* dU, int64_t ldu, const double* dy
   if (n <= 0) return GELIM_FAIL(GELIM_E_ARG, "backsub: n <= 0");
   hipStream_t s = (hipStream_t)stream;
   double* yw = nullptr;
-  HIP_TRY(hipMallocAsync((void**)&yw, sizeof(double) * n, s));
-  int rc = gelim::backsub_f64(dU, ldu, dy, incy, dx, dbnorm, n, unit, yw, s);
+  HIP_TRY(hipMallocAsync((void**)&yw, sizeof(double) * (n + 2), s));
+  int rc = gelim::backsub_f64(dU, ldu, dy, incy, dx, dbnorm, n, unit, yw, s, nullptr, nullptr);
   HIP_TRY(hipFreeAsync(yw, s));
   return rc;
 }

@@ -30,9 +30,15 @@ int swap_trsm(double* C, int64_t ldc, int64_t ncols, const double* L, int64_t ld
 int gemm_update(double* C, int64_t ldc, const double* L, int64_t ldl, const double* U,
                 int64_t ldu, int64_t M, int64_t N, int64_t K, hipStream_t s);
 int backsub_f64(const double* U, int64_t ldu, const double* y, int64_t incy, double* x,
-                double* bnorm, int64_t n, int unit, double* yw, hipStream_t s);
+                double* bnorm, int64_t n, int unit, double* yw, hipStream_t s,
+                const int* perm = nullptr, int* err = nullptr);
 int backsub_f32(const float* U, int64_t ldu, const float* y, int64_t incy, double* x,
-                double* bnorm, int64_t n, int unit, double* yw, hipStream_t s);
+                double* bnorm, int64_t n, int unit, double* yw, hipStream_t s,
+                const int* perm = nullptr, int* err = nullptr);
+int64_t rlu_max_n();
+size_t rlu_workspace_bytes(int64_t n);
+int rlu_factor(const double* src, int64_t lds, double* work, int64_t ldw, int64_t n, int mode,
+               int* piv, int* info, void* ws, hipStream_t s, unsigned long long* stamps = nullptr);
 template <typename T>
 int pivot_elimination(T* A, int64_t lda, int64_t n, int mode, T* mcol, int* info,
                       hipStream_t s);
@@ -56,6 +62,8 @@ struct gelim_gauss_plan {
   bool lookahead = false;                // GELIM_LOOKAHEAD=1: side-stream wide updates
   bool fused = true;                     // GELIM_SCHEDULE=classic: separate update kernels
   bool narrow = true;                    // GELIM_NARROW=0: next strip updated by the panel WG
+  bool resident = false;                 // resident LU (rlu.hip): the default for n <= 2048
+  void* rws = nullptr;                   // its hand-off workspace
   double* sbuf = nullptr;                // narrow-kernel strip buffer ((n + 16) x 16)
   hipGraphExec_t exec = nullptr;
   const void* k_src = nullptr;
@@ -72,6 +80,17 @@ int enqueue(gelim_gauss_plan* p, const void* src, int64_t src_ld, void* dx, void
             hipStream_t s) {
   using namespace gelim;
   const int64_t n = p->n, lda = p->lda;
+  if (p->algo == GELIM_GPU_BLOCKED && p->resident) {
+    // One persistent launch reads the system straight from src (no copy),
+    // leaves U rows at their physical positions and the pivot row of every
+    // column in piv; the persistent back substitution follows through piv.
+    double* A = static_cast<double*>(p->work);
+    HIP_TRY(hipMemsetAsync(p->info, 0, 16, s));
+    GELIM_TRY(rlu_factor(static_cast<const double*>(src), src_ld, A, lda, n, p->pivot, p->piv, p->info,
+                         p->rws, s));
+    return backsub_f64(A, lda, A + n, lda, static_cast<double*>(dx), static_cast<double*>(bnorm), n, 0,
+                       p->yw, s, p->piv, p->info + 1);
+  }
   if (src)
     HIP_TRY(hipMemcpy2DAsync(p->work, lda * p->eb, src, src_ld * p->eb, (n + 1) * p->eb, n,
                              hipMemcpyDeviceToDevice, s));
@@ -201,6 +220,18 @@ extern "C" gelim_gauss_plan* gelim_gauss_plan_create(int64_t n, int algo, int pi
   if (const char* e = std::getenv("GELIM_SCHEDULE")) p->fused = std::string(e) != "classic";
   if (p->lookahead) p->fused = false;
   if (const char* e = std::getenv("GELIM_NARROW")) p->narrow = std::atoi(e) != 0;
+  {
+    // GELIM_SCHEDULE: auto (default) | resident | fused | classic.  auto =
+    // the resident LU up to n = 1024 (R <= 2 register slots: measured 0.73
+    // vs 0.93 ms at 512, 1.58 vs 2.06 ms at 1024) and the fused step
+    // schedule above (at R = 4 the resident engine's strip update spills and
+    // its scalar-cache broadcasts are latency-bound: 6.1 vs 4.95 ms at 2048,
+    // profiles/rlu_phase_stamps.txt).  resident forces it up to 2048.
+    const char* e = std::getenv("GELIM_SCHEDULE");
+    const std::string sched = e ? e : "auto";
+    const int64_t lim = sched == "resident" ? gelim::rlu_max_n() : sched == "auto" ? 1024 : 0;
+    p->resident = algo == GELIM_GPU_BLOCKED && n <= lim && !p->lookahead;
+  }
   if (algo == GELIM_GPU_BLOCKED) {
     for (int64_t k = 0; k < n;) {
       const int64_t w = std::min<int64_t>(gelim::panel_width_for(n - k), n - k);
@@ -217,6 +248,8 @@ extern "C" gelim_gauss_plan* gelim_gauss_plan_create(int64_t n, int algo, int pi
         if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return fail("event");
     if (hipMalloc((void**)&p->pairs, sizeof(int) * kPairSlot * S) != hipSuccess) return fail("pairs");
     if (hipMalloc((void**)&p->sbuf, sizeof(double) * 16 * (n + 16)) != hipSuccess) return fail("sbuf");
+    if (p->resident && hipMalloc(&p->rws, gelim::rlu_workspace_bytes(n)) != hipSuccess)
+      return fail("resident LU workspace");
   }
   (void)hipMemset(p->work, 0, (size_t)(n * p->lda * dtype_bytes));
   return p;
@@ -232,6 +265,7 @@ extern "C" void gelim_gauss_plan_destroy(gelim_gauss_plan* p) {
       if (e) (void)hipEventDestroy(e);
   (void)hipFree(p->pairs);
   (void)hipFree(p->sbuf);
+  (void)hipFree(p->rws);
   (void)hipFree(p->work);
   (void)hipFree(p->piv);
   (void)hipFree(p->info);
@@ -283,5 +317,8 @@ extern "C" int gelim_gauss_plan_info(gelim_gauss_plan* p, void* stream) {
   int h[4] = {0, 0, 0, 0};
   HIP_TRY(hipMemcpyAsync(h, p->info, 16, hipMemcpyDeviceToHost, (hipStream_t)stream));
   HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
+  if (h[1] != 0)
+    return GELIM_FAIL(GELIM_E_HIP, "GPU hand-off timed out (code " + std::to_string(h[1]) +
+                                       "): workgroups of a persistent kernel were not co-resident");
   return h[0];
 }

@@ -15,7 +15,7 @@ hipGraph.  N GPUs = N ranks (torchrun), each solving its own system per step
 ranks and `value` is that wall time.  Data: synthetic random U[-1,1) matrices
 (b = A (1..n)), generated on device; weights/checkpoints do not apply.
 
-  python bench.py [--gpus N --steps K --warmup W] [--n 2048] [--extras]
+  python bench.py [--gpus N --steps K --warmup W] [--n 2048] [--extras 0|1]
 
 Output: ONE JSON line on rank 0.
 """
@@ -45,8 +45,11 @@ def parse():
     p.add_argument("--backend", default="hip", choices=["hip", "hip-pivot"])
     p.add_argument("--graph", type=int, default=0, help="replay the solve from a hipGraph (1) or launch eagerly (0)")
     p.add_argument("--no-matmul", action="store_true")
-    p.add_argument("--extras", action="store_true",
-                   help="also time the distributed 8192^2 solve and 16384^2 ring matmul (N>1)")
+    p.add_argument("--extras", type=int, default=None,
+                   help="also time the distributed 8192^2 solve and 16384^2 ring matmul "
+                        "(default: on when N > 1; bounded by a watchdog)")
+    p.add_argument("--extras-budget", type=float, default=240.0,
+                   help="seconds the extras may take before the headline line is printed without them")
     p.add_argument("--measure-seq", action="store_true",
                    help="time the reference sequential loops on this host (slow)")
     return p.parse_args()
@@ -114,11 +117,8 @@ def main() -> None:
     elif HOST_SEQ_FILE.exists():
         seq = json.loads(HOST_SEQ_FILE.read_text())
 
-    extras = {}
     solver.close()
-    if args.extras and N > 1:
-        extras = run_extras(comm, gelim, torch)
-
+    out = None
     if rank == 0:
         out = {
             "metric": "wall-clock sec per 2048x2048 Gauss-elim solve (fp64, partial pivoting, "
@@ -151,8 +151,34 @@ def main() -> None:
             if mm and "matmul_2048_s" in seq:
                 mm["speedup_vs_seq_end_to_end"] = seq["matmul_2048_s"] / mm["end_to_end_s"]
                 mm["speedup_vs_seq_kernel"] = seq["matmul_2048_s"] / mm["kernel_s"]
-        if extras:
-            out["extras"] = extras
+
+    # -- distributed configs of BASELINE.json (N > 1), after the headline
+    #    timing; a watchdog prints the headline line without them if the
+    #    collectives do not finish in time, so they can never cost the line
+    want_extras = (N > 1) if args.extras is None else bool(args.extras)
+    if want_extras and N > 1:
+        import threading
+
+        printed = threading.Event()
+
+        def emit(extras: dict) -> None:
+            if rank == 0 and not printed.is_set():
+                printed.set()
+                out["extras"] = extras
+                print(json.dumps(out), flush=True)
+
+        def watchdog() -> None:
+            emit({"error": f"extras did not finish within {args.extras_budget:.0f} s"})
+            sys.stdout.flush()
+            os._exit(0)
+
+        timer = threading.Timer(args.extras_budget, watchdog)
+        timer.daemon = True
+        timer.start()
+        extras = run_extras(comm, gelim, torch)
+        timer.cancel()
+        emit(extras)
+    elif rank == 0:
         print(json.dumps(out), flush=True)
     C.destroy()
 
@@ -180,39 +206,54 @@ def measure_host_seq(n: int) -> dict:
     return res
 
 
-def run_extras(comm, gelim, torch) -> dict:
+def run_extras(comm, gelim, torch, n_gauss: int = 8192, n_mm: int = 16384) -> dict:
     """Distributed configs of BASELINE.json: 8192^2 Gauss (column block-cyclic,
-    RCCL panel broadcast) and 16384^2 fp32 ring matmul (B all-gather
-    overlapped with MFMA compute)."""
+    one RCCL panel broadcast per 64-column block) and 16384^2 fp32 ring matmul
+    (B blocks rotated with isend/irecv, overlapped with the MFMA GEMM).
+    Each is run twice and the second (warm) run is reported; wall time
+    bracketed by barrier + device sync, max over ranks."""
     out = {}
+    dev = comm.device
+
+    def sync():
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+        comm.barrier()
+
+    def tmax(dt: float) -> float:
+        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        comm.all_reduce(t, "max")
+        return t.item()
+
     try:
         from gelim.parallel import DistributedGauss, ring_matmul
 
-        n = 8192
+        n = n_gauss
         dg = DistributedGauss(comm, n, block=64)
-        for it in range(2):
+        for _ in range(2):
             loc = dg.generate_random(seed=99)
-            torch.cuda.synchronize()
-            comm.barrier()
+            sync()
             t0 = time.perf_counter()
             x = dg.solve_(loc)
-            torch.cuda.synchronize()
-            comm.barrier()
-            dt = time.perf_counter() - t0
-        out["dist_gauss_8192"] = {"time_s": dt, "error": gelim.ops.gauss.error_metric(x)}
-        M = K = Nn = 16384
+            sync()
+            dt = tmax(time.perf_counter() - t0)
+        out[f"dist_gauss_{n}"] = {"time_s": dt, "error": gelim.ops.gauss.error_metric(x),
+                                   "gflops_total": (2.0 / 3.0) * n ** 3 / dt * 1e-9,
+                                   "layout": "1-D column block-cyclic, D=64"}
+        del dg, loc, x
+        M = K = Nn = n_mm
         P = comm.world_size
-        Aloc = torch.randn(M // P, K, device=comm.device)
-        Bloc = torch.randn(K // P, Nn, device=comm.device)
-        for it in range(2):
-            torch.cuda.synchronize()
-            comm.barrier()
+        g = torch.Generator().manual_seed(1 + comm.rank)
+        Aloc = torch.randn(M // P, K, generator=g).to(dev)
+        Bloc = torch.randn(K // P, Nn, generator=g).to(dev)
+        for _ in range(2):
+            sync()
             t0 = time.perf_counter()
             ring_matmul(comm, Aloc, Bloc)
-            torch.cuda.synchronize()
-            comm.barrier()
-            dt = time.perf_counter() - t0
-        out["dist_matmul_16384"] = {"time_s": dt, "tflops_total": 2 * M * K * Nn / dt * 1e-12}
+            sync()
+            dt = tmax(time.perf_counter() - t0)
+        out[f"dist_matmul_{n_mm}"] = {"time_s": dt, "tflops_total": 2 * M * K * Nn / dt * 1e-12,
+                                      "algo": "ring (B all-gather overlapped with MFMA)"}
     except Exception as e:  # report, never kill the headline line
         out["error"] = repr(e)
     return out

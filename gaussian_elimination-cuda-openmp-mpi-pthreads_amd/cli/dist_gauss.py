@@ -16,6 +16,11 @@ back substitution, the reference times computeGauss only, MPIe:356-365) and
 Unlike the reference's master/worker scheme (rank 0 ships full rows out and
 back every pivot step), the matrix is resident and
 column block-cyclic: one panel broadcast per block (parallel/dist_gauss.py).
+
+--emulate P runs P ranks as threads of this one process on one device (the
+emulated communicator, parallel/emulated.py) — the distributed algorithm on a
+single GPU.  --checkpoint-dir / --checkpoint-every / --resume save and resume
+the elimination at panel boundaries (utils/checkpoint.py).
 """
 from __future__ import annotations
 
@@ -44,6 +49,11 @@ def parse(argv=None):
     p.add_argument("--warmup", type=int, default=0, help="untimed solves before the timed one")
     p.add_argument("--verify", action="store_true", help="print the max error against the exact solution")
     p.add_argument("--json", action="store_true", help="also print one JSON result line")
+    p.add_argument("--emulate", type=int, default=0, metavar="P",
+                   help="run P emulated ranks (threads) in this process on one device")
+    p.add_argument("--checkpoint-dir", default=None, help="save panel-boundary checkpoints here")
+    p.add_argument("--checkpoint-every", type=int, default=8, help="blocks between checkpoints")
+    p.add_argument("--resume", action="store_true", help="resume from --checkpoint-dir")
     return p.parse_args(argv)
 
 
@@ -69,7 +79,19 @@ def synthetic_local(dg: DistributedGauss) -> torch.Tensor:
 
 def main(argv=None) -> int:
     args = parse(argv)
+    if args.emulate and args.emulate > 1:
+        from ..parallel.emulated import run_emulated
+
+        dev = args.device or ("cuda:0" if torch.cuda.is_available() else "cpu")
+        return max(run_emulated(args.emulate, lambda comm: run(args, comm), device=dev))
     comm = C.init_from_env(device=args.device)
+    try:
+        return run(args, comm)
+    finally:
+        C.destroy()
+
+
+def run(args, comm) -> int:
     dev = comm.device
 
     def sync():
@@ -85,9 +107,10 @@ def main(argv=None) -> int:
             for _ in range(args.warmup):
                 dg.solve_(synthetic_local(dg))
             sync()
+            ck = dg.checkpointer(args.checkpoint_dir, args.checkpoint_every) if args.checkpoint_dir else None
             t0 = time.perf_counter()
             loc = synthetic_local(dg)
-            x = dg.solve_(loc)
+            x = dg.solve_(loc, ckpt=ck, resume=args.resume)
             sync()
             dt = time.perf_counter() - t0
             if comm.rank == 0:
@@ -99,9 +122,9 @@ def main(argv=None) -> int:
                     err = float((x.cpu() - exact).abs().max())
                     print(f"Max error vs exact solution: {err:e}")
                 if args.json:
-                    print(json_line({"program": "dist_gauss_internal", "n": n, "ranks": comm.world_size,
+                    json_line({"program": "dist_gauss_internal", "n": n, "ranks": comm.world_size,
                                      "block": args.block, "time_s": dt, "max_abs_error": err,
-                                     "backend": comm.backend, "device": dev.type}))
+                                     "backend": comm.backend, "device": dev.type})
         else:
             A = load_global(args.file)
             n = A.shape[0]
@@ -110,9 +133,10 @@ def main(argv=None) -> int:
             for _ in range(args.warmup):
                 dg.solve_(dg.scatter_from_global(aug))
             loc = dg.scatter_from_global(aug)
+            ck = dg.checkpointer(args.checkpoint_dir, args.checkpoint_every) if args.checkpoint_dir else None
             sync()
             t0 = time.perf_counter()
-            x = dg.solve_(loc)
+            x = dg.solve_(loc, ckpt=ck, resume=args.resume)
             sync()
             dt = time.perf_counter() - t0
             if comm.rank == 0:
@@ -121,15 +145,13 @@ def main(argv=None) -> int:
                 print(f"Time:  {dt:f} seconds")
                 print(f"Error: {err:e}", flush=True)
                 if args.json:
-                    print(json_line({"program": "dist_gauss_external", "file": args.file, "n": n,
+                    json_line({"program": "dist_gauss_external", "file": args.file, "n": n,
                                      "ranks": comm.world_size, "block": args.block, "time_s": dt,
-                                     "error": err, "backend": comm.backend, "device": dev.type}))
+                                     "error": err, "backend": comm.backend, "device": dev.type})
     except _native.SingularMatrixError:
         if comm.rank == 0:
             print("The matrix is singular", file=sys.stderr)
         rc = 255  # the reference's exit(-1)
-    finally:
-        C.destroy()
     return rc
 
 

@@ -89,9 +89,9 @@ def main(argv=None) -> int:
             if rel is not None:
                 print(f"Max relative error: {rel:e}")
             if args.json:
-                print(json_line({"program": "dist_matmul", "algo": args.algo, "n": n, "ranks": P,
+                json_line({"program": "dist_matmul", "algo": args.algo, "n": n, "ranks": P,
                                  "time_s": dt.item(), "tflops": 2 * n ** 3 / dt.item() * 1e-12,
-                                 "max_rel_err": rel, "backend": comm.backend, "device": dev.type}))
+                                 "max_rel_err": rel, "backend": comm.backend, "device": dev.type})
     finally:
         C.destroy()
     return 0

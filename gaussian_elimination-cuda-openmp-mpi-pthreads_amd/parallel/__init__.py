@@ -1,6 +1,7 @@
 """Multi-GPU layer: communicator (RCCL / gloo), distributed Gauss, distributed
 matmul."""
-from . import comm, dist_gauss, dist_matmul  # noqa: F401
+from . import comm, dist_gauss, dist_matmul, emulated  # noqa: F401
 from .comm import Communicator, destroy, init_from_env  # noqa: F401
 from .dist_gauss import ColumnLayout, DistributedGauss  # noqa: F401
 from .dist_matmul import ring_matmul, summa_matmul  # noqa: F401
+from .emulated import EmulatedComm, make_world, run_emulated  # noqa: F401

@@ -41,6 +41,7 @@ import torch
 
 from .. import _native
 from ..ops import lu
+from ..utils.checkpoint import Checkpointer, maybe_inject_fault
 from ..utils.tensors import padded_ld, ptr, stream_handle
 from .comm import Communicator
 
@@ -164,11 +165,33 @@ class DistributedGauss:
                                    panel[so:so + ws, so + ws:])
         return piv
 
-    def factor_(self, loc: torch.Tensor) -> None:
-        """Forward elimination of the distributed augmented system in place."""
+    def checkpointer(self, directory, every: int = 1) -> Checkpointer:
+        """Panel-boundary checkpoints of this solve (utils/checkpoint.py)."""
+        L = self.layout
+        return Checkpointer(directory, self.comm, {"n": self.n, "D": L.D, "pivot": self.pivot,
+                                                   "ld": self.ld}, every)
+
+    def factor_(self, loc: torch.Tensor, ckpt: Checkpointer | None = None, resume: bool = False,
+                fault_at_block: int | None = None) -> None:
+        """Forward elimination of the distributed augmented system in place.
+
+        ckpt: save the state every ckpt.every blocks; resume: continue from
+        its last complete generation (loc is overwritten with the saved slab).
+        fault_at_block / GELIM_FAULT_AT_BLOCK: raise InjectedFault on entering
+        that block (fault injection for the resume tests)."""
         L, n, r = self.layout, self.n, self.comm.rank
         self._info.zero_()
-        for g in range(L.nblocks):
+        g0 = 0
+        if ckpt is not None and resume:
+            st = ckpt.load()
+            if st is not None:
+                loc.copy_(st.loc.to(loc.device))
+                self._info.copy_(st.info.to(self._info.device))
+                g0 = st.block
+        for g in range(g0, L.nblocks):
+            maybe_inject_fault(g, r, fault_at_block)
+            if ckpt is not None and g > g0 and ckpt.due(g):
+                ckpt.save(g, loc, self._info)
             k, wg, o = g * L.D, L.width(g), L.owner(g)
             m = n - k
             buf = self._buf[:(m + 1) * wg].view(m + 1, wg)
@@ -231,9 +254,10 @@ class DistributedGauss:
                 lu.gemm_update(acc[:s0], loc[:s0, c:c + w], xp)
         return x
 
-    def solve_(self, loc: torch.Tensor) -> torch.Tensor:
+    def solve_(self, loc: torch.Tensor, ckpt: Checkpointer | None = None, resume: bool = False,
+               fault_at_block: int | None = None) -> torch.Tensor:
         """Factor + back-substitute (destroys loc); raises on a zero pivot."""
-        self.factor_(loc)
+        self.factor_(loc, ckpt, resume, fault_at_block)
         if self.info() != 0:
             raise _native.SingularMatrixError(_native.E_SINGULAR, "The matrix is singular")
         return self.backsolve(loc)

@@ -56,18 +56,22 @@ def ring_matmul(comm: Communicator, A_loc: torch.Tensor, B_loc: torch.Tensor, ke
         raise ValueError("ring_matmul needs K divisible by the world size")
     C = torch.empty((A_loc.shape[0], N), dtype=torch.float32, device=A_loc.device)
     cur = B_loc.contiguous()
-    nxt = torch.empty_like(cur) if P > 1 else None
+    # receive buffers: the caller's B_loc is only ever read (it may be a view
+    # of a larger tensor), so the ring rotates through two scratch blocks
+    bufs = [torch.empty_like(cur) for _ in range(min(2, P - 1))]
     for t in range(P):
         src = (r - t) % P  # whose B block we hold now
         reqs = []
+        nxt = bufs[t % 2] if t < P - 1 else None
         if t < P - 1:
             reqs = [comm.send(cur, (r + 1) % P), comm.recv(nxt, (r - 1) % P)]
         matmul_acc_(C, A_loc[:, src * kb:(src + 1) * kb], cur, accumulate=t > 0, kernel=kernel)
         for q in reqs:
             q.wait()
         if t < P - 1:
-            # the send of `cur` must have completed before it is reused
-            cur, nxt = nxt, cur
+            # the send of `cur` has completed (waited) before its buffer is
+            # received into again two steps later
+            cur = nxt
     return C
 
 

@@ -1,2 +1,2 @@
 """Utilities: tensor plumbing, timers, IO, result reporting."""
-from . import io, report, tensors, timing  # noqa: F401
+from . import checkpoint, io, report, tensors, timing  # noqa: F401

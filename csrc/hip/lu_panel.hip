@@ -108,7 +108,8 @@ struct Panel {
   static __device__ __forceinline__ void step(double (&a)[R][W], bool (&live)[R],
                                               PanelLds<W>& sh, int t, int lane, int wave,
                                               bool active, int w, int row0,
-                                              int* __restrict__ info, StepStamps& ss) {
+                                              int* __restrict__ info, StepStamps& ss,
+                                              double* __restrict__ Lout, int ldL) {
     if (J >= w) return;  // uniform across the workgroup
     constexpr int par = J & 1;
     stamp<J>(ss, 0);
@@ -268,14 +269,24 @@ struct Panel {
         ss.v[5] = stamp_now();
       }
     }
+    // 5. column J is final for every row now (multipliers of the live rows,
+    //    U entries of the retired ones): store it column-major in physical
+    //    row order while the next columns are factored — coalesced, and off
+    //    the critical path.  Rows >= m land in the buffer's padding
+    //    (ldL >= NT * R); the <= 2w moved rows are fixed up at the end.
+    if (Lout != nullptr) {
+#pragma unroll
+      for (int i = 0; i < R; ++i) Lout[(int64_t)J * ldL + t + i * NT] = a[i][J];
+    }
   }
 
   template <int... J>
   static __device__ __forceinline__ void steps(double (&a)[R][W], bool (&live)[R],
                                                PanelLds<W>& sh, int t, int lane, int wave,
                                                bool active, int w, int row0, int* info,
-                                               StepStamps& ss, std::integer_sequence<int, J...>) {
-    (step<J>(a, live, sh, t, lane, wave, active, w, row0, info, ss), ...);
+                                               StepStamps& ss, double* Lout, int ldL,
+                                               std::integer_sequence<int, J...>) {
+    (step<J>(a, live, sh, t, lane, wave, active, w, row0, info, ss, Lout, ldL), ...);
   }
 
   // LDS staging tile: NT rows x W doubles in 16-byte chunks, XOR-swizzled by
@@ -396,6 +407,22 @@ struct Panel {
     }
   }
 
+  // Column-major source (the narrow kernel's strip buffer): every load of the
+  // panel in flight at once, column 0 first — coalesced 8-byte loads (lanes =
+  // consecutive rows), no LDS transpose, and the compiler's per-register
+  // vmcnt waits let column 0's pivot search start before the later columns
+  // have arrived.
+  static __device__ __forceinline__ void load_colmajor(double (&a)[R][W], const double* __restrict__ Pin,
+                                                       int64_t ld, int m, int w, int t) {
+#pragma unroll
+    for (int c = 0; c < W; ++c)
+#pragma unroll
+      for (int i = 0; i < R; ++i) {
+        const double v = Pin[(int64_t)c * ld + min(t + i * NT, m - 1)];
+        a[i][c] = c < w ? v : 0.0;
+      }
+  }
+
   static __device__ __forceinline__ void store_direct(const double (&a)[R][W], const int (&dest)[R],
                                                       double* __restrict__ P, int64_t ldp, int m,
                                                       int t) {
@@ -418,8 +445,11 @@ __device__ __forceinline__ void panel_body(double* __restrict__ P, int64_t ldp, 
                                            unsigned long long* __restrict__ stamps,
                                            int* __restrict__ pairs, PanelLds<W>& sh,
                                            int io = 0, const double* Pin = nullptr,
-                                           int64_t ldin = 0) {
-  // the panel is read from Pin (default: P itself) and written to P
+                                           int64_t ldin = 0, double* __restrict__ Lout = nullptr,
+                                           int ldL = 0, bool pin_colmajor = false) {
+  // the panel is read from Pin (default: P itself) and written to P; with
+  // Lout, the factored panel goes column-major (ld ldL, final row order) to
+  // Lout and only the U11 rows to P (the fused step schedule)
   if (Pin == nullptr) {
     Pin = P;
     ldin = ldp;
@@ -436,7 +466,9 @@ __device__ __forceinline__ void panel_body(double* __restrict__ P, int64_t ldp, 
   // global loads are coalesced (W/2 lanes per row segment)
   const bool staged = (w == W) && (W % 2 == 0) && ((((uintptr_t)P) & 15) == 0) && (ldp % 2 == 0) &&
                       ((((uintptr_t)Pin) & 15) == 0) && (ldin % 2 == 0);
-  if (staged && io == 1) {
+  if (pin_colmajor) {
+    K::load_colmajor(a, Pin, ldin, m, w, t);
+  } else if (staged && io == 1) {
     K::load_direct(a, Pin, ldin, m, t);
   } else if (staged && io == 2) {
     K::stage_in_all(a, Pin, ldin, m, t);
@@ -465,7 +497,8 @@ __device__ __forceinline__ void panel_body(double* __restrict__ P, int64_t ldp, 
   }
 
   StepStamps ss{};
-  K::steps(a, live, sh, t, lane, wave, active, w, row0, info, ss, std::make_integer_sequence<int, W>{});
+  K::steps(a, live, sh, t, lane, wave, active, w, row0, info, ss, Lout, ldL,
+           std::make_integer_sequence<int, W>{});
   unsigned long long t2 = 0;
   if constexpr (STAMP) t2 = stamp_now();
 
@@ -517,7 +550,12 @@ __device__ __forceinline__ void panel_body(double* __restrict__ P, int64_t ldp, 
       if (lane == 0) pairs[0] = __popcll(mask);
     }
   }
+  // early column stores complete before any fix-up store to the same rows
+  if (Lout != nullptr) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  unsigned long long ta = 0, tb = 0, tc = 0;
+  if constexpr (STAMP) ta = stamp_now();
   __syncthreads();
+  if constexpr (STAMP) tb = stamp_now();
 
   // final position of every physical row
   int dest[R];
@@ -538,7 +576,26 @@ __device__ __forceinline__ void panel_body(double* __restrict__ P, int64_t ldp, 
     }
     dest[i] = d;
   }
-  if (staged && io == 1) {
+  if constexpr (STAMP) tc = stamp_now();
+  if (Lout != nullptr) {
+    // rows that moved overwrite their final position's early store; the
+    // rows landing in the top w (U11) also go to P for the back substitution
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      const int lr = t + i * NT;
+      if (lr < m && dest[i] != lr) {
+#pragma unroll
+        for (int c = 0; c < W; ++c)
+          if (c < w) Lout[(int64_t)c * ldL + dest[i]] = a[i][c];
+      }
+      if (lr < m && dest[i] < w) {
+        double* dst = P + (int64_t)dest[i] * ldp;
+#pragma unroll
+        for (int c = 0; c < W; ++c)
+          if (c < w) dst[c] = a[i][c];
+      }
+    }
+  } else if (staged && io == 1) {
     K::store_direct(a, dest, P, ldp, m, t);
   } else if (staged) {
     K::stage_out(a, dest, P, ldp, m, t);
@@ -562,6 +619,9 @@ __device__ __forceinline__ void panel_body(double* __restrict__ P, int64_t ldp, 
       stamps[1] = t1;
       stamps[2] = t2;
       stamps[3] = stamp_now();
+      stamps[4] = ta;
+      stamps[5] = tb;
+      stamps[6] = tc;
       for (int k = 0; k < 6; ++k) stamps[8 + k] = ss.v[k];
     }
   }
@@ -603,10 +663,13 @@ struct StepArgs {
   int wide_c0;             // first column of the wide strips
   unsigned long long* stamps;  // diagnostics (STAMP builds): realtime per phase
   int io;                      // panel IO: 0 LDS-staged, 1 direct
-  const double* buf;           // narrow-kernel output (rows rel kp, ld kBufLd) or null
+  const double* buf;           // narrow-kernel output (rows rel kp, column-major, ld ldL) or null
+  double* lout;                // this step's factored panel, column-major (ld ldL)
+  const double* lprev;         // the previous step's, same layout
+  int ldL;                     // >= NT * R of every step (padding rows absorb the
+                               // unconditional early stores)
 };
 
-constexpr int kBufLd = 16;  // row stride of the narrow strip buffer (doubles)
 
 // Panel IO of the fused step: 2 (default) every coalesced load in flight at
 // once + LDS transpose, LDS-staged coalesced stores; 1 direct 16-byte
@@ -634,7 +697,8 @@ struct alignas(16) StripLds {
 };
 
 // Apply a finished panel (rows [0, m) relative to its top, width wp, net row
-// movement `pairs`) to an ncols <= 16 column strip C: swap, U12 = L11^-1 A12,
+// movement `pairs`; L column-major with leading dimension ldl, final row
+// order) to an ncols <= 16 column strip C: swap, U12 = L11^-1 A12,
 // A22 -= L21 U12 on the fp64 matrix cores.  Whole workgroup (NT = 512).
 // One forward-substitution step of the DPP-row TRSM (see strip_update).
 template <int I>
@@ -673,7 +737,7 @@ __device__ __forceinline__ void strip_update(double* __restrict__ C, int64_t ldc
   if (t < kStripMaxW * kStripMaxW) {
     const int r = t / kStripMaxW, q = t % kStripMaxW;
     const int rc = min(r, wp - 1), qc = min(q, wp - 1);
-    sh.l11[r][q] = dev::load_sel(L + (int64_t)rc * ldl + qc, q < r && r < wp);
+    sh.l11[r][q] = dev::load_sel(L + (int64_t)qc * ldl + rc, q < r && r < wp);
   }
   const double top = dev::load_sel(C + (int64_t)min(e, wp - 1) * ldc + cc, e < wp && colok);
   __syncthreads();
@@ -732,17 +796,10 @@ __device__ __forceinline__ void strip_update(double* __restrict__ C, int64_t ldc
       const int lrow = rbase + r16;
       // clamped rows / columns: unconditional loads, selects afterwards
       const bool okb = blk < nblk && lrow < m;
-      const double* lp = L + (int64_t)min(lrow, m - 1) * ldl;
-      if (wp == kStripMaxW) {  // uniform: full panel, two 16-byte loads
-        const double2 v0 = reinterpret_cast<const double2*>(lp + 4 * q)[0];
-        const double2 v1 = reinterpret_cast<const double2*>(lp + 4 * q)[1];
-        la[s][0] = okb ? v0.x : 0.0; la[s][1] = okb ? v0.y : 0.0;
-        la[s][2] = okb ? v1.x : 0.0; la[s][3] = okb ? v1.y : 0.0;
-      } else {  // partial last panel: stay inside the row
+      const double* lp = L + min(lrow, m - 1);  // column-major: lanes r16 coalesce
 #pragma unroll
-        for (int e = 0; e < 4; ++e)
-          la[s][e] = dev::load_sel(lp + min(4 * q + e, wp - 1), okb && 4 * q + e < wp);
-      }
+      for (int e = 0; e < 4; ++e)
+        la[s][e] = dev::load_sel(lp + (int64_t)min(4 * q + e, wp - 1) * ldl, okb && 4 * q + e < wp);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int row = rbase + q + 4 * r;
@@ -788,12 +845,12 @@ __global__ __launch_bounds__(NT) void step_kernel(StepArgs g) {
     {
       const int r = threadIdx.x >> 4, c = threadIdx.x & 15;
       if (r < g.wp && c < g.w)
-        g.A[(int64_t)(g.kp + r) * lda + g.k + c] = g.buf[r * kBufLd + c];
+        g.A[(int64_t)(g.kp + r) * lda + g.k + c] = g.buf[(int64_t)c * g.ldL + r];
     }
     if constexpr (STAMP) t1 = realtime_now();
     panel_body<NT, R, W, MODE, STAMP>(g.A + (int64_t)g.k * lda + g.k, lda, g.n - g.k, g.w, g.k,
                                       g.piv + g.k, g.info, STAMP ? g.stamps + 700 : nullptr,
-                                      g.pairs, sh, g.io, g.buf + (int64_t)g.wp * kBufLd, kBufLd);
+                                      g.pairs, sh, g.io, g.buf + g.wp, g.ldL, g.lout, g.ldL, true);
     if constexpr (STAMP) {
       __syncthreads();
       if (threadIdx.x == 0) {
@@ -806,14 +863,14 @@ __global__ __launch_bounds__(NT) void step_kernel(StepArgs g) {
   }
   if (has_panel && blockIdx.x == 0) {
     if (g.wp > 0) {
-      strip_update<NT, STAMP>(g.A + (int64_t)g.kp * lda + g.k, lda, g.w,
-                              g.A + (int64_t)g.kp * lda + g.kp, lda, g.wp, g.n - g.kp, g.pairs_prev,
-                              ss, sts);
+      strip_update<NT, STAMP>(g.A + (int64_t)g.kp * lda + g.k, lda, g.w, g.lprev, g.ldL, g.wp,
+                              g.n - g.kp, g.pairs_prev, ss, sts);
       __syncthreads();  // strip writes visible to the panel's loads (same CU)
     }
     if constexpr (STAMP) t1 = realtime_now();
     panel_body<NT, R, W, MODE, false>(g.A + (int64_t)g.k * lda + g.k, lda, g.n - g.k, g.w, g.k,
-                                      g.piv + g.k, g.info, nullptr, g.pairs, sh, g.io);
+                                      g.piv + g.k, g.info, nullptr, g.pairs, sh, g.io, nullptr, 0,
+                                      g.lout, g.ldL);
     if constexpr (STAMP) {
       __syncthreads();
       if (threadIdx.x == 0) {
@@ -829,8 +886,8 @@ __global__ __launch_bounds__(NT) void step_kernel(StepArgs g) {
   const int c0 = g.wide_c0 + kStripCols * wb;
   const int ncols = min(kStripCols, g.n + 1 - c0);
   if (ncols <= 0) return;
-  strip_update<NT>(g.A + (int64_t)g.kp * lda + c0, lda, ncols, g.A + (int64_t)g.kp * lda + g.kp,
-                   lda, g.wp, g.n - g.kp, g.pairs_prev, ss);
+  strip_update<NT>(g.A + (int64_t)g.kp * lda + c0, lda, ncols, g.lprev, g.ldL, g.wp, g.n - g.kp,
+                   g.pairs_prev, ss);
   if constexpr (STAMP) {
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -852,12 +909,13 @@ struct NarrowArgs {
   const double* C;  // strip: A + kp*lda + k (rows relative to kp)
   int64_t ldc;
   int ncols;        // strip width (next panel's w)
-  const double* L;  // A + kp*lda + kp
+  const double* L;  // step-j panel, column-major (ld ldl)
   int64_t ldl;
   int wp;           // step-j panel width
   int m;            // n - kp
   const int* pairs; // step-j row movement
-  double* out;      // buffer, ld kBufLd
+  double* out;      // buffer, column-major (rows relative to kp), ld ldo
+  int64_t ldo;
 };
 
 __global__ __launch_bounds__(256) void narrow_kernel(NarrowArgs g) {
@@ -875,7 +933,7 @@ __global__ __launch_bounds__(256) void narrow_kernel(NarrowArgs g) {
       const int np = g.pairs[0];
       pr[t] = dev::load_sel(g.pairs + t, t == 0 || t <= 2 * np);
     }
-    l11[rr][cc] = dev::load_sel(g.L + (int64_t)min(rr, wp - 1) * g.ldl + min(cc, wp - 1),
+    l11[rr][cc] = dev::load_sel(g.L + (int64_t)min(cc, wp - 1) * g.ldl + min(rr, wp - 1),
                                 cc < rr && rr < wp);
     x[rr][cc] = dev::load_sel(g.C + (int64_t)min(rr, wp - 1) * g.ldc + min(cc, ncols - 1),
                               rr < wp && cc < ncols);
@@ -902,7 +960,7 @@ __global__ __launch_bounds__(256) void narrow_kernel(NarrowArgs g) {
     for (int i = 0; i < kStripMaxW; ++i) lrow[i] = l11[j][i];
     trsm_dpp_steps(xv, lrow, j, std::make_integer_sequence<int, kStripMaxW>{});
     x[j][cc] = xv;
-    if (r0 == 0 && j < wp) g.out[j * kBufLd + cc] = xv;
+    if (r0 == 0 && j < wp) g.out[(int64_t)cc * g.ldo + j] = xv;
   }
   __syncthreads();
   // rows [max(r0, wp), r1): out[r] = A[src(r)] - L[r] U12 (MFMA, K permuted)
@@ -922,17 +980,10 @@ __global__ __launch_bounds__(256) void narrow_kernel(NarrowArgs g) {
     const int rbase = a0 + 16 * blk;
     const int lrow = rbase + r16;
     const bool okb = blk < nblk && lrow < r1;
-    const double* lp = g.L + (int64_t)min(lrow, r1 - 1) * g.ldl;
-    if (wp == kStripMaxW) {  // uniform: full panel, two 16-byte loads
-      const double2 v0 = reinterpret_cast<const double2*>(lp + 4 * q)[0];
-      const double2 v1 = reinterpret_cast<const double2*>(lp + 4 * q)[1];
-      la[s][0] = okb ? v0.x : 0.0; la[s][1] = okb ? v0.y : 0.0;
-      la[s][2] = okb ? v1.x : 0.0; la[s][3] = okb ? v1.y : 0.0;
-    } else {
+    const double* lp = g.L + min(lrow, r1 - 1);  // column-major L
 #pragma unroll
-      for (int e = 0; e < 4; ++e)
-        la[s][e] = dev::load_sel(lp + min(4 * q + e, wp - 1), okb && 4 * q + e < wp);
-    }
+    for (int e = 0; e < 4; ++e)
+      la[s][e] = dev::load_sel(lp + (int64_t)min(4 * q + e, wp - 1) * g.ldl, okb && 4 * q + e < wp);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int row = rbase + q + 4 * r;
@@ -955,7 +1006,7 @@ __global__ __launch_bounds__(256) void narrow_kernel(NarrowArgs g) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int row = rbase + q + 4 * r;
-      if (blk < nblk && row < r1) g.out[(int64_t)row * kBufLd + r16] = acc[s][r];
+      if (blk < nblk && row < r1) g.out[(int64_t)r16 * g.ldo + row] = acc[s][r];
     }
   }
 }
@@ -1014,13 +1065,25 @@ int panel_factor(double* P, int64_t ldp, int64_t m, int64_t w, int64_t row0, int
 // One fused step of the blocked LU (see step_kernel).  (kp, wp): previous
 // panel (wp = 0 for the first step); (k, w): this step's panel (w = 0 for the
 // closing step that only finishes the previous update).
+// Rows of the column-major panel buffers (lout / lprev of lu_step): >= NT * R
+// of the first (largest) step, so every early column store lands in bounds.
+int64_t lu_panel_buffer_ld(int64_t n) {
+  int64_t r = 512;
+  while (r < n) r *= 2;
+  return r;
+}
+
 int lu_step(double* A, int64_t lda, int64_t n, int64_t kp, int64_t wp, const int* pairs_prev,
             int64_t k, int64_t w, int mode, int* piv, int* info, int* pairs, hipStream_t s,
-            const double* buf) {
+            const double* buf, double* lout, const double* lprev, int64_t ldL) {
   if (wp > kStripMaxW || w > 16) return GELIM_FAIL(GELIM_E_ARG, "lu_step: panel wider than 16");
+  if (ldL < lu_panel_buffer_ld(n) || (w > 0 && !lout) || (wp > 0 && !lprev))
+    return GELIM_FAIL(GELIM_E_ARG, "lu_step: panel buffers missing or too small");
   StepArgs a{A, lda, (int)n, (int)kp, (int)wp, pairs_prev, (int)k, (int)w, piv, info, pairs, 0,
-             nullptr, panel_io_mode(), (w > 0 && wp > 0) ? buf : nullptr};
-  const int64_t c0 = (w > 0) ? k + w : n;
+             nullptr, panel_io_mode(), (w > 0 && wp > 0) ? buf : nullptr, lout, lprev, (int)ldL};
+  // w = 0: closing launch, step (kp, wp) applied to every column from k on
+  // (k = n: just b; the hybrid schedule closes at its split column)
+  const int64_t c0 = (w > 0) ? k + w : k;
   a.wide_c0 = (int)c0;
   const int64_t nwide = (wp > 0) ? (n + 1 - c0 + kStripCols - 1) / kStripCols : 0;
   const unsigned blocks = (unsigned)(nwide + (w > 0 ? 1 : 0));
@@ -1037,12 +1100,13 @@ int lu_step(double* A, int64_t lda, int64_t n, int64_t kp, int64_t wp, const int
 }
 
 // Step (kp, wp) applied to the next panel's strip [k, k + w) into buf
-// (rows relative to kp, ld 16).  buf must hold (n - kp) x 16 doubles.
+// (rows relative to kp, column-major, ld ldL: 16 x ldL doubles); L is step
+// kp's factored panel (column-major, ld ldL) from lu_step.
 int lu_narrow(double* A, int64_t lda, int64_t n, int64_t kp, int64_t wp, const int* pairs,
-              int64_t k, int64_t w, double* buf, hipStream_t s) {
+              int64_t k, int64_t w, double* buf, hipStream_t s, const double* L, int64_t ldL) {
   if (wp > kStripMaxW || w > kStripCols) return GELIM_FAIL(GELIM_E_ARG, "lu_narrow: width > 16");
   const int64_t m = n - kp;
-  NarrowArgs a{A + kp * lda + k, lda, (int)w, A + kp * lda + kp, lda, (int)wp, (int)m, pairs, buf};
+  NarrowArgs a{A + kp * lda + k, lda, (int)w, L, ldL, (int)wp, (int)m, pairs, buf, ldL};
   hipLaunchKernelGGL(narrow_kernel, dim3((unsigned)((m + kNarrowRows - 1) / kNarrowRows)), dim3(256), 0,
                      s, a);
   HIP_TRY(hipGetLastError());
@@ -1143,18 +1207,23 @@ extern "C" int gelim_debug_step_stamps(int64_t n, int64_t j, double* out) {
       h[r * lda + c] = (double)(((r * 7919 + c * 104729) * 2654435761ull) % 2000) / 1000.0 - 1.0;
   HIP_TRY(hipMemcpy(A, h.data(), h.size() * 8, hipMemcpyHostToDevice));
   double* sbuf = nullptr;
-  HIP_TRY(hipMalloc((void**)&sbuf, sizeof(double) * 16 * (n + 16)));
+  const int64_t ldL = lu_panel_buffer_ld(n);
+  HIP_TRY(hipMalloc((void**)&sbuf, sizeof(double) * 16 * ldL));
+  double* lbuf = nullptr;
+  HIP_TRY(hipMalloc((void**)&lbuf, sizeof(double) * 2 * 16 * ldL));
+  auto lb = [&](int64_t i) { return lbuf + (i & 1) * 16 * ldL; };
   const char* en = std::getenv("GELIM_NARROW");
   const bool nar = !en || std::atoi(en) != 0;
   for (int64_t i = 0; i < j; ++i) {
     GELIM_TRY(lu_step(A, lda, n, i ? 16 * (i - 1) : 0, i ? 16 : 0, i ? pairs + (i - 1) * 72 : nullptr,
                       16 * i, 16, GELIM_PIVOT_PARTIAL, piv, info, pairs + i * 72, 0,
-                      nar ? sbuf : nullptr));
-    if (nar) GELIM_TRY(lu_narrow(A, lda, n, 16 * i, 16, pairs + i * 72, 16 * (i + 1), 16, sbuf, 0));
+                      nar ? sbuf : nullptr, lb(i), i ? lb(i - 1) : nullptr, ldL));
+    if (nar)
+      GELIM_TRY(lu_narrow(A, lda, n, 16 * i, 16, pairs + i * 72, 16 * (i + 1), 16, sbuf, 0, lb(i), ldL));
   }
   StepArgs a{A, lda, (int)n, (int)(16 * (j - 1)), 16, pairs + (j - 1) * 72, (int)(16 * j), 16,
              piv, info, pairs + j * 72, (int)(16 * j + 16), st, panel_io_mode(),
-             nar ? sbuf : nullptr};
+             nar ? sbuf : nullptr, lb(j), lb(j - 1), (int)ldL};
   const int64_t m = n - 16 * j;
   const unsigned nwide = (unsigned)((n + 1 - (16 * j + 16) + 15) / 16);
   constexpr size_t lds = Panel<512, 4, 16, 1, false>::stage_bytes();
@@ -1182,7 +1251,13 @@ extern "C" int gelim_debug_step_stamps(int64_t n, int64_t j, double* out) {
   out[12] = (double)(hs[701] - hs[700]) / 24.0;
   out[13] = (double)(hs[702] - hs[701]) / 24.0;
   out[14] = (double)(hs[703] - hs[702]) / 24.0;
+  // store phase split: reconstruction+drain, barrier, dest, fix-ups+end
+  out[15] = (double)(hs[704] - hs[702]) / 24.0;
+  out[16] = (double)(hs[705] - hs[704]) / 24.0;
+  out[17] = (double)(hs[706] - hs[705]) / 24.0;
+  out[18] = (double)(hs[703] - hs[706]) / 24.0;
   (void)hipFree(sbuf);
+  (void)hipFree(lbuf);
   (void)hipFree(A);
   (void)hipFree(piv);
   (void)hipFree(info);

@@ -18,11 +18,12 @@ namespace gelim {
 int64_t panel_width_for(int64_t m);
 int panel_factor(double* P, int64_t ldp, int64_t m, int64_t w, int64_t row0, int mode, int* piv,
                  int* info, hipStream_t s, int* pairs);
+int64_t lu_panel_buffer_ld(int64_t n);
 int lu_step(double* A, int64_t lda, int64_t n, int64_t kp, int64_t wp, const int* pairs_prev,
             int64_t k, int64_t w, int mode, int* piv, int* info, int* pairs, hipStream_t s,
-            const double* buf);
+            const double* buf, double* lout, const double* lprev, int64_t ldL);
 int lu_narrow(double* A, int64_t lda, int64_t n, int64_t kp, int64_t wp, const int* pairs,
-              int64_t k, int64_t w, double* buf, hipStream_t s);
+              int64_t k, int64_t w, double* buf, hipStream_t s, const double* L, int64_t ldL);
 int pairs_trsm(double* C, int64_t ldc, int64_t ncols, const double* L, int64_t ldl, int64_t w,
                const int* pairs, hipStream_t s);
 int swap_trsm(double* C, int64_t ldc, int64_t ncols, const double* L, int64_t ldl, int64_t w,
@@ -62,9 +63,13 @@ struct gelim_gauss_plan {
   bool lookahead = false;                // GELIM_LOOKAHEAD=1: side-stream wide updates
   bool fused = true;                     // GELIM_SCHEDULE=classic: separate update kernels
   bool narrow = true;                    // GELIM_NARROW=0: next strip updated by the panel WG
-  bool resident = false;                 // resident LU (rlu.hip): the default for n <= 2048
+  bool resident = false;                 // resident LU (rlu.hip): the default for n <= 1024
+  int64_t split = 0;                     // hybrid: fused steps for columns < split, then the
+                                         // resident LU on the trailing (n - split) system
   void* rws = nullptr;                   // its hand-off workspace
-  double* sbuf = nullptr;                // narrow-kernel strip buffer ((n + 16) x 16)
+  double* sbuf = nullptr;                // narrow-kernel strip buffer (16 x ldL, column-major)
+  double* lbuf = nullptr;                // fused steps: factored panels, column-major, ping-pong
+  int64_t ldL = 0;                       //   (2 x 16 x ldL doubles)
   hipGraphExec_t exec = nullptr;
   const void* k_src = nullptr;
   int64_t k_ld = 0;
@@ -75,6 +80,19 @@ struct gelim_gauss_plan {
 namespace {
 
 constexpr int64_t kPairSlot = 72;  // 1 + 4*16 ints, padded
+
+// Hybrid hand-off: perm[i] = i for the fused part (rows already in LAPACK
+// order), split + piv[i] for the resident part (its pivot rows are physical
+// rows of the trailing block); the resident kernel's singular column and
+// hand-off error (info[2], info[3]) are folded into info[0], info[1].
+__global__ void hybrid_perm_kernel(int* __restrict__ perm, int n, int split, int* __restrict__ info) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) perm[i] = i < split ? i : split + perm[i];
+  if (i == 0) {
+    if (info[0] == 0 && info[2] != 0) info[0] = split + info[2];
+    if (info[1] == 0 && info[3] != 0) info[1] = info[3];
+  }
+}
 
 int enqueue(gelim_gauss_plan* p, const void* src, int64_t src_ld, void* dx, void* bnorm,
             hipStream_t s) {
@@ -104,17 +122,41 @@ int enqueue(gelim_gauss_plan* p, const void* src, int64_t src_ld, void* dx, void
     // applies step i to panel i+1's strip, so the panel workgroup starts on
     // an up-to-date strip.
     double* A = static_cast<double*>(p->work);
-    const size_t S = p->step_k.size();
+    const bool hyb = p->split > 0 && p->split < n;
+    // hybrid: only the steps left of the split run here; the closing launch
+    // applies the last of them to every column from the split on (b too)
+    size_t S = p->step_k.size();
+    if (hyb) S = (size_t)(std::lower_bound(p->step_k.begin(), p->step_k.end(), p->split) - p->step_k.begin());
+    const int64_t kend = hyb ? p->split : n;
     const bool nar = p->narrow;
+    // step i writes its factored panel to lbuf[i % 2]; step i + 1's trailing
+    // updates and narrow(i) read it there
+    auto lb = [&](size_t i) { return p->lbuf + (i & 1) * 16 * p->ldL; };
     for (size_t i = 0; i <= S; ++i) {
       const int64_t kp = i ? p->step_k[i - 1] : 0, wp = i ? p->step_w[i - 1] : 0;
-      const int64_t k = i < S ? p->step_k[i] : n, w = i < S ? p->step_w[i] : 0;
+      const int64_t k = i < S ? p->step_k[i] : kend, w = i < S ? p->step_w[i] : 0;
       const int* prev = i ? p->pairs + (i - 1) * kPairSlot : nullptr;
       int* cur = i < S ? p->pairs + i * kPairSlot : nullptr;
       GELIM_TRY(lu_step(A, lda, n, kp, wp, prev, k, w, p->pivot, p->piv, p->info, cur, s,
-                        nar ? p->sbuf : nullptr));
+                        nar ? p->sbuf : nullptr, i < S ? lb(i) : nullptr, i ? lb(i - 1) : nullptr,
+                        p->ldL));
       if (nar && i + 1 < S)
-        GELIM_TRY(lu_narrow(A, lda, n, k, w, cur, p->step_k[i + 1], p->step_w[i + 1], p->sbuf, s));
+        GELIM_TRY(lu_narrow(A, lda, n, k, w, cur, p->step_k[i + 1], p->step_w[i + 1], p->sbuf, s,
+                            lb(i), p->ldL));
+    }
+    if (hyb) {
+      // the trailing (n - split) system, fully updated, factored in place by
+      // the resident LU (one persistent launch; faster than the step
+      // launches once the panel fits 2 register slots); one back
+      // substitution over both parts through the merged row map
+      const int64_t K = p->split;
+      GELIM_TRY(rlu_factor(nullptr, 0, A + K * lda + K, lda, n - K, p->pivot, p->piv + K, p->info + 2,
+                           p->rws, s));
+      hipLaunchKernelGGL(hybrid_perm_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, p->piv,
+                         (int)n, (int)K, p->info);
+      HIP_TRY(hipGetLastError());
+      return backsub_f64(A, lda, A + n, lda, static_cast<double*>(dx), static_cast<double*>(bnorm), n, 0,
+                         p->yw, s, p->piv, p->info + 1);
     }
     return backsub_f64(A, lda, A + n, lda, static_cast<double*>(dx),
                        static_cast<double*>(bnorm), n, 0, p->yw, s);
@@ -231,6 +273,13 @@ extern "C" gelim_gauss_plan* gelim_gauss_plan_create(int64_t n, int algo, int pi
     const std::string sched = e ? e : "auto";
     const int64_t lim = sched == "resident" ? gelim::rlu_max_n() : sched == "auto" ? 1024 : 0;
     p->resident = algo == GELIM_GPU_BLOCKED && n <= lim && !p->lookahead;
+    // GELIM_HYBRID: trailing-system size handed to the resident LU by the
+    // fused schedule (default 1024, the resident LU's 2-slot regime; 0 = off)
+    const char* eh = std::getenv("GELIM_HYBRID");
+    const int64_t tail = eh ? std::atoll(eh) : 1024;
+    if (algo == GELIM_GPU_BLOCKED && !p->resident && p->fused && tail > 0 && n > tail &&
+        tail <= gelim::rlu_max_n() && sched != "fused")
+      p->split = n - tail;  // rounded to a panel boundary below
   }
   if (algo == GELIM_GPU_BLOCKED) {
     for (int64_t k = 0; k < n;) {
@@ -238,6 +287,15 @@ extern "C" gelim_gauss_plan* gelim_gauss_plan_create(int64_t n, int algo, int pi
       p->step_k.push_back(k);
       p->step_w.push_back(w);
       k += w;
+    }
+    if (p->split > 0) {  // first panel start with at most `tail` rows below it
+      const int64_t want = p->split;
+      p->split = n;
+      for (int64_t k : p->step_k)
+        if (k >= want) {
+          p->split = k;
+          break;
+        }
     }
     const size_t S = p->step_k.size();
     if (hipStreamCreateWithFlags(&p->side, hipStreamNonBlocking) != hipSuccess) return fail("side");
@@ -247,9 +305,14 @@ extern "C" gelim_gauss_plan* gelim_gauss_plan_create(int64_t n, int algo, int pi
       for (auto& e : *v)
         if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return fail("event");
     if (hipMalloc((void**)&p->pairs, sizeof(int) * kPairSlot * S) != hipSuccess) return fail("pairs");
-    if (hipMalloc((void**)&p->sbuf, sizeof(double) * 16 * (n + 16)) != hipSuccess) return fail("sbuf");
+    p->ldL = gelim::lu_panel_buffer_ld(n);
+    if (hipMalloc((void**)&p->sbuf, sizeof(double) * 16 * p->ldL) != hipSuccess) return fail("sbuf");
+    if (hipMalloc((void**)&p->lbuf, sizeof(double) * 2 * 16 * p->ldL) != hipSuccess) return fail("lbuf");
     if (p->resident && hipMalloc(&p->rws, gelim::rlu_workspace_bytes(n)) != hipSuccess)
       return fail("resident LU workspace");
+    if (!p->resident && p->split > 0 && p->split < n &&
+        hipMalloc(&p->rws, gelim::rlu_workspace_bytes(n - p->split)) != hipSuccess)
+      return fail("resident LU workspace (hybrid)");
   }
   (void)hipMemset(p->work, 0, (size_t)(n * p->lda * dtype_bytes));
   return p;
@@ -265,6 +328,7 @@ extern "C" void gelim_gauss_plan_destroy(gelim_gauss_plan* p) {
       if (e) (void)hipEventDestroy(e);
   (void)hipFree(p->pairs);
   (void)hipFree(p->sbuf);
+  (void)hipFree(p->lbuf);
   (void)hipFree(p->rws);
   (void)hipFree(p->work);
   (void)hipFree(p->piv);

@@ -18,9 +18,11 @@ for j in (1, 2, 8, 32, 64, 65, 96, 97, 120):
     if 16 * j >= n:
         continue
     for rep in range(2):
-        out = (C.c_double * 16)()
+        out = (C.c_double * 24)()
         gelim._native.check(f(n, j, out))
     print(f"{j:4d} {n - 16 * j:5d} | {out[0] / 100:8.2f} {out[1] / 100:8.2f} {out[2] / 100:8.2f} | "
           f"{out[3] / 100:8.2f} {out[4] / 100:8.2f} {int(out[5])} | prologue phases us: "
           + " ".join(f"{v / 100:6.2f}" for v in out[6:12])
-          + f" | panel load/steps/store us: {out[12] / 100:6.2f} {out[13] / 100:6.2f} {out[14] / 100:6.2f}")
+          + f" | panel load/steps/store us: {out[12] / 100:6.2f} {out[13] / 100:6.2f} {out[14] / 100:6.2f}"
+          + f" | store = recon+drain {out[15] / 100:5.2f} barrier {out[16] / 100:5.2f} dest {out[17] / 100:5.2f}"
+          + f" fixup+end {out[18] / 100:5.2f}")

@@ -119,6 +119,23 @@ __device__ __forceinline__ unsigned wave_min_u32(unsigned v) {
   return (unsigned)__builtin_amdgcn_readlane((int)v, 63);
 }
 
+// Write-through (sc1) stores through a buffer resource.  Bulk results written
+// this way leave no dirty lines in the XCD's L2, so the kernel-end release
+// has nothing to write back: a dependent kernel boundary costs ~1.5 us plus
+// B / 6 TB/s for B dirty bytes (MI355X_MICROARCH.md, "boundary"), i.e. ~5 us
+// behind a trailing update of a 2048^2 fp64 matrix.  The store itself is
+// issued like any other and overlaps the kernel's remaining work.
+typedef unsigned wt_u32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buffer_rsrc(const void* p, uint64_t bytes) {
+  const uint32_t n = bytes > 0xffffffffull ? 0xffffffffu : (uint32_t)bytes;
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)n, 0x00020000);
+}
+__device__ __forceinline__ void store_wt(__amdgpu_buffer_rsrc_t r, uint32_t byte_off, double v) {
+  const uint64_t b = (uint64_t)__double_as_longlong(v);
+  const wt_u32x2 x = {(unsigned)b, (unsigned)(b >> 32)};
+  __builtin_amdgcn_raw_buffer_store_b64(x, r, (int)byte_off, 0, 16 /* sc1 */);
+}
+
 // Masked load without control flow: p must be a valid address (callers
 // clamp their indices), the value is selected afterwards.  Written as
 // `ok ? p[i] : 0`, LLVM turns each masked load into an exec-masked branch

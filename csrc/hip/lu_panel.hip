@@ -729,6 +729,8 @@ __device__ __forceinline__ void strip_update(double* __restrict__ C, int64_t ldc
   const int c = t & (kStripCols - 1);
   const int e = t >> 4;
   const bool colok = c < ncols;
+  // U12 rows and the updated block are stored write-through (dev::store_wt)
+  const __amdgpu_buffer_rsrc_t crs = dev::buffer_rsrc(C, ((uint64_t)(m - 1) * ldc + kStripCols) * 8);
   const int cc = min(c, ncols - 1);  // clamped column: every load below is unconditional
   if (t < 1 + 4 * kStripMaxW) {
     const int np = pairs[0];
@@ -769,7 +771,7 @@ __device__ __forceinline__ void strip_update(double* __restrict__ C, int64_t ldc
     for (int i = 0; i < kStripMaxW; ++i) lrow[i] = sh.l11[j][i];
     trsm_dpp_steps(x, lrow, j, std::make_integer_sequence<int, kStripMaxW>{});
     sh.x[j][cc] = x;
-    if (j < wp && cc < ncols) C[(int64_t)j * ldc + cc] = x;
+    if (j < wp && cc < ncols) dev::store_wt(crs, (uint32_t)(((int64_t)j * ldc + cc) * 8), x);
   }
   __syncthreads();
   mark(3);
@@ -821,7 +823,8 @@ __device__ __forceinline__ void strip_update(double* __restrict__ C, int64_t ldc
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int row = rbase + q + 4 * r;
-        if (blk < nblk && row < m && ccol) C[(int64_t)row * ldc + r16] = acc[s][r];
+        if (blk < nblk && row < m && ccol)
+          dev::store_wt(crs, (uint32_t)(((int64_t)row * ldc + r16) * 8), acc[s][r]);
       }
     }
   }
@@ -925,6 +928,7 @@ __global__ __launch_bounds__(256) void narrow_kernel(NarrowArgs g) {
   __shared__ int srcmap[kNarrowRows];
   const int t = threadIdx.x;
   const int r0 = blockIdx.x * kNarrowRows;
+  const __amdgpu_buffer_rsrc_t ors = dev::buffer_rsrc(g.out, (uint64_t)kStripCols * g.ldo * 8);
   const int r1 = min(r0 + kNarrowRows, g.m);
   const int wp = g.wp, ncols = g.ncols;
   {
@@ -960,7 +964,7 @@ __global__ __launch_bounds__(256) void narrow_kernel(NarrowArgs g) {
     for (int i = 0; i < kStripMaxW; ++i) lrow[i] = l11[j][i];
     trsm_dpp_steps(xv, lrow, j, std::make_integer_sequence<int, kStripMaxW>{});
     x[j][cc] = xv;
-    if (r0 == 0 && j < wp) g.out[(int64_t)cc * g.ldo + j] = xv;
+    if (r0 == 0 && j < wp) dev::store_wt(ors, (uint32_t)(((int64_t)cc * g.ldo + j) * 8), xv);
   }
   __syncthreads();
   // rows [max(r0, wp), r1): out[r] = A[src(r)] - L[r] U12 (MFMA, K permuted)
@@ -1006,7 +1010,7 @@ __global__ __launch_bounds__(256) void narrow_kernel(NarrowArgs g) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int row = rbase + q + 4 * r;
-      if (blk < nblk && row < r1) g.out[(int64_t)r16 * g.ldo + row] = acc[s][r];
+      if (blk < nblk && row < r1) dev::store_wt(ors, (uint32_t)(((int64_t)r16 * g.ldo + row) * 8), acc[s][r]);
     }
   }
 }

@@ -931,6 +931,16 @@ __global__ __launch_bounds__(256) void narrow_kernel(NarrowArgs g) {
   const __amdgpu_buffer_rsrc_t ors = dev::buffer_rsrc(g.out, (uint64_t)kStripCols * g.ldo * 8);
   const int r1 = min(r0 + kNarrowRows, g.m);
   const int wp = g.wp, ncols = g.ncols;
+  const int lane = t & 63, wave = t >> 6;
+  const int r16 = lane & 15, q = lane >> 4;
+  const bool ccol = r16 < ncols;
+  const int a0 = max(r0, wp);
+  const int nblk = (r1 - a0 + 15) >> 4;  // <= 16
+  // Round trip 1 — everything that does not depend on the row movement is in
+  // flight together: pairs, L11, the top rows, this slice's multipliers and
+  // its strip rows at their own positions (unmoved rows: all but <= 2w).
+  dev::d4 acc[4];
+  double la[4][4];
   {
     const int rr = t >> 4, cc = t & 15;
     if (t < 1 + 4 * kStripMaxW) {
@@ -943,41 +953,6 @@ __global__ __launch_bounds__(256) void narrow_kernel(NarrowArgs g) {
                               rr < wp && cc < ncols);
     srcmap[t] = r0 + t;
   }
-  __syncthreads();
-  const int np = pr[0];
-  // post-swap top rows; source rows of this slice's permuted rows
-  for (int idx = t; idx < np * kStripCols; idx += 256) {
-    const int e = idx >> 4, cc = idx & 15;
-    const int d = pr[1 + 2 * e];
-    if (d < wp) x[d][cc] = dev::load_sel(g.C + (int64_t)pr[2 + 2 * e] * g.ldc + min(cc, ncols - 1), cc < ncols);
-  }
-  if (t < np) {
-    const int d = pr[1 + 2 * t];
-    if (d >= r0 && d < r1) srcmap[d - r0] = pr[2 + 2 * t];
-  }
-  __syncthreads();
-  {  // U12 = L11^-1 x: DPP row = one column
-    const int cc = t >> 4, j = t & 15;
-    double xv = x[j][cc];
-    double lrow[kStripMaxW];
-#pragma unroll
-    for (int i = 0; i < kStripMaxW; ++i) lrow[i] = l11[j][i];
-    trsm_dpp_steps(xv, lrow, j, std::make_integer_sequence<int, kStripMaxW>{});
-    x[j][cc] = xv;
-    if (r0 == 0 && j < wp) dev::store_wt(ors, (uint32_t)(((int64_t)cc * g.ldo + j) * 8), xv);
-  }
-  __syncthreads();
-  // rows [max(r0, wp), r1): out[r] = A[src(r)] - L[r] U12 (MFMA, K permuted)
-  const int lane = t & 63, wave = t >> 6;
-  const int r16 = lane & 15, q = lane >> 4;
-  double b[4];
-#pragma unroll
-  for (int kk = 0; kk < 4; ++kk) b[kk] = x[4 * q + kk][r16];
-  const bool ccol = r16 < ncols;
-  const int a0 = max(r0, wp);
-  const int nblk = (r1 - a0 + 15) >> 4;  // <= 16
-  dev::d4 acc[4];
-  double la[4][4];
 #pragma unroll
   for (int s = 0; s < 4; ++s) {
     const int blk = wave + 4 * s;
@@ -992,10 +967,52 @@ __global__ __launch_bounds__(256) void narrow_kernel(NarrowArgs g) {
     for (int r = 0; r < 4; ++r) {
       const int row = rbase + q + 4 * r;
       const int rowc = min(max(row, r0), r1 - 1);
-      acc[s][r] = dev::load_sel(g.C + (int64_t)srcmap[rowc - r0] * g.ldc + min(r16, ncols - 1),
+      acc[s][r] = dev::load_sel(g.C + (int64_t)rowc * g.ldc + min(r16, ncols - 1),
                                 blk < nblk && row < r1 && ccol);
     }
   }
+  __syncthreads();
+  const int np = pr[0];
+  // round trip 2: post-swap top rows; source rows of this slice's permuted rows
+  for (int idx = t; idx < np * kStripCols; idx += 256) {
+    const int e = idx >> 4, cc = idx & 15;
+    const int d = pr[1 + 2 * e];
+    if (d < wp) x[d][cc] = dev::load_sel(g.C + (int64_t)pr[2 + 2 * e] * g.ldc + min(cc, ncols - 1), cc < ncols);
+  }
+  if (t < np) {
+    const int d = pr[1 + 2 * t];
+    if (d >= r0 && d < r1) srcmap[d - r0] = pr[2 + 2 * t];
+  }
+  __syncthreads();
+  // the moved rows of this slice re-read their source (in flight under the TRSM)
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    const int blk = wave + 4 * s;
+    const int rbase = a0 + 16 * blk;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = rbase + q + 4 * r;
+      const int rowc = min(max(row, r0), r1 - 1);
+      const int src = srcmap[rowc - r0];
+      if (src != rowc && blk < nblk && row < r1 && ccol)
+        acc[s][r] = g.C[(int64_t)src * g.ldc + r16];
+    }
+  }
+  {  // U12 = L11^-1 x: DPP row = one column
+    const int cc = t >> 4, j = t & 15;
+    double xv = x[j][cc];
+    double lrow[kStripMaxW];
+#pragma unroll
+    for (int i = 0; i < kStripMaxW; ++i) lrow[i] = l11[j][i];
+    trsm_dpp_steps(xv, lrow, j, std::make_integer_sequence<int, kStripMaxW>{});
+    x[j][cc] = xv;
+    if (r0 == 0 && j < wp) dev::store_wt(ors, (uint32_t)(((int64_t)cc * g.ldo + j) * 8), xv);
+  }
+  __syncthreads();
+  // rows [max(r0, wp), r1): out[r] = A[src(r)] - L[r] U12 (MFMA, K permuted)
+  double b[4];
+#pragma unroll
+  for (int kk = 0; kk < 4; ++kk) b[kk] = x[4 * q + kk][r16];
 #pragma unroll
   for (int s = 0; s < 4; ++s)
 #pragma unroll

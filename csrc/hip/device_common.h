@@ -136,6 +136,16 @@ __device__ __forceinline__ void store_wt(__amdgpu_buffer_rsrc_t r, uint32_t byte
   __builtin_amdgcn_raw_buffer_store_b64(x, r, (int)byte_off, 0, 16 /* sc1 */);
 }
 
+// Plain 8-byte buffer store: the per-thread part of the address is one 32-bit
+// VGPR and the uniform part an SGPR / immediate, so a run of stores to
+// different columns of a column-major buffer costs one instruction each
+// (global stores need a 64-bit address add per store).
+__device__ __forceinline__ void store_buf(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff, double v) {
+  const uint64_t b = (uint64_t)__double_as_longlong(v);
+  const wt_u32x2 x = {(unsigned)b, (unsigned)(b >> 32)};
+  __builtin_amdgcn_raw_buffer_store_b64(x, r, (int)voff, (int)soff, 0);
+}
+
 // Masked load without control flow: p must be a valid address (callers
 // clamp their indices), the value is selected afterwards.  Written as
 // `ok ? p[i] : 0`, LLVM turns each masked load into an exec-masked branch

@@ -105,11 +105,12 @@ struct Panel {
   // hi-word DPP arg-max with one ballot, a publish of only columns >= J, and
   // a lane-parallel DPP merge of the per-wave candidates.
   template <int J>
-  static __device__ __forceinline__ void step(double (&a)[R][W], bool (&live)[R],
+  static __device__ __forceinline__ void step(double (&a)[R][W], bool (&live)[R], int (&retj)[R],
                                               PanelLds<W>& sh, int t, int lane, int wave,
                                               bool active, int w, int row0,
                                               int* __restrict__ info, StepStamps& ss,
-                                              double* __restrict__ Lout, int ldL) {
+                                              double* __restrict__ Lout, int ldL,
+                                              __amdgpu_buffer_rsrc_t lrs) {
     if (J >= w) return;  // uniform across the workgroup
     constexpr int par = J & 1;
     stamp<J>(ss, 0);
@@ -242,7 +243,11 @@ struct Panel {
       if (gkey <= 1 && info && *info == 0) *info = row0 + J + 1;  // zero pivot
     }
 #pragma unroll
-    for (int i = 0; i < R; ++i) live[i] = live[i] && (t + i * NT != (int)p);
+    for (int i = 0; i < R; ++i) {
+      const bool won = t + i * NT == (int)p;
+      retj[i] = won ? J : retj[i];  // the step this row was chosen at (dest, below)
+      live[i] = live[i] && !won;
+    }
     stamp<J>(ss, 4);
 
     // 4. multipliers + rank-1 update of every live row (retired rows: l = 0);
@@ -276,17 +281,19 @@ struct Panel {
     //    (ldL >= NT * R); the <= 2w moved rows are fixed up at the end.
     if (Lout != nullptr) {
 #pragma unroll
-      for (int i = 0; i < R; ++i) Lout[(int64_t)J * ldL + t + i * NT] = a[i][J];
+      for (int i = 0; i < R; ++i)
+        dev::store_buf(lrs, (uint32_t)t * 8u, (uint32_t)(J * ldL + i * NT) * 8u, a[i][J]);
     }
   }
 
   template <int... J>
-  static __device__ __forceinline__ void steps(double (&a)[R][W], bool (&live)[R],
+  static __device__ __forceinline__ void steps(double (&a)[R][W], bool (&live)[R], int (&retj)[R],
                                                PanelLds<W>& sh, int t, int lane, int wave,
                                                bool active, int w, int row0, int* info,
                                                StepStamps& ss, double* Lout, int ldL,
+                                               __amdgpu_buffer_rsrc_t lrs,
                                                std::integer_sequence<int, J...>) {
-    (step<J>(a, live, sh, t, lane, wave, active, w, row0, info, ss, Lout, ldL), ...);
+    (step<J>(a, live, retj, sh, t, lane, wave, active, w, row0, info, ss, Lout, ldL, lrs), ...);
   }
 
   // LDS staging tile: NT rows x W doubles in 16-byte chunks, XOR-swizzled by
@@ -487,8 +494,13 @@ __device__ __forceinline__ void panel_body(double* __restrict__ P, int64_t ldp, 
     }
   }
   bool live[R];
+  int retj[R];
 #pragma unroll
-  for (int i = 0; i < R; ++i) live[i] = t + i * NT < m;
+  for (int i = 0; i < R; ++i) {
+    live[i] = t + i * NT < m;
+    retj[i] = 0;
+  }
+  const __amdgpu_buffer_rsrc_t lrs = dev::buffer_rsrc(Lout, (uint64_t)W * (uint64_t)ldL * 8);
   const bool active = wave * dev::kWave < m;  // the wave holds panel rows
   unsigned long long t1 = 0;
   if constexpr (STAMP) {
@@ -497,7 +509,7 @@ __device__ __forceinline__ void panel_body(double* __restrict__ P, int64_t ldp, 
   }
 
   StepStamps ss{};
-  K::steps(a, live, sh, t, lane, wave, active, w, row0, info, ss, Lout, ldL,
+  K::steps(a, live, retj, sh, t, lane, wave, active, w, row0, info, ss, Lout, ldL, lrs,
            std::make_integer_sequence<int, W>{});
   unsigned long long t2 = 0;
   if constexpr (STAMP) t2 = stamp_now();
@@ -511,18 +523,30 @@ __device__ __forceinline__ void panel_body(double* __restrict__ P, int64_t ldp, 
   // writes are lane selects) — no serial LDS round trips.
   if (wave == 0) {
     const int selv = (lane < w) ? sh.sel[lane] : 0;  // lane j: row chosen at step j
+    // fully unrolled with the chosen rows in SGPRs: per step two v_readlane
+    // (pos of the chosen row, row at position j) and four lane selects; the
+    // LAPACK ipiv (one more dependent readlane) only for the standalone panel
+    int ssel[W];
+#pragma unroll
+    for (int j = 0; j < W; ++j) ssel[j] = __builtin_amdgcn_readlane(selv, j);
+    const bool need_piv = Lout == nullptr;
     int pos = lane, rat = lane, pivv = 0;
-    for (int j = 0; j < w; ++j) {
-      const int p = __builtin_amdgcn_readlane(selv, j);
-      const int idp = p < w ? p : w + j;
-      const int cur = __builtin_amdgcn_readlane(pos, idp);
-      const int other = __builtin_amdgcn_readlane(rat, j);
-      rat = (lane == j) ? idp : rat;  // row_at[j] = idp; row_at[cur] = other
-      rat = (lane == cur) ? other : rat;
-      pos = (lane == idp) ? j : pos;  // pos_of[idp] = j; pos_of[other] = cur
-      pos = (lane == other) ? cur : pos;
-      const int pj = cur < w ? cur : __builtin_amdgcn_readlane(selv, cur < w ? 0 : cur - w);
-      pivv = (lane == j) ? pj : pivv;
+#pragma unroll
+    for (int j = 0; j < W; ++j) {
+      if (j < w) {
+        const int p = ssel[j];
+        const int idp = p < w ? p : w + j;
+        const int cur = __builtin_amdgcn_readlane(pos, idp);
+        const int other = __builtin_amdgcn_readlane(rat, j);
+        rat = (lane == j) ? idp : rat;  // row_at[j] = idp; row_at[cur] = other
+        rat = (lane == cur) ? other : rat;
+        pos = (lane == idp) ? j : pos;  // pos_of[idp] = j; pos_of[other] = cur
+        pos = (lane == other) ? cur : pos;
+        if (need_piv) {
+          const int pj = cur < w ? cur : __builtin_amdgcn_readlane(selv, cur < w ? 0 : cur - w);
+          pivv = (lane == j) ? pj : pivv;
+        }
+      }
     }
     if (lane < w) sh.piv[lane] = pivv;
     if (lane < 2 * w) {
@@ -550,6 +574,8 @@ __device__ __forceinline__ void panel_body(double* __restrict__ P, int64_t ldp, 
       if (lane == 0) pairs[0] = __popcll(mask);
     }
   }
+  unsigned long long tr = 0;
+  if constexpr (STAMP) tr = stamp_now();
   // early column stores complete before any fix-up store to the same rows
   if (Lout != nullptr) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   unsigned long long ta = 0, tb = 0, tc = 0;
@@ -567,8 +593,7 @@ __device__ __forceinline__ void panel_body(double* __restrict__ P, int64_t ldp, 
     if (lr < w) {
       id = lr;
     } else if (lr < m && !live[i]) {
-      for (int j = 0; j < w; ++j)
-        if (sh.sel[j] == lr) id = w + j;
+      id = w + retj[i];
     }
     if (id >= 0) {
       const int cp = sh.pos_of[id];
@@ -580,19 +605,20 @@ __device__ __forceinline__ void panel_body(double* __restrict__ P, int64_t ldp, 
   if (Lout != nullptr) {
     // rows that moved overwrite their final position's early store; the
     // rows landing in the top w (U11) also go to P for the back substitution
+    const __amdgpu_buffer_rsrc_t urs = dev::buffer_rsrc(P, (uint64_t)W * (uint64_t)ldp * 8);
 #pragma unroll
     for (int i = 0; i < R; ++i) {
       const int lr = t + i * NT;
       if (lr < m && dest[i] != lr) {
 #pragma unroll
         for (int c = 0; c < W; ++c)
-          if (c < w) Lout[(int64_t)c * ldL + dest[i]] = a[i][c];
+          if (c < w) dev::store_buf(lrs, (uint32_t)dest[i] * 8u, (uint32_t)(c * ldL) * 8u, a[i][c]);
       }
       if (lr < m && dest[i] < w) {
-        double* dst = P + (int64_t)dest[i] * ldp;
+        const uint32_t ro = (uint32_t)((int64_t)dest[i] * ldp * 8);
 #pragma unroll
         for (int c = 0; c < W; ++c)
-          if (c < w) dst[c] = a[i][c];
+          if (c < w) dev::store_buf(urs, ro, (uint32_t)c * 8u, a[i][c]);
       }
     }
   } else if (staged && io == 1) {
@@ -622,6 +648,7 @@ __device__ __forceinline__ void panel_body(double* __restrict__ P, int64_t ldp, 
       stamps[4] = ta;
       stamps[5] = tb;
       stamps[6] = tc;
+      stamps[7] = tr;
       for (int k = 0; k < 6; ++k) stamps[8 + k] = ss.v[k];
     }
   }
@@ -1277,6 +1304,7 @@ extern "C" int gelim_debug_step_stamps(int64_t n, int64_t j, double* out) {
   out[16] = (double)(hs[705] - hs[704]) / 24.0;
   out[17] = (double)(hs[706] - hs[705]) / 24.0;
   out[18] = (double)(hs[703] - hs[706]) / 24.0;
+  out[19] = (double)(hs[707] - hs[702]) / 24.0;  // reconstruction alone (wave 0)
   (void)hipFree(sbuf);
   (void)hipFree(lbuf);
   (void)hipFree(A);

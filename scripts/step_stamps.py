@@ -25,4 +25,4 @@ for j in (1, 2, 8, 32, 64, 65, 96, 97, 120):
           + " ".join(f"{v / 100:6.2f}" for v in out[6:12])
           + f" | panel load/steps/store us: {out[12] / 100:6.2f} {out[13] / 100:6.2f} {out[14] / 100:6.2f}"
           + f" | store = recon+drain {out[15] / 100:5.2f} barrier {out[16] / 100:5.2f} dest {out[17] / 100:5.2f}"
-          + f" fixup+end {out[18] / 100:5.2f}")
+          + f" fixup+end {out[18] / 100:5.2f} (recon alone {out[19] / 100:5.2f})")

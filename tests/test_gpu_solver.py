@@ -90,3 +90,28 @@ def test_blocked_ops_composition_gpu(gelim, cuda):
     ref = gelim.GaussSolver(n, backend="hip", device=cuda).solve(aug)
     x = gelim.blocked_solve_(aug.clone())
     assert torch.allclose(x, ref, rtol=1e-10, atol=1e-10)
+
+
+@pytest.mark.parametrize("n", [1500, 2048])
+def test_hybrid_matches_pure_fused(gelim, cuda, monkeypatch, n):
+    """The hybrid schedule (fused steps, then the resident LU on the trailing
+    1024 rows) against the pure fused schedule: same pivots up to rounding."""
+    aug = gelim.random_system(n, seed=n + 1, device=cuda)
+    x_h = gelim.GaussSolver(n, backend="hip", device=cuda).solve(aug, check=True)
+    monkeypatch.setenv("GELIM_HYBRID", "0")
+    x_f = gelim.GaussSolver(n, backend="hip", device=cuda).solve(aug, check=True)
+    torch.cuda.synchronize()
+    assert torch.allclose(x_h, x_f, rtol=1e-8, atol=1e-8 * n)
+    assert gelim.ops.gauss.error_metric(x_h) < 1e-7
+
+
+@pytest.mark.parametrize("zero_col", [100, 1500])
+def test_hybrid_singular_column(gelim, cuda, zero_col):
+    """A zero column in the fused part (100) or in the resident tail (1500):
+    info is the 1-based column of the first zero pivot either way."""
+    n = 1600
+    aug = gelim.random_system(n, seed=5, device=cuda)
+    aug[:, zero_col] = 0.0
+    s = gelim.GaussSolver(n, backend="hip", device=cuda)
+    s.solve(aug)
+    assert s.info() == zero_col + 1

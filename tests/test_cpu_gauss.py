@@ -146,3 +146,20 @@ def test_cli_external_usage_and_missing_file(tmp_path):
     assert r.returncode != 0 and "usage:" in r.stderr
     r = run_cli(BIN / "gauss_external_input", "--backend=seq", tmp_path / "nope.dat")
     assert r.returncode != 0 and "The matrix file open error" in r.stderr
+
+
+def test_refinement_cpu_seq(gelim):
+    """Iterative refinement on a CPU backend: fp64 elimination + fp64
+    residual corrections never make the solution worse, and converge."""
+    import torch
+    n = 96
+    aug = gelim.random_system(n, seed=11)
+    s = gelim.GaussSolver(n, backend="seq")
+    x0 = s.solve(aug)
+    x, steps = s.solve_refined(aug, max_steps=3)
+    assert 0 <= steps <= 3
+    e0 = gelim.ops.gauss.error_metric(x0)
+    e1 = gelim.ops.gauss.error_metric(x)
+    assert e1 <= max(e0, 1e-14)
+    ref = torch.linalg.solve(aug[:, :n], aug[:, n])
+    assert torch.allclose(x, ref, rtol=1e-12, atol=1e-12)

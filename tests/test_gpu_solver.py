@@ -115,3 +115,44 @@ def test_hybrid_singular_column(gelim, cuda, zero_col):
     s = gelim.GaussSolver(n, backend="hip", device=cuda)
     s.solve(aug)
     assert s.info() == zero_col + 1
+
+
+@pytest.mark.parametrize("n", [64, 1000, 2048])
+def test_fp32_refined_reaches_fp64_accuracy(gelim, cuda, n):
+    """fp32 per-pivot elimination on MFMA-free HIP kernels + fp64 residual
+    refinement: error lands in the fp64 class, far below plain fp32."""
+    aug = gelim.random_system(n, seed=n + 5, device=cuda)
+    s32 = gelim.GaussSolver(n, backend="hip-pivot", dtype=torch.float32, device=cuda)
+    x32 = s32.solve(aug.float(), check=True)
+    x, steps = s32.solve_refined(aug, max_steps=8, check=True)
+    torch.cuda.synchronize()
+    e32 = gelim.ops.gauss.error_metric(x32)
+    e = gelim.ops.gauss.error_metric(x)
+    assert steps >= 1
+    assert e < 1e-10 and e < e32 / 100, (e32, e, steps)
+
+
+@pytest.mark.parametrize("name", list(GOLDEN_ERROR))
+def test_fp32_refined_golden(gelim, cuda, name):
+    A = gelim.utils.io.load_fixture(name)
+    n = A.shape[0]
+    aug = gelim.augment_with_rhs(A).to(cuda)
+    s = gelim.GaussSolver(n, backend="hip-pivot", dtype=torch.float32, device=cuda)
+    x32 = s.solve(aug.float(), check=True)
+    x, steps = s.solve_refined(aug, max_steps=10, check=True)
+    err = gelim.ops.gauss.error_metric(x)
+    e32 = gelim.ops.gauss.error_metric(x32)
+    # refinement never makes it worse; the well-conditioned matrices reach
+    # the fp64 golden class from an fp32 factorisation
+    assert err <= e32 * (1 + 1e-6), (name, err, e32)
+    if name in ("matrix_10", "jpwh_991"):
+        assert err <= max(20 * GOLDEN_ERROR[name], 1e-13), (name, err, steps)
+
+
+def test_fp64_refined_hip(gelim, cuda):
+    n = 1500
+    aug = gelim.random_system(n, seed=9, device=cuda)
+    s = gelim.GaussSolver(n, backend="hip", device=cuda)
+    x, steps = s.solve_refined(aug, max_steps=2, check=True)
+    assert steps >= 1
+    assert gelim.ops.gauss.error_metric(x) < 1e-10

@@ -273,10 +273,14 @@ extern "C" gelim_gauss_plan* gelim_gauss_plan_create(int64_t n, int algo, int pi
     const std::string sched = e ? e : "auto";
     const int64_t lim = sched == "resident" ? gelim::rlu_max_n() : sched == "auto" ? 1024 : 0;
     p->resident = algo == GELIM_GPU_BLOCKED && n <= lim && !p->lookahead;
-    // GELIM_HYBRID: trailing-system size handed to the resident LU by the
-    // fused schedule (default 1024, the resident LU's 2-slot regime; 0 = off)
+    // GELIM_HYBRID: 0 turns the hybrid off (pure fused schedule); any other
+    // value keeps the validated 1024-row tail (the resident LU's 2-slot
+    // regime).  Other tails (512 / 640 / 768 / 896 / 1152: 1- and 4-slot
+    // regimes, in-place) are not offered: an A/B sweep over them ended in an
+    // illegal-address fault (profiles/hybrid_tail_sweep.txt) and none of them
+    // is covered by a GPU test.
     const char* eh = std::getenv("GELIM_HYBRID");
-    const int64_t tail = eh ? std::atoll(eh) : 1024;
+    const int64_t tail = (eh && std::atoll(eh) == 0) ? 0 : 1024;
     if (algo == GELIM_GPU_BLOCKED && !p->resident && p->fused && tail > 0 && n > tail &&
         tail <= gelim::rlu_max_n() && sched != "fused")
       p->split = n - tail;  // rounded to a panel boundary below

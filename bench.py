@@ -107,8 +107,16 @@ def main() -> None:
         ker = sorted(r.kernel_s for r in runs)[len(runs) // 2]
         ref = A.double() @ B.double()
         rel = ((Ch.double() - ref).abs().max() / ref.abs().max()).item()
-        mm = {"n": 2048, "end_to_end_s": e2e, "kernel_s": ker, "kernel_tflops": 2 * 2048 ** 3 / ker * 1e-12,
-              "vs_reference_cuda_v2": BASELINE_MATMUL_S / e2e, "max_rel_err": rel}
+        # same timer scope, transfers overlapped with the GEMM in row chunks
+        for _ in range(2):
+            model.run_pipelined(A, B, Ch)
+        pruns = [model.run_pipelined(A, B, Ch) for _ in range(5)]
+        pe2e = sorted(r.end_to_end_s for r in pruns)[len(pruns) // 2]
+        prel = ((Ch.double() - ref).abs().max() / ref.abs().max()).item()
+        best = min(e2e, pe2e)
+        mm = {"n": 2048, "end_to_end_s": best, "end_to_end_serial_s": e2e, "end_to_end_pipelined_s": pe2e,
+              "kernel_s": ker, "kernel_tflops": 2 * 2048 ** 3 / ker * 1e-12,
+              "vs_reference_cuda_v2": BASELINE_MATMUL_S / best, "max_rel_err": max(rel, prel)}
 
     # -- speedup vs the reference's sequential loops on THIS host --------------
     seq = None

@@ -62,3 +62,14 @@ def test_matmul_model_reference_timing(gelim, cuda):
     t = gelim.MatMul("mfma", cuda).run_reference_style(A.pin_memory(), B.pin_memory(), Ch)
     assert t.end_to_end_s >= t.kernel_s > 0
     _check(Ch.to(cuda), A.to(cuda), B.to(cuda))
+
+
+@pytest.mark.parametrize("n,chunks", [(512, 8), (2048, 8), (1000, 3)])
+def test_matmul_model_pipelined(gelim, cuda, n, chunks):
+    """Chunked H2D / GEMM / D2H overlap: same result as the serial path."""
+    A, B = gelim.ops.matmul.reference_inputs(n)
+    A, B = A.pin_memory(), B.pin_memory()
+    Ch = torch.empty_like(A).pin_memory()
+    t = gelim.MatMul("mfma", cuda).run_pipelined(A, B, Ch, chunks=chunks)
+    assert t.end_to_end_s >= t.kernel_s > 0
+    _check(Ch.to(cuda), A.to(cuda), B.to(cuda))

@@ -63,19 +63,27 @@ class MatMul:
         return MatMulTiming(e2e, kt.elapsed_s, n, self.kernel)
 
     def run_pipelined(self, A_host: torch.Tensor, B_host: torch.Tensor, C_host: torch.Tensor,
-                      chunks: int = 8) -> MatMulTiming:
+                      chunks: int = 2) -> MatMulTiming:
         """End-to-end multiply (same timer scope as run_reference_style) with
         chunked H2D / GEMM / D2H overlap on three streams.  kernel_s is the
-        sum of the per-chunk GEMM times."""
+        sum of the per-chunk GEMM times.  Measured at 2048^2
+        (profiles/matmul2048_pipeline_sweep.txt): 2 chunks 1.07 ms vs 1.17 ms
+        serial; every extra chunk costs ~0.13 ms of per-copy overhead, so
+        the default is 2."""
         n, dev = A_host.shape[0], self.device
         if not (A_host.is_pinned() and B_host.is_pinned() and C_host.is_pinned()):
             raise ValueError("run_pipelined needs pinned host tensors")
         bounds = [(n * c // chunks, n * (c + 1) // chunks) for c in range(chunks)]
         bounds = [(r0, r1) for r0, r1 in bounds if r1 > r0]
         cur = torch.cuda.current_stream(dev)
-        up, down = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
-        ev = [(torch.cuda.Event(), torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-              for _ in bounds]
+        if not hasattr(self, "_streams"):  # created once: stream creation is ~100 us
+            self._streams = (torch.cuda.Stream(dev), torch.cuda.Stream(dev))
+            self._events = []
+        up, down = self._streams
+        while len(self._events) < len(bounds):
+            self._events.append((torch.cuda.Event(), torch.cuda.Event(enable_timing=True),
+                                 torch.cuda.Event(enable_timing=True)))
+        ev = self._events[:len(bounds)]
         torch.cuda.synchronize(dev)
         t0 = wall()
         dA = torch.empty_like(A_host, device=dev)

@@ -105,6 +105,19 @@ def test_hybrid_matches_pure_fused(gelim, cuda, monkeypatch, n):
     assert gelim.ops.gauss.error_metric(x_h) < 1e-7
 
 
+@pytest.mark.parametrize("value", ["512", "1152"])
+def test_hybrid_tail_knob_pinned(gelim, cuda, monkeypatch, value):
+    """Only the validated 1024-row tail is selectable: any non-zero
+    GELIM_HYBRID value runs exactly the default schedule (bitwise)."""
+    n = 2048
+    aug = gelim.random_system(n, seed=77, device=cuda)
+    x_d = gelim.GaussSolver(n, backend="hip", device=cuda).solve(aug, check=True).clone()
+    monkeypatch.setenv("GELIM_HYBRID", value)
+    x_v = gelim.GaussSolver(n, backend="hip", device=cuda).solve(aug, check=True)
+    torch.cuda.synchronize()
+    assert torch.equal(x_d, x_v)
+
+
 @pytest.mark.parametrize("zero_col", [100, 1500])
 def test_hybrid_singular_column(gelim, cuda, zero_col):
     """A zero column in the fused part (100) or in the resident tail (1500):

@@ -51,13 +51,20 @@ __global__ void naive_elem_kernel(Mat p) {
   *c = p.acc ? *c + temp : temp;
 }
 
-constexpr int BM = 128, BN = 128, BK = 16;
+// 128 x 64 tiles: 512 workgroups at 2048^2, two co-resident per CU, so one
+// workgroup's LDS store + barrier hides under the other's MFMAs
+constexpr int BM = 128, BN = 64, BK = 16;
+constexpr int WN = BN / 2;  // columns per wave (2 x 2 waves)
 constexpr int kMmThreads = 256;
 constexpr int APAD = 4, BPAD = 4;
 
+// float4s per thread for one A (BM x BK, k fastest) / B (BK x BN) tile
+constexpr int kFA = BM * BK / 4 / kMmThreads, kFB = BK * BN / 4 / kMmThreads;
+static_assert(kFA * 4 * kMmThreads == BM * BK && kFB * 4 * kMmThreads == BK * BN, "tile / threads");
+
 struct Frag {
-  float4 a[2];  // A tile: 2 float4 per thread (128 rows x 16 k)
-  float4 b[2];  // B tile: 2 float4 per thread (16 k x 128 cols)
+  float4 a[kFA];  // A tile: row = idx / (BK/4), k = 4 (idx % (BK/4)), idx = t + 256 h
+  float4 b[kFB];  // B tile: k = idx / (BN/4), col = 4 (idx % (BN/4))
 };
 
 template <bool CHECK>
@@ -68,8 +75,9 @@ __device__ __forceinline__ void load_tiles(Frag& f, const Mat& p, int m0, int n0
   const int64_t lda = p.lda, ldb = p.ldb;
   const int t = threadIdx.x;
 #pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    const int row = (t >> 2) + 64 * h, kc = (t & 3) * 4;
+  for (int h = 0; h < kFA; ++h) {
+    const int idx = t + kMmThreads * h;
+    const int row = idx / (BK / 4), kc = (idx % (BK / 4)) * 4;
     const int gm = m0 + row, gk = k0 + kc;
     if (!CHECK) {
       f.a[h] = *reinterpret_cast<const float4*>(A + (int64_t)gm * lda + gk);
@@ -79,7 +87,11 @@ __device__ __forceinline__ void load_tiles(Frag& f, const Mat& p, int m0, int n0
       for (int e = 0; e < 4; ++e) v[e] = (gm < M && gk + e < K) ? A[(int64_t)gm * lda + gk + e] : 0.f;
       f.a[h] = make_float4(v[0], v[1], v[2], v[3]);
     }
-    const int kr = (t >> 5) + 8 * h, nc = (t & 31) * 4;
+  }
+#pragma unroll
+  for (int h = 0; h < kFB; ++h) {
+    const int idx = t + kMmThreads * h;
+    const int kr = idx / (BN / 4), nc = (idx % (BN / 4)) * 4;
     const int gkb = k0 + kr, gn = n0 + nc;
     if (!CHECK) {
       f.b[h] = *reinterpret_cast<const float4*>(B + (int64_t)gkb * ldb + gn);
@@ -96,19 +108,24 @@ __device__ __forceinline__ void store_tiles(const Frag& f, float (*As)[BM + APAD
                                             float (*Bs)[BN + BPAD]) {
   const int t = threadIdx.x;
 #pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    const int row = (t >> 2) + 64 * h, kc = (t & 3) * 4;
+  for (int h = 0; h < kFA; ++h) {
+    const int idx = t + kMmThreads * h;
+    const int row = idx / (BK / 4), kc = (idx % (BK / 4)) * 4;
     As[kc + 0][row] = f.a[h].x;
     As[kc + 1][row] = f.a[h].y;
     As[kc + 2][row] = f.a[h].z;
     As[kc + 3][row] = f.a[h].w;
-    const int kr = (t >> 5) + 8 * h, nc = (t & 31) * 4;
+  }
+#pragma unroll
+  for (int h = 0; h < kFB; ++h) {
+    const int idx = t + kMmThreads * h;
+    const int kr = idx / (BN / 4), nc = (idx % (BN / 4)) * 4;
     *reinterpret_cast<float4*>(&Bs[kr][nc]) = f.b[h];
   }
 }
 
 template <bool CHECK>
-__global__ __launch_bounds__(kMmThreads) void mfma_gemm_kernel(Mat p, int tiles_n, int ntiles) {
+__global__ __launch_bounds__(kMmThreads, 2) void mfma_gemm_kernel(Mat p, int tiles_n, int ntiles) {
   const int M = p.M, N = p.N, K = p.K;
   __shared__ __attribute__((aligned(16))) float As[2][BK][BM + APAD];
   __shared__ __attribute__((aligned(16))) float Bs[2][BK][BN + BPAD];
@@ -121,14 +138,15 @@ __global__ __launch_bounds__(kMmThreads) void mfma_gemm_kernel(Mat p, int tiles_
   const int m0 = (tile / tiles_n) * BM, n0 = (tile % tiles_n) * BN;
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
+  const int wm = (wave >> 1) * 64, wn = (wave & 1) * WN;
   const int l31 = lane & 31, kh = lane >> 5;
 
-  dev::f16x acc[2][2];
+  constexpr int NJ = WN / 32;
+  dev::f16x acc[2][NJ];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < NJ; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
@@ -146,12 +164,12 @@ __global__ __launch_bounds__(kMmThreads) void mfma_gemm_kernel(Mat p, int tiles_
       const int kk = k + kh;
       float a0 = As[cur][kk][wm + l31];
       float a1 = As[cur][kk][wm + 32 + l31];
-      float b0 = Bs[cur][kk][wn + l31];
-      float b1 = Bs[cur][kk][wn + 32 + l31];
-      acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
-      acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
-      acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
-      acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const float bj = Bs[cur][kk][wn + 32 * j + l31];
+        acc[0][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, bj, acc[0][j], 0, 0, 0);
+        acc[1][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, bj, acc[1][j], 0, 0, 0);
+      }
     }
     if (kt + 1 < nk) store_tiles(f, As[cur ^ 1], Bs[cur ^ 1]);
     __syncthreads();
@@ -161,7 +179,7 @@ __global__ __launch_bounds__(kMmThreads) void mfma_gemm_kernel(Mat p, int tiles_
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
+    for (int j = 0; j < NJ; ++j) {
       const int col = n0 + wn + 32 * j + l31;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {

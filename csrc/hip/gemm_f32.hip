@@ -51,10 +51,12 @@ __global__ void naive_elem_kernel(Mat p) {
   *c = p.acc ? *c + temp : temp;
 }
 
-// 128 x 64 tiles: 512 workgroups at 2048^2, two co-resident per CU, so one
-// workgroup's LDS store + barrier hides under the other's MFMAs
-constexpr int BM = 128, BN = 64, BK = 16;
-constexpr int WN = BN / 2;  // columns per wave (2 x 2 waves)
+// 64 x 64 tiles: 1024 workgroups at 2048^2, four co-resident per CU, so one
+// workgroup's LDS store + barrier hides under the others' MFMAs.  Measured
+// at 2048^2: 128x128 179 us, 128x64 170 us, 64x64 166 us (103.8 TFLOP/s);
+// BK = 32 is no better at either tile size.
+constexpr int BM = 64, BN = 64, BK = 16;
+constexpr int WM = BM / 2, WN = BN / 2;  // rows / columns per wave (2 x 2 waves)
 constexpr int kMmThreads = 256;
 constexpr int APAD = 4, BPAD = 4;
 
@@ -138,13 +140,13 @@ __global__ __launch_bounds__(kMmThreads, 2) void mfma_gemm_kernel(Mat p, int til
   const int m0 = (tile / tiles_n) * BM, n0 = (tile % tiles_n) * BN;
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int wm = (wave >> 1) * 64, wn = (wave & 1) * WN;
+  const int wm = (wave >> 1) * WM, wn = (wave & 1) * WN;
   const int l31 = lane & 31, kh = lane >> 5;
 
-  constexpr int NJ = WN / 32;
-  dev::f16x acc[2][NJ];
+  constexpr int MI = WM / 32, NJ = WN / 32;
+  dev::f16x acc[MI][NJ];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < MI; ++i)
 #pragma unroll
     for (int j = 0; j < NJ; ++j)
 #pragma unroll
@@ -162,13 +164,15 @@ __global__ __launch_bounds__(kMmThreads, 2) void mfma_gemm_kernel(Mat p, int til
 #pragma unroll
     for (int k = 0; k < BK; k += 2) {
       const int kk = k + kh;
-      float a0 = As[cur][kk][wm + l31];
-      float a1 = As[cur][kk][wm + 32 + l31];
+      float ai[MI];
+#pragma unroll
+      for (int i = 0; i < MI; ++i) ai[i] = As[cur][kk][wm + 32 * i + l31];
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
         const float bj = Bs[cur][kk][wn + 32 * j + l31];
-        acc[0][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, bj, acc[0][j], 0, 0, 0);
-        acc[1][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, bj, acc[1][j], 0, 0, 0);
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(ai[i], bj, acc[i][j], 0, 0, 0);
       }
     }
     if (kt + 1 < nk) store_tiles(f, As[cur ^ 1], Bs[cur ^ 1]);
@@ -177,7 +181,7 @@ __global__ __launch_bounds__(kMmThreads, 2) void mfma_gemm_kernel(Mat p, int til
 
   // epilogue: C/D map of 32x32 f32 MFMA: col = l&31, row = (r&3) + 8(r>>2) + 4(l>>5)
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < MI; ++i)
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
       const int col = n0 + wn + 32 * j + l31;

@@ -1,0 +1,222 @@
+// fp64 GEMM on the CDNA4 matrix cores: C += alpha * A * B (alpha = +-1),
+// row-major operands with arbitrary leading dimensions.  This is the trailing
+// update A22 -= L21 * U12 of the wide-panel blocked LU (biglu.hip) -- the
+// reference's O(n^3) hot loop `matrix[j][k] -= pivotval * matrix[i][k]`
+// (OpenMP_and_MPI/gauss_openmp/gauss_external_input.c:172-180) with nb
+// rank-1 updates fused into one rank-nb product -- and of the distributed
+// solver's per-block update.
+//
+// Shape of the kernel (measured, tools/microbench/mfma_f64.hip): one wave
+// issues a v_mfma_f64_16x16x4_f64 every 64 cycles whatever the number of
+// independent accumulators, two waves on a SIMD interleave to one per 32
+// cycles (77 TFLOP/s chip-wide).  So the kernel runs two 256-thread
+// workgroups per CU (2 waves per SIMD, <= 256 VGPRs per lane):
+//  * workgroup tile 128 x 128, 4 waves as 2 x 2, each wave 64 x 64 = 4 x 4
+//    blocks of the 16x16x4 f64 MFMA (64 accumulator doubles per lane);
+//  * K in steps of BK = 16, A and B tiles double-buffered in LDS (one barrier
+//    per step); A is stored transposed ([k][m]) and negated when alpha < 0,
+//    B as is ([k][n]); rows padded to 144 doubles so the two 16-lane halves
+//    of every ds_read_b64 land on disjoint bank sets;
+//  * f64 MFMA operand maps (cdna_hip_programming.md §3): A lane l holds
+//    A[l&15][k=l>>4], B lane l holds B[k=l>>4][l&15], C/D register r of lane l
+//    is C[row=(l>>4)+4r][col=l&15] (NOT the f32 C/D map);
+//  * C is read into the accumulators up front and written back once;
+//  * tiles are dealt to XCDs in contiguous runs (consecutive tiles share an
+//    A row panel -> same L2).
+// Interior tiles use 16-byte loads with no bounds logic; edge tiles clamp
+// rows/columns (results outside C are never stored) and zero k >= K.
+// Contract (checked on the host): A and B 16-byte aligned, lda / ldb / K
+// even, ldb > N when N is odd.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <string>
+
+#include "device_common.h"
+#include "gelim/internal.h"
+
+namespace gelim {
+namespace {
+
+constexpr int BM = 128, BN = 128, BK = 16;
+constexpr int kThreads = 256;
+constexpr int SA = BM + 16, SB = BN + 16;   // LDS row strides (doubles)
+constexpr int WM = 64, WN = 64;             // per-wave tile
+constexpr int MB = WM / 16, NB = WN / 16;   // 16x16 blocks per wave
+
+struct Args {
+  double* C;
+  int64_t ldc;
+  const double* A;
+  int64_t lda;
+  const double* B;
+  int64_t ldb;
+  int M, N, K;
+  int tiles_n, ntiles;
+  double alpha;
+};
+
+// 16-byte chunks per thread per tile: A 128x16 -> 1024 chunks, B 16x128 -> 1024
+constexpr int kCA = BM * BK / 2 / kThreads, kCB = BK * BN / 2 / kThreads;
+
+struct Stage {
+  double2 a[kCA];
+  double2 b[kCB];
+};
+
+template <bool FULL>
+__device__ __forceinline__ void load_stage(Stage& st, const Args& g, int m0, int n0, int k0) {
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int h = 0; h < kCA; ++h) {
+    const int idx = t + kThreads * h;
+    const int row = idx >> 3, kc = (idx & 7) * 2;  // 8 chunks per A row of the tile
+    if constexpr (FULL) {
+      st.a[h] = *reinterpret_cast<const double2*>(g.A + (int64_t)(m0 + row) * g.lda + k0 + kc);
+    } else {
+      // rows past M are clamped (their products are never stored); K is even,
+      // so a chunk is wholly inside or wholly past K
+      const int r = min(m0 + row, g.M - 1);
+      const int k = k0 + kc;
+      const double2 v = *reinterpret_cast<const double2*>(g.A + (int64_t)r * g.lda + min(k, g.K - 2));
+      st.a[h] = k < g.K ? v : make_double2(0.0, 0.0);
+    }
+  }
+#pragma unroll
+  for (int h = 0; h < kCB; ++h) {
+    const int idx = t + kThreads * h;
+    const int kr = idx >> 6, nc = (idx & 63) * 2;  // 64 chunks per B row of the tile
+    if constexpr (FULL) {
+      st.b[h] = *reinterpret_cast<const double2*>(g.B + (int64_t)(k0 + kr) * g.ldb + n0 + nc);
+    } else {
+      // columns past N are clamped to the last chunk (never stored); with N
+      // odd that chunk reads one double of row padding (ldb > N, checked)
+      const int k = k0 + kr;
+      const int c = min(n0 + nc, (g.N - 1) & ~1);
+      const double2 v = *reinterpret_cast<const double2*>(g.B + (int64_t)min(k, g.K - 1) * g.ldb + c);
+      st.b[h] = k < g.K ? v : make_double2(0.0, 0.0);
+    }
+  }
+}
+
+__device__ __forceinline__ void store_stage(const Stage& st, double* As, double* Bs, double alpha) {
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int h = 0; h < kCA; ++h) {
+    const int idx = t + kThreads * h;
+    const int row = idx >> 3, kc = (idx & 7) * 2;
+    As[kc * SA + row] = alpha * st.a[h].x;
+    As[(kc + 1) * SA + row] = alpha * st.a[h].y;
+  }
+#pragma unroll
+  for (int h = 0; h < kCB; ++h) {
+    const int idx = t + kThreads * h;
+    const int kr = idx >> 6, nc = (idx & 63) * 2;
+    *reinterpret_cast<double2*>(&Bs[kr * SB + nc]) = st.b[h];
+  }
+}
+
+template <bool FULL>
+__device__ __forceinline__ void tile_body(const Args& g, int m0, int n0, double* lds) {
+  double* As[2] = {lds, lds + BK * SA};
+  double* Bs[2] = {lds + 2 * BK * SA, lds + 2 * BK * SA + BK * SB};
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wm = (wave >> 1) * WM, wn = (wave & 1) * WN;
+  const int r16 = lane & 15, q = lane >> 4;
+
+  dev::d4 acc[MB][NB];
+#pragma unroll
+  for (int i = 0; i < MB; ++i)
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      const int col = n0 + wn + 16 * j + r16;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = m0 + wm + 16 * i + q + 4 * r;
+        // edge tiles: clamped address, the value is never stored back
+        acc[i][j][r] = g.C[(int64_t)(FULL ? row : min(row, g.M - 1)) * g.ldc + (FULL ? col : min(col, g.N - 1))];
+      }
+    }
+
+  Stage st;
+  load_stage<FULL>(st, g, m0, n0, 0);
+  store_stage(st, As[0], Bs[0], g.alpha);
+  __syncthreads();
+  const int nk = (g.K + BK - 1) / BK;
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) load_stage<FULL>(st, g, m0, n0, (kt + 1) * BK);
+    const double* a_s = As[cur] + wm + r16;
+    const double* b_s = Bs[cur] + wn + r16;
+#pragma unroll
+    for (int kk = 0; kk < BK; kk += 4) {
+      const int k = kk + q;
+      double af[MB], bf[NB];
+#pragma unroll
+      for (int i = 0; i < MB; ++i) af[i] = a_s[k * SA + 16 * i];
+#pragma unroll
+      for (int j = 0; j < NB; ++j) bf[j] = b_s[k * SB + 16 * j];
+#pragma unroll
+      for (int i = 0; i < MB; ++i)
+#pragma unroll
+        for (int j = 0; j < NB; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[i], bf[j], acc[i][j], 0, 0, 0);
+    }
+    if (kt + 1 < nk) store_stage(st, As[cur ^ 1], Bs[cur ^ 1], g.alpha);
+    __syncthreads();
+  }
+
+#pragma unroll
+  for (int i = 0; i < MB; ++i)
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      const int col = n0 + wn + 16 * j + r16;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = m0 + wm + 16 * i + q + 4 * r;
+        if (FULL || (row < g.M && col < g.N)) g.C[(int64_t)row * g.ldc + col] = acc[i][j][r];
+      }
+    }
+}
+
+__global__ __launch_bounds__(kThreads, 2) void dgemm_kernel(Args g) {
+  __shared__ __attribute__((aligned(16))) double lds[2 * BK * SA + 2 * BK * SB];
+  // XCD-aware bijective remap: XCD x (blocks x, x+8, ...) gets a contiguous
+  // run of tiles, so tiles sharing an A row panel share that XCD's L2
+  const int orig = blockIdx.x;
+  const int q = g.ntiles / 8, rem = g.ntiles % 8, xcd = orig % 8;
+  const int tile = (xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q) + orig / 8;
+  const int m0 = (tile / g.tiles_n) * BM, n0 = (tile % g.tiles_n) * BN;
+  if (m0 + BM <= g.M && n0 + BN <= g.N && (g.K % BK) == 0)
+    tile_body<true>(g, m0, n0, lds);
+  else
+    tile_body<false>(g, m0, n0, lds);
+}
+
+}  // namespace
+
+// C (M x N, ldc) += alpha * A (M x K, lda) * B (K x N, ldb); alpha in {+1, -1}
+// in practice (any value works: A is scaled once on its way into LDS).
+int dgemm(double* C, int64_t ldc, const double* A, int64_t lda, const double* B, int64_t ldb, int64_t M,
+          int64_t N, int64_t K, double alpha, hipStream_t s) {
+  if (M <= 0 || N <= 0 || K <= 0) return GELIM_OK;
+  if (M > INT32_MAX || N > INT32_MAX || K > INT32_MAX) return GELIM_FAIL(GELIM_E_ARG, "dgemm: dimension > 2^31");
+  // 16-byte operand chunks: 16-byte aligned A and B, even leading dimensions
+  // and K, and one double of row padding in B when N is odd
+  if ((K & 1) || (lda & 1) || (ldb & 1) || (((uintptr_t)A | (uintptr_t)B) & 15) || ((N & 1) && ldb <= N) ||
+      lda < K || ldb < N || ldc < N)
+    return GELIM_FAIL(GELIM_E_ARG, "dgemm: unsupported alignment / leading dimensions (K=" + std::to_string(K) +
+                                       " lda=" + std::to_string(lda) + " ldb=" + std::to_string(ldb) + ")");
+  const int tm = (int)((M + BM - 1) / BM), tn = (int)((N + BN - 1) / BN);
+  Args g{C, ldc, A, lda, B, ldb, (int)M, (int)N, (int)K, tn, tm * tn, alpha};
+  hipLaunchKernelGGL(dgemm_kernel, dim3((unsigned)(tm * tn)), dim3(kThreads), 0, s, g);
+  HIP_TRY(hipGetLastError());
+  return GELIM_OK;
+}
+
+}  // namespace gelim
+
+extern "C" int gelim_gpu_dgemm(double* dC, int64_t ldc, const double* dA, int64_t lda, const double* dB,
+                               int64_t ldb, int64_t M, int64_t N, int64_t K, double alpha, void* stream) {
+  return gelim::dgemm(dC, ldc, dA, lda, dB, ldb, M, N, K, alpha, (hipStream_t)stream);
+}

@@ -36,6 +36,20 @@ int backsub_f64(const double* U, int64_t ldu, const double* y, int64_t incy, dou
 int backsub_f32(const float* U, int64_t ldu, const float* y, int64_t incy, double* x,
                 double* bnorm, int64_t n, int unit, double* yw, hipStream_t s,
                 const int* perm = nullptr, int* err = nullptr);
+int dgemm(double* C, int64_t ldc, const double* A, int64_t lda, const double* B, int64_t ldb, int64_t M,
+          int64_t N, int64_t K, double alpha, hipStream_t s);
+namespace big {
+size_t workspace_bytes();
+int leaf_width();
+int64_t max_rows();
+int leaf_factor(double* A, int64_t lda, int64_t m, int64_t c0, int mode, int* ipiv, int* pairs, int* info,
+                void* ws, int set, hipStream_t s);
+int laswp_trsm(double* A, int64_t lda, int64_t c0, int64_t lend, int64_t rbeg, int64_t rend, int64_t trsm_end,
+               const int* pairs, hipStream_t s);
+int tail_gemv(const double* A, int64_t lda, int64_t n, int64_t K, const double* x, double* y, double* bnorm,
+              hipStream_t s);
+int fold_info(int* info, const int* tinfo, int64_t K, hipStream_t s);
+}  // namespace big
 int64_t rlu_max_n();
 size_t rlu_workspace_bytes(int64_t n);
 int rlu_factor(const double* src, int64_t lds, double* work, int64_t ldw, int64_t n, int mode,
@@ -70,6 +84,16 @@ struct gelim_gauss_plan {
   double* sbuf = nullptr;                // narrow-kernel strip buffer (16 x ldL, column-major)
   double* lbuf = nullptr;                // fused steps: factored panels, column-major, ping-pong
   int64_t ldL = 0;                       //   (2 x 16 x ldL doubles)
+  // wide-panel engine (n > big_tail): columns [0, big_k) are eliminated by
+  // 256-column outer panels of 32-column multi-workgroup leaves (biglu.hip)
+  // with fp64 MFMA trailing updates (dgemm.hip); the trailing
+  // (n - big_k)-order system is solved by a nested plan of this file and the
+  // top rows by one mat-vec + back substitution.
+  int64_t big_k = 0;
+  gelim_gauss_plan* tail = nullptr;
+  void* big_ws = nullptr;                // leaf exchange granules + rows
+  int* big_pairs = nullptr;              // per-leaf row movement
+  double* big_y = nullptr;               // top right-hand side after the tail
   hipGraphExec_t exec = nullptr;
   const void* k_src = nullptr;
   int64_t k_ld = 0;
@@ -94,10 +118,62 @@ __global__ void hybrid_perm_kernel(int* __restrict__ perm, int n, int split, int
   }
 }
 
+constexpr int64_t kBigNb = 256;          // outer panel width of the wide-panel engine
+constexpr int64_t kBigPairSlot = 1 + 4 * 32 + 3;
+
+int enqueue(gelim_gauss_plan* p, const void* src, int64_t src_ld, void* dx, void* bnorm, hipStream_t s);
+
+// Wide-panel LU of columns [0, big_k) of the working system, then the tail
+// solve and the block back substitution:
+//   x[K..n) = tail solve of A[K:, K:] (already carrying every update),
+//   y = A[0:K, n] - A[0:K, K:n] x[K..n),  x[0..K) = U11^-1 y.
+int enqueue_big(gelim_gauss_plan* p, double* A, double* x, double* bnorm, hipStream_t s) {
+  using namespace gelim;
+  const int64_t n = p->n, lda = p->lda, K = p->big_k, LW = big::leaf_width();
+  HIP_TRY(hipMemsetAsync(p->big_ws, 0, big::workspace_bytes(), s));
+  int leaf = 0;
+  for (int64_t k = 0; k < K; k += kBigNb) {
+    const int64_t kend = std::min(k + kBigNb, K);
+    for (int64_t c0 = k; c0 < kend; c0 += LW, ++leaf) {
+      int* pr = p->big_pairs + leaf * kBigPairSlot;
+      GELIM_TRY(big::leaf_factor(A + c0 * lda + c0, lda, n - c0, c0, p->pivot, p->piv, pr, p->info, p->big_ws,
+                                 leaf, s));
+      // interchanges on every other column (L part, rest of the panel,
+      // trailing columns, b); TRSM of the leaf's U rows inside the panel
+      GELIM_TRY(big::laswp_trsm(A + c0 * lda, lda, c0, c0, c0 + LW, n + 1, kend, pr, s));
+      const int64_t c1 = c0 + LW;
+      if (c1 < kend)  // the rest of this outer panel
+        GELIM_TRY(dgemm(A + c1 * lda + c1, lda, A + c1 * lda + c0, lda, A + c0 * lda + c1, lda, n - c1, kend - c1, LW,
+                        -1.0, s));
+    }
+    // U12 of the outer panel (its rows are final only now): blocked forward
+    // substitution with the panel's unit-lower L11, one 32-row block at a time
+    for (int64_t r = k; r < kend; r += LW) {
+      GELIM_TRY(big::laswp_trsm(A + r * lda, lda, r, 0, kend, n + 1, n + 1, nullptr, s));
+      if (r + LW < kend)
+        GELIM_TRY(dgemm(A + (r + LW) * lda + kend, lda, A + (r + LW) * lda + r, lda, A + r * lda + kend, lda,
+                        kend - r - LW, n + 1 - kend, LW, -1.0, s));
+    }
+    // trailing update of the outer panel: A22 -= L21 U12, K = kend - k
+    GELIM_TRY(dgemm(A + kend * lda + kend, lda, A + kend * lda + k, lda, A + k * lda + kend, lda, n - kend,
+                    n + 1 - kend, kend - k, -1.0, s));
+  }
+  GELIM_TRY(enqueue(p->tail, A + K * lda + K, lda, x + K, bnorm ? bnorm + K : nullptr, s));
+  GELIM_TRY(big::fold_info(p->info, p->tail->info, K, s));
+  GELIM_TRY(big::tail_gemv(A, lda, n, K, x, p->big_y, bnorm, s));
+  return backsub_f64(A, lda, p->big_y, 1, x, nullptr, K, 0, p->yw, s, nullptr, p->info + 1);
+}
+
 int enqueue(gelim_gauss_plan* p, const void* src, int64_t src_ld, void* dx, void* bnorm,
             hipStream_t s) {
   using namespace gelim;
   const int64_t n = p->n, lda = p->lda;
+  if (p->big_k > 0) {
+    if (src)
+      HIP_TRY(hipMemcpy2DAsync(p->work, lda * 8, src, src_ld * 8, (n + 1) * 8, n, hipMemcpyDeviceToDevice, s));
+    HIP_TRY(hipMemsetAsync(p->info, 0, 16, s));
+    return enqueue_big(p, static_cast<double*>(p->work), static_cast<double*>(dx), static_cast<double*>(bnorm), s);
+  }
   if (p->algo == GELIM_GPU_BLOCKED && p->resident) {
     // One persistent launch reads the system straight from src (no copy),
     // leaves U rows at their physical positions and the pivot row of every
@@ -233,8 +309,16 @@ extern "C" gelim_gauss_plan* gelim_gauss_plan_create(int64_t n, int algo, int pi
     GELIM_FAIL(GELIM_E_ARG, "blocked LU is fp64 only (fp32 fails saylr4/orsreg_1, SURVEY §4.3)");
     return nullptr;
   }
-  if (algo == GELIM_GPU_BLOCKED && gelim::panel_width_for(n) <= 0) {
-    GELIM_FAIL(GELIM_E_ARG, "blocked LU: n > 16384 not supported on one GPU yet");
+  // wide-panel engine for n > big_tail (default 2048, the largest order the
+  // register-resident engines take; GELIM_BIG_TAIL lowers it for tests):
+  // columns [0, big_k) with big_k the multiple of the leaf width that leaves
+  // a trailing system of at most big_tail
+  int64_t big_tail = 2048;
+  if (const char* e = std::getenv("GELIM_BIG_TAIL")) big_tail = std::max<int64_t>(64, std::min<int64_t>(2048, std::atoll(e)));
+  const int64_t lw = gelim::big::leaf_width();
+  const int64_t big_k = (algo == GELIM_GPU_BLOCKED && n > big_tail) ? (n - big_tail + lw - 1) / lw * lw : 0;
+  if (big_k > 0 && n > gelim::big::max_rows()) {
+    GELIM_FAIL(GELIM_E_ARG, "blocked LU: n > " + std::to_string(gelim::big::max_rows()) + " not supported on one GPU");
     return nullptr;
   }
   auto* p = new gelim_gauss_plan;
@@ -244,12 +328,33 @@ extern "C" gelim_gauss_plan* gelim_gauss_plan_create(int64_t n, int algo, int pi
   p->eb = dtype_bytes;
   p->use_graph = use_graph != 0;
   const int64_t align = 64 / dtype_bytes;  // 64-byte rows
-  p->lda = (n + 1 + align - 1) / align * align;
+  // the wide-panel engine's GEMMs read 16-byte chunks that may reach one
+  // column past b: keep at least one padding column
+  p->lda = (n + 1 + (big_k > 0 ? 1 : 0) + align - 1) / align * align;
   auto fail = [&](const char* what) -> gelim_gauss_plan* {
     GELIM_FAIL(GELIM_E_NOMEM, std::string("plan_create: ") + what);
     gelim_gauss_plan_destroy(p);
     return nullptr;
   };
+  if (big_k > 0) {
+    p->big_k = big_k;
+    if (hipMalloc(&p->work, (size_t)(n * p->lda * 8)) != hipSuccess) return fail("work");
+    if (hipMalloc((void**)&p->piv, (size_t)(n + 64) * sizeof(int)) != hipSuccess) return fail("piv");
+    if (hipMalloc((void**)&p->info, 16) != hipSuccess) return fail("info");
+    if (hipMalloc((void**)&p->yw, (size_t)n * sizeof(double)) != hipSuccess) return fail("yw");
+    if (hipMalloc((void**)&p->big_y, (size_t)big_k * sizeof(double)) != hipSuccess) return fail("big_y");
+    if (hipMalloc(&p->big_ws, gelim::big::workspace_bytes()) != hipSuccess) return fail("leaf workspace");
+    const int64_t nleaves = big_k / lw;
+    if (hipMalloc((void**)&p->big_pairs, sizeof(int) * kBigPairSlot * nleaves) != hipSuccess) return fail("pairs");
+    if (hipStreamCreateWithFlags(&p->cap, hipStreamNonBlocking) != hipSuccess) return fail("stream");
+    p->tail = gelim_gauss_plan_create(n - big_k, algo, pivot, dtype_bytes, 0);
+    if (!p->tail) {
+      gelim_gauss_plan_destroy(p);
+      return nullptr;
+    }
+    (void)hipMemset(p->work, 0, (size_t)(n * p->lda * 8));
+    return p;
+  }
   if (hipMalloc(&p->work, (size_t)(n * p->lda * dtype_bytes)) != hipSuccess) return fail("work");
   if (hipMalloc((void**)&p->piv, (size_t)(n + 64) * sizeof(int)) != hipSuccess) return fail("piv");
   if (hipMalloc((void**)&p->info, 16) != hipSuccess) return fail("info");
@@ -340,6 +445,10 @@ extern "C" void gelim_gauss_plan_destroy(gelim_gauss_plan* p) {
   (void)hipFree(p->yw);
   (void)hipFree(p->mcol);
   (void)hipFree(p->tmp);
+  (void)hipFree(p->big_ws);
+  (void)hipFree(p->big_pairs);
+  (void)hipFree(p->big_y);
+  gelim_gauss_plan_destroy(p->tail);
   delete p;
 }
 

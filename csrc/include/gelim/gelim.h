@@ -160,6 +160,22 @@ int gelim_gpu_swap_trsm(double* dC, int64_t ldc, int64_t ncols,
                         const double* dL, int64_t ldl, int64_t w,
                         const int32_t* dpiv, int64_t nrows, void* stream);
 /* C (M x N) -= L (M x K) * U (K x N); fp64 MFMA (v_mfma_f64_16x16x4_f64). */
+/* C (M x N, ldc) += alpha * A (M x K, lda) * B (K x N, ldb) on the fp64
+ * matrix cores (LDS-tiled v_mfma_f64_16x16x4_f64).  A, B 16-byte aligned,
+ * lda / ldb / K even, ldb > N when N is odd. */
+int gelim_gpu_dgemm(double* dC, int64_t ldc, const double* dA, int64_t lda, const double* dB,
+                    int64_t ldb, int64_t M, int64_t N, int64_t K, double alpha, void* stream);
+/* Wide-panel LU pieces (biglu.hip), exposed for tests: factor the m x 32
+ * leaf at dA (its diagonal is row/column c0 of the system: dipiv[c0 + j]
+ * gets the absolute LAPACK pivot row of column c0 + j, dpairs the net row
+ * movement relative to c0), and apply a movement (dpairs may be NULL) to
+ * columns [0, lend) and [rbeg, rend) of rows [c0, ...) plus the TRSM of the
+ * 32 rows from c0 (L11 = the leaf at (c0, c0)) on right columns below
+ * trsm_end (dA: row c0, column 0 of the system). */
+int gelim_gpu_leaf_factor(double* dA, int64_t lda, int64_t m, int64_t c0, int pivot, int32_t* dipiv,
+                          int32_t* dpairs, int32_t* dinfo, void* stream);
+int gelim_gpu_laswp_trsm(double* dA, int64_t lda, int64_t c0, int64_t lend, int64_t rbeg, int64_t rend,
+                         int64_t trsm_end, const int32_t* dpairs, void* stream);
 int gelim_gpu_gemm_update(double* dC, int64_t ldc, const double* dL,
                           int64_t ldl, const double* dU, int64_t ldu,
                           int64_t M, int64_t N, int64_t K, void* stream);

@@ -67,11 +67,17 @@ _PROTOS = {
     "gelim_gpu_panel_max_rows": (_i64, [_i64]),
     "gelim_gpu_swap_trsm": (_int, [_vp, _i64, _i64, _vp, _i64, _i64, _vp, _i64, _vp]),
     "gelim_gpu_gemm_update": (_int, [_vp, _i64, _vp, _i64, _vp, _i64, _i64, _i64, _i64, _vp]),
+    "gelim_gpu_dgemm": (_int, [_vp, _i64, _vp, _i64, _vp, _i64, _i64, _i64, _i64, _dbl, _vp]),
+    "gelim_gpu_leaf_factor": (_int, [_vp, _i64, _i64, _i64, _int, _vp, _vp, _vp, _vp]),
+    "gelim_gpu_leaf_factor_ws": (_int, [_vp, _i64, _i64, _i64, _int, _vp, _vp, _vp, _vp, _int, _vp]),
+    "gelim_gpu_leaf_workspace_bytes": (_i64, []),
+    "gelim_gpu_laswp_trsm": (_int, [_vp, _i64, _i64, _i64, _i64, _i64, _i64, _vp, _vp]),
     "gelim_gpu_backsub": (_int, [_vp, _i64, _vp, _i64, _vp, _vp, _i64, _int, _vp]),
     "gelim_gauss_plan_create": (_vp, [_i64, _int, _int, _int, _int]),
     "gelim_gauss_plan_destroy": (None, [_vp]),
     "gelim_gauss_plan_lda": (_i64, [_vp]),
     "gelim_gauss_plan_work": (_vp, [_vp]),
+    "gelim_gpu_memcpy_d2h": (_int, [_vp, _vp, _i64, _vp]),
     "gelim_gauss_plan_solve": (_int, [_vp, _vp, _i64, _vp, _vp, _vp]),
     "gelim_gauss_plan_info": (_int, [_vp, _vp]),
     "gelim_gpu_matmul_f32": (_int, [_vp, _vp, _vp, _i64, _i64, _i64, _int, _vp]),

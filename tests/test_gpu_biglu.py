@@ -1,0 +1,220 @@
+"""Wide-panel LU (n > 2048; biglu.hip + dgemm.hip) and the fp64 MFMA GEMM,
+against plain fp64 PyTorch references of the same ops."""
+import pytest
+import torch
+
+from conftest import GOLDEN_ERROR
+
+pytestmark = pytest.mark.gpu
+
+
+def _dgemm(gelim, C, A, B, alpha):
+    from gelim import _native
+    from gelim.utils.tensors import ptr, row_major_ld, stream_handle
+
+    M, N = C.shape
+    K = A.shape[1]
+    rc = _native.lib().gelim_gpu_dgemm(ptr(C), row_major_ld(C), ptr(A), row_major_ld(A), ptr(B), row_major_ld(B),
+                                       M, N, K, alpha, stream_handle(C.device))
+    _native.check(rc, "dgemm")
+
+
+@pytest.mark.parametrize("M,N,K", [(128, 128, 16), (256, 384, 256), (300, 517, 32), (129, 1, 2),
+                                   (1000, 2049, 64), (64, 64, 30)])
+@pytest.mark.parametrize("alpha", [-1.0, 1.0])
+def test_dgemm_matches_torch(gelim, cuda, M, N, K, alpha):
+    torch.manual_seed(M * 7 + N + K)
+    ldn = N + 1 + (N + 1) % 2  # even, > N (the dgemm contract)
+    Cf = torch.randn(M, ldn, dtype=torch.float64, device=cuda)
+    Af = torch.randn(M, K + 2, dtype=torch.float64, device=cuda)
+    Bf = torch.randn(K, ldn, dtype=torch.float64, device=cuda)
+    C, A, B = Cf[:, :N], Af[:, :K], Bf[:, :N]
+    ref = C + alpha * (A @ B)
+    C0 = Cf.clone()
+    _dgemm(gelim, C, A, B, alpha)
+    torch.cuda.synchronize()
+    assert torch.allclose(C, ref, rtol=1e-12, atol=1e-11 * K)
+    assert torch.equal(Cf[:, N:], C0[:, N:])  # padding untouched
+
+
+def test_dgemm_rejects_odd_k(gelim, cuda):
+    C = torch.zeros(16, 16, dtype=torch.float64, device=cuda)
+    A = torch.zeros(16, 3, dtype=torch.float64, device=cuda)
+    B = torch.zeros(3, 16, dtype=torch.float64, device=cuda)
+    with pytest.raises(gelim.GelimError):
+        _dgemm(gelim, C, A, B, -1.0)
+
+
+@pytest.mark.parametrize("m", [32, 100, 1024, 1025, 3000, 8192])
+def test_leaf_factor_matches_lapack(gelim, cuda, m):
+    """One 32-column leaf over P = ceil(m/1024) workgroups: pivots equal
+    LAPACK's getrf, factors match to rounding, pairs reproduce the row
+    order."""
+    from gelim import _native
+    from gelim.utils.tensors import ptr, stream_handle
+
+    torch.manual_seed(m)
+    ld = 40
+    P = torch.randn(m, ld, dtype=torch.float64)
+    Pg = P.to(cuda)
+    ipiv = torch.zeros(32, dtype=torch.int32, device=cuda)
+    pairs = torch.zeros(1 + 4 * 32, dtype=torch.int32, device=cuda)
+    info = torch.zeros(4, dtype=torch.int32, device=cuda)
+    rc = _native.lib().gelim_gpu_leaf_factor(ptr(Pg), ld, m, 0, 1, ptr(ipiv), ptr(pairs), ptr(info),
+                                             stream_handle(cuda))
+    _native.check(rc, "leaf_factor")
+    torch.cuda.synchronize()
+    assert info.cpu()[1].item() == 0
+    lu_, piv_ref = torch.linalg.lu_factor(P[:, :32])
+    assert torch.equal(ipiv.cpu().long() + 1, piv_ref.long())
+    assert torch.allclose(Pg.cpu()[:, :32], lu_, rtol=1e-10, atol=1e-10)
+    assert torch.equal(Pg.cpu()[:, 32:], P[:, 32:])
+    # the pair list is the net permutation of the LAPACK interchanges
+    perm = list(range(m))
+    for j, pj in enumerate(piv_ref.tolist()):
+        perm[j], perm[pj - 1] = perm[pj - 1], perm[j]
+    pr = pairs.cpu().tolist()
+    moved = {pr[1 + 2 * e]: pr[2 + 2 * e] for e in range(pr[0])}
+    for dst in range(m):
+        assert moved.get(dst, dst) == perm[dst]
+
+
+def test_laswp_trsm_matches_torch(gelim, cuda):
+    from gelim import _native
+    from gelim.utils.tensors import ptr, stream_handle
+
+    torch.manual_seed(1)
+    n, c0 = 300, 64
+    ncols = n + 1
+    A = torch.randn(n, ncols + 1, dtype=torch.float64)
+    m = n - c0
+    perm = torch.randperm(m)[:40]
+    tgt = torch.arange(m)
+    src_rows = tgt.clone()
+    src_rows[perm] = perm[torch.randperm(40)]  # a permutation of 40 rows
+    pl = [(int(d), int(s)) for d, s in zip(tgt.tolist(), src_rows.tolist()) if d != s]
+    pairs = torch.zeros(1 + 4 * 32, dtype=torch.int32)
+    pairs[0] = len(pl)
+    for e, (d, s) in enumerate(pl):
+        pairs[1 + 2 * e], pairs[2 + 2 * e] = d, s
+    Ag = A.to(cuda)
+    rc = _native.lib().gelim_gpu_laswp_trsm(ptr(Ag[c0:]), A.shape[1], c0, c0, c0 + 32, ncols, ncols,
+                                            ptr(pairs.to(cuda)), stream_handle(cuda))
+    _native.check(rc, "laswp_trsm")
+    torch.cuda.synchronize()
+    L2 = torch.tril(A[c0:c0 + 32, c0:c0 + 32], -1) + torch.eye(32, dtype=torch.float64)
+    ref2 = A.clone()
+    ref2[c0:, :c0] = A[c0:][src_rows][:, :c0]
+    ref2[c0:, c0 + 32:] = A[c0:][src_rows][:, c0 + 32:]
+    ref2[c0:c0 + 32, c0 + 32:ncols] = torch.linalg.solve_triangular(L2, ref2[c0:c0 + 32, c0 + 32:ncols],
+                                                                    upper=False, unitriangular=True)
+    assert torch.allclose(Ag.cpu()[:, :ncols], ref2[:, :ncols], rtol=1e-11, atol=1e-11)
+
+
+def _check_solve(gelim, cuda, n, seed, rtol=1e-8):
+    aug = gelim.random_system(n, seed=seed, device=cuda)
+    x = gelim.GaussSolver(n, backend="hip", device=cuda).solve(aug, check=True)
+    ref = torch.linalg.solve(aug[:, :n], aug[:, n])
+    torch.cuda.synchronize()
+    assert torch.allclose(x, ref, rtol=rtol, atol=rtol * n), (x - ref).abs().max().item()
+    assert gelim.ops.gauss.error_metric(x) < 1e-6
+
+
+@pytest.mark.parametrize("n", [2049, 2500, 3000, 4096, 8192])
+def test_big_solver_vs_torch(gelim, cuda, n):
+    _check_solve(gelim, cuda, n, seed=n + 11)
+
+
+@pytest.mark.parametrize("n", [300, 700, 1000])
+def test_big_solver_small_tail(gelim, cuda, monkeypatch, n):
+    """GELIM_BIG_TAIL=256 runs the wide-panel engine on small systems: several
+    outer panels, leaves with 1 workgroup, a short tail."""
+    monkeypatch.setenv("GELIM_BIG_TAIL", "256")
+    _check_solve(gelim, cuda, n, seed=n + 3)
+
+
+def test_big_solver_multi_workgroup_leaf_ties(gelim, cuda, monkeypatch):
+    """Integer-valued system with many equal |a| candidates across
+    workgroups: the global arg-max must resolve ties to the lowest row
+    (LAPACK / the reference's strict '>') or the solution drifts."""
+    n = 3100
+    g = torch.Generator().manual_seed(5)
+    A = torch.randint(-3, 4, (n, n), generator=g).double()
+    A += torch.eye(n, dtype=torch.float64) * 0.5
+    x0 = torch.arange(1, n + 1, dtype=torch.float64)
+    aug = torch.cat([A, (A @ x0)[:, None]], 1).to(cuda)
+    x = gelim.GaussSolver(n, backend="hip", device=cuda).solve(aug, check=True)
+    P, L, U = torch.linalg.lu(A)
+    ref = torch.linalg.solve(A, A @ x0)
+    assert torch.allclose(x.cpu(), ref, rtol=1e-7, atol=1e-6)
+
+
+def test_big_zero_rule_verify_pattern(gelim, cuda):
+    """The internal programs' zero-pivot rule through the wide-panel engine:
+    synthetic 2*min(i+1,j+1) system, exact pattern."""
+    n = 2300
+    aug = gelim.synthetic_system(n, device=cuda)
+    s = gelim.GaussSolver(n, backend="hip", pivot="zero", device=cuda)
+    x, bn = s.solve(aug, return_bnorm=True)
+    expect = torch.zeros(n, dtype=torch.float64)
+    expect[0], expect[-1] = -0.5, 0.5
+    eb = torch.full((n,), 0.5, dtype=torch.float64)
+    eb[0] = 0.0
+    assert torch.allclose(x.cpu(), expect, rtol=0, atol=1e-11)
+    assert torch.allclose(bn.cpu(), eb, rtol=0, atol=1e-11)
+
+
+@pytest.mark.parametrize("zero_col", [40, 700, 2900])
+def test_big_singular_column(gelim, cuda, zero_col):
+    """A zero column inside a leaf (40, 700) or inside the tail system (2900):
+    info is the 1-based column of the first zero pivot."""
+    n = 3000
+    aug = gelim.random_system(n, seed=5, device=cuda)
+    aug[:, zero_col] = 0.0
+    s = gelim.GaussSolver(n, backend="hip", device=cuda)
+    s.solve(aug)
+    assert s.info() == zero_col + 1
+
+
+def test_big_graph_replay_two_plans(gelim, cuda):
+    n = 2600
+    s1 = gelim.GaussSolver(n, backend="hip", device=cuda)
+    s2 = gelim.GaussSolver(n, backend="hip", device=cuda)
+    a1 = gelim.random_system(n, seed=1, device=cuda)
+    a2 = gelim.random_system(n, seed=2, device=cuda)
+    x1 = s1.solve(a1).clone()
+    x2 = s2.solve(a2).clone()
+    for _ in range(3):  # interleaved replays of both graphs
+        assert torch.equal(s1.solve(a1), x1)
+        assert torch.equal(s2.solve(a2), x2)
+    torch.cuda.synchronize()
+    for x, a in ((x1, a1), (x2, a2)):
+        assert torch.allclose(x, torch.linalg.solve(a[:, :n], a[:, n]), rtol=1e-8, atol=1e-8 * n)
+
+
+@pytest.mark.parametrize("name", [k for k in GOLDEN_ERROR if k in ("orsreg_1", "sherman5", "saylr4", "sherman3")])
+def test_big_golden_errors(gelim, cuda, name):
+    """The four reference matrices with n > 2048 now run the wide-panel
+    engine: same accuracy class as the reference's fp64 OpenMP program."""
+    A = gelim.utils.io.load_fixture(name)
+    n = A.shape[0]
+    aug = gelim.augment_with_rhs(A).to(cuda)
+    x = gelim.GaussSolver(n, backend="hip", device=cuda).solve(aug, check=True)
+    err = gelim.ops.gauss.error_metric(x)
+    assert err <= max(20 * GOLDEN_ERROR[name], 1e-14), (name, err)
+
+
+def test_memplus_blocked(gelim, cuda):
+    """memplus (n = 17758, the one reference matrix the reference never
+    benchmarked): solved by the blocked engine on one GPU.  No golden value
+    exists, so the oracle is rocSOLVER's fp64 solve of the same system
+    (parity unpinned against the reference)."""
+    A = gelim.utils.io.load_fixture("memplus")
+    n = A.shape[0]
+    aug = gelim.augment_with_rhs(A).to(cuda)
+    del A
+    x = gelim.GaussSolver(n, backend="hip", device=cuda).solve(aug, check=True)
+    err = gelim.ops.gauss.error_metric(x)
+    xr = torch.linalg.solve(aug[:, :n], aug[:, n])
+    err_ref = gelim.ops.gauss.error_metric(xr)
+    assert err <= max(20 * err_ref, 1e-12), (err, err_ref)

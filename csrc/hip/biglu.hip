@@ -51,12 +51,10 @@ namespace gelim {
 namespace big {
 namespace {
 
-constexpr int NT = 256;            // leaf workgroup: 4 waves, one per SIMD
-constexpr int kWaves = NT / 64;
 constexpr int LW = 32;             // leaf width
 constexpr int R = 4;               // rows per lane
-constexpr int kRowsPerWg = NT * R;
-constexpr int kMaxP = 64;          // leaf workgroups (m <= 65536)
+constexpr int kRowsPerWave = 64 * R;
+constexpr int kMaxW = 128;         // participating waves (m <= 32768)
 constexpr int kAuxSc1 = 16;        // buffer-op aux: sc1
 constexpr unsigned long long kSpinTicks = 20000000ull;  // 200 ms at 100 MHz
 
@@ -77,6 +75,7 @@ __device__ __forceinline__ unsigned hi32(double x) { return (unsigned)((uint64_t
 __device__ __forceinline__ double mkd(unsigned lo, unsigned hi) {
   return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
 }
+__device__ __forceinline__ uint64_t u64of(unsigned lo, unsigned hi) { return ((uint64_t)hi << 32) | lo; }
 
 // 1/p: v_rcp_f64 + two Newton steps (within an ulp of the IEEE quotient)
 __device__ __forceinline__ double recip(double p) {
@@ -91,39 +90,48 @@ __device__ __forceinline__ T opq(T x) {
   return x;
 }
 
+// Exchange workspace: per (set, parity, participant) one key granule and
+// the candidate row as LW data-tagged granules.
+struct Xchg {
+  u32x4* key;   // [2 sets][2 parities][kMaxW] {key lo, key hi, row, seq}
+  u32x4* row;   // [2 sets][2 parities][kMaxW][LW] {value lo, value hi, row, seq}
+};
+constexpr size_t kKeyBytes = (size_t)2 * 2 * kMaxW * 16;
+constexpr size_t kRowBytes = (size_t)2 * 2 * kMaxW * LW * 16;
+
 struct LeafArgs {
   double* A;         // leaf top-left: row c0, column c0 of the system
   int64_t lda;
   int m;             // rows n - c0 (>= LW)
   int col0;          // c0 (absolute column / row of the leaf's diagonal)
-  int P;             // workgroups
+  int P;             // participating waves (one per workgroup)
   int set;           // granule set used by this launch (leaf counter & 1)
   int* ipiv;         // ipiv[c0 + J] = absolute row swapped with row c0 + J
   int* pairs;        // [0] = count, then (dst, src) rows relative to c0
   int* info;         // [0] 1 + first zero-pivot column (kept if set), [1] hand-off error
-  u32x4* gran;       // [2 sets][2 parities][kMaxP] {key lo, key hi, row, seq}
-  double* rows;      // [2 parities][kMaxP][LW] published candidate rows
+  Xchg x;
+  unsigned long long* stamps;  // diagnostics (null in production): [P][LW][8] shader clocks
 };
+
+// Diagnostic phase stamp of column J (lane 0 of every participant):
+// 0 start, 1 arg-max done, 2 published, 3 key sweep ready, 4 pivot row
+// loaded, 5 pivot row in LDS, 6 update done, 7 key sweeps + 256 * row loads
+__device__ __forceinline__ void lstamp(const LeafArgs& g, int J, int k, unsigned long long v) {
+  if (g.stamps != nullptr && threadIdx.x == 0) g.stamps[((int64_t)blockIdx.x * LW + J) * 8 + k] = v;
+}
 
 struct alignas(16) LeafLds {
-  double cand[2][kWaves][LW];  // each wave's winning row, parity-buffered
-  u32x4 ckey[2][kWaves];       // {key lo, key hi, row, -}
-  double prow[kWaves][LW];     // each wave's private copy of the pivot row
-  int dest[kRowsPerWg];        // final row of a moved local row (-1: unmoved)
-  int abort_flag;
+  double cand[LW];             // this wave's candidate row on its way out
+  double prow[LW];             // the pivot row
+  int dest[kRowsPerWave];      // final row of a moved local row (-1: unmoved)
 };
 
-// ---- the LAPACK interchange replay, one table per wave -----------------------
+// ---- the LAPACK interchange replay, in the lanes of the wave -----------------
 // Lane e < cnt holds one displaced row: trow (row index, relative to c0) now
 // at position tpos.  Rows not in the table sit at their own index.
 struct Table {
   int trow, tpos, cnt;
 };
-
-__device__ __forceinline__ int table_pos_of(const Table& tb, int row, int lane) {
-  const uint64_t m = __ballot(lane < tb.cnt && tb.trow == row);
-  return m ? __builtin_amdgcn_readlane(tb.tpos, __ffsll((long long)m) - 1) : row;
-}
 
 __device__ __forceinline__ int table_row_at(const Table& tb, int pos, int lane) {
   const uint64_t m = __ballot(lane < tb.cnt && tb.tpos == pos);
@@ -152,30 +160,33 @@ __device__ __forceinline__ int table_swap(Table& tb, int J, int pr, int lane) {
   return q;
 }
 
-template <int MODE>
-__device__ __forceinline__ uint64_t cand_key(double v, bool is_diag, bool ok) {
-  return dev::pivot_ukey_t<MODE>(v, is_diag, ok);
+// Wave arg-max of (key, row): largest key, lowest row; returns the winning
+// lane (-1 when every key is 0).  DPP max of the high word + one ballot; the
+// exact 64-bit / lowest-row resolution only on high-word ties.
+__device__ __forceinline__ int wave_argmax_lane(uint64_t k, unsigned row) {
+  const unsigned h = (unsigned)(k >> 32);
+  const unsigned hm = dev::wave_max_u32(h);
+  const bool c1 = h == hm && k != 0;
+  const uint64_t hold = __ballot(c1);
+  if (hold == 0) return -1;
+  if (__popcll(hold) == 1) return __ffsll((long long)hold) - 1;
+  const unsigned lm = dev::wave_max_u32(c1 ? (unsigned)k : 0u);
+  const bool c2 = c1 && (unsigned)k == lm;
+  const unsigned mr = dev::wave_min_u32(c2 ? row : 0xffffffffu);
+  return __ffsll((long long)__ballot(c2 && row == mr)) - 1;
 }
 
-// put one register row into LDS (the empty asm keeps the per-slot branches
-// from being merged into a dynamically indexed access)
-__device__ __forceinline__ void put_row(double* dst, const double (&row)[LW]) {
-#pragma unroll
-  for (int c = 0; c < LW; c += 2) {
-    const double x = row[c], y = row[c + 1];
-    asm volatile("" ::"v"(x), "v"(y));
-    *reinterpret_cast<double2*>(dst + c) = make_double2(x, y);
-  }
-}
-
-template <int MODE>
+template <int MODE, int NKK>
 struct Leaf {
+  // one column J of the leaf (compile time); false: hand-off aborted
   template <int J>
   static __device__ __forceinline__ bool col(double (&a)[R][LW], bool (&live)[R], LeafLds& sh, Table& tb,
-                                             const LeafArgs& g, int t, int lane, int wave, int base) {
+                                             const LeafArgs& g, int lane, int base) {
     constexpr int par = J & 1;
-    t = opq(t);
     lane = opq(lane);
+    const unsigned seq = (unsigned)(J + 1);
+    const int slot = (g.set * 2 + par) * kMaxW;
+    lstamp(g, J, 0, __builtin_amdgcn_s_memtime());
     // 1. this lane's candidate: best live row (rows grow with the slot, so a
     //    strict '>' keeps the lowest row on ties)
     const int diag = MODE == 0 ? table_row_at(tb, J, lane) : -1;
@@ -183,175 +194,207 @@ struct Leaf {
     int bi = 0;
 #pragma unroll
     for (int i = 0; i < R; ++i) {
-      const int r = base + t + NT * i;
-      const uint64_t k = cand_key<MODE>(a[i][J], r == diag, live[i]);
+      const int r = base + lane + 64 * i;
+      const uint64_t k = dev::pivot_ukey_t<MODE>(a[i][J], r == diag, live[i]);
       const bool c = k > bk;
       bk = c ? k : bk;
       bi = c ? i : bi;
     }
-    const unsigned brow = (unsigned)(base + t + NT * bi);
-    // 2. wave arg-max; the wave's winner parks its row in LDS
-    const uint64_t wk = dev::wave_max_u64(bk);
-    unsigned wrow = 0xffffffffu;
-    if (wk != 0) {
-      const uint64_t hold = __ballot(bk == wk);
-      int wl;
-      if (__popcll(hold) == 1) {
-        wl = __ffsll((long long)hold) - 1;
-      } else {
-        const unsigned mr = dev::wave_min_u32(bk == wk ? brow : 0xffffffffu);
-        wl = __ffsll((long long)__ballot(bk == wk && brow == mr)) - 1;
-      }
-      wrow = (unsigned)__builtin_amdgcn_readlane((int)brow, wl);
-      const int wbi = __builtin_amdgcn_readlane(bi, wl);
-      if (lane == wl) {
+    const unsigned brow = (unsigned)(base + lane + 64 * bi);
+    // 2. this wave's candidate
+    const int wl = wave_argmax_lane(bk, brow);
+    lstamp(g, J, 1, __builtin_amdgcn_s_memtime());
+    // 3. publish: the winning lane stores its row as LW data-tagged granules
+    //    {value, row, seq}, then its key granule; no drain and no flag -- a
+    //    reader trusts a granule exactly when its seq matches (16-byte sc1
+    //    store / load, untorn on gfx950)
+    {
+      const __amdgpu_buffer_rsrc_t rk = rsrc(g.x.key + slot + blockIdx.x, 16);
+      if (wl >= 0) {
+        // the winner's row goes through LDS (the winning lane writes it,
+        // lane c reads element c) so the LW granules leave in ONE 32-lane
+        // store instead of LW single-lane ones (each of which stalls the
+        // wave for a write-through round trip).  The slot is wave-uniform
+        // (readlane): every slot branch is a uniform one over compile-time
+        // indices, so the register panel is never dynamically indexed.
+        const int wbi = __builtin_amdgcn_readlane(bi, wl);
+        const unsigned wrow = (unsigned)__builtin_amdgcn_readlane((int)brow, wl);
 #pragma unroll
         for (int i = 0; i < R; ++i)
-          if (wbi == i) put_row(&sh.cand[par][wave][0], a[i]);
-      }
-    }
-    if (lane == 0) sh.ckey[par][wave] = u32x4{(unsigned)wk, (unsigned)(wk >> 32), wrow, 0u};
-    __syncthreads();
-
-    // 3. workgroup candidate (wave 0 publishes it) and the global exchange
-    {
-      const u32x4 kk = sh.ckey[par][lane & (kWaves - 1)];
-      const uint64_t key = ((uint64_t)kk.y << 32) | kk.x;
-      const bool in = lane < kWaves;
-      const uint64_t gk = dev::wave_max_u64(in ? key : 0);
-      const unsigned gr = dev::wave_min_u32(in && key == gk ? kk.z : 0xffffffffu);
-      const int q = __ffsll((long long)__ballot(in && key == gk && kk.z == gr)) - 1;
-      if (wave == 0) {
-        const __amdgpu_buffer_rsrc_t rr = rsrc(g.rows + ((int64_t)par * kMaxP + blockIdx.x) * LW, LW * 8);
-        if (lane < LW / 2) {
-          const double2 v = *reinterpret_cast<const double2*>(&sh.cand[par][q][2 * lane]);
-          __builtin_amdgcn_raw_buffer_store_b128(u32x4{lo32(v.x), hi32(v.x), lo32(v.y), hi32(v.y)}, rr, lane * 16, 0,
+          if (wbi == i && lane == wl) {
+#pragma unroll
+            for (int c = 0; c < LW; c += 2) {
+              const double x = a[i][c], y = a[i][c + 1];
+              asm volatile("" ::"v"(x), "v"(y));
+              *reinterpret_cast<double2*>(&sh.cand[c]) = make_double2(x, y);
+            }
+          }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // wave-local LDS hand-off
+        if (lane < LW) {
+          const double x = sh.cand[lane];
+          const __amdgpu_buffer_rsrc_t rr = rsrc(g.x.row + (int64_t)(slot + blockIdx.x) * LW, LW * 16);
+          __builtin_amdgcn_raw_buffer_store_b128(u32x4{lo32(x), hi32(x), wrow, seq}, rr, lane * 16, 0, kAuxSc1);
+        }
+        if (lane == wl)
+          __builtin_amdgcn_raw_buffer_store_b128(u32x4{(unsigned)bk, (unsigned)(bk >> 32), brow, seq}, rk, 0, 0,
                                                  kAuxSc1);
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (lane == 0) {
-          const __amdgpu_buffer_rsrc_t rg = rsrc(g.gran + ((g.set * 2 + par) * kMaxP + blockIdx.x), 16);
-          __builtin_amdgcn_raw_buffer_store_b128(u32x4{(unsigned)gk, (unsigned)(gk >> 32), gr, (unsigned)(J + 1)}, rg, 0,
-                                                 0, kAuxSc1);
-        }
+      } else if (lane == 0) {  // no live row here: an empty candidate
+        __builtin_amdgcn_raw_buffer_store_b128(u32x4{0u, 0u, 0xffffffffu, seq}, rk, 0, 0, kAuxSc1);
       }
     }
-    // every wave polls the P granules of column J (lane p <-> workgroup p)
-    const __amdgpu_buffer_rsrc_t rg = rsrc(g.gran + (g.set * 2 + par) * kMaxP, kMaxP * 16);
-    const int pl = lane < g.P ? lane : 0;
-    u32x4 gv = __builtin_amdgcn_raw_buffer_load_b128(rg, pl * 16, 0, kAuxSc1);
-    if (__ballot(lane < g.P && gv.w != (unsigned)(J + 1)) != 0) {
-      const unsigned long long t0 = rtc();
-      for (;;) {
-        gv = __builtin_amdgcn_raw_buffer_load_b128(rg, pl * 16, 0, kAuxSc1);
-        if (__ballot(lane < g.P && gv.w != (unsigned)(J + 1)) == 0) break;
-        if (__hip_atomic_load(g.info + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return false;
-        if (rtc() - t0 > kSpinTicks) {
+    lstamp(g, J, 2, __builtin_amdgcn_s_memtime());
+    // 4. key sweep: lane p (+ 64 k) reads participant p's key; all loads in
+    //    flight at once (unconditional, clamped: a predicated load is a
+    //    branch with its own vmcnt(0) wait)
+    const __amdgpu_buffer_rsrc_t rks = rsrc(g.x.key + slot, kMaxW * 16);
+    u32x4 kv[NKK];
+    unsigned long long t0 = 0;
+    int sweeps = 0;
+    for (int it = 0;; ++it) {
+#pragma unroll
+      for (int k = 0; k < NKK; ++k) kv[k] = __builtin_amdgcn_raw_buffer_load_b128(rks, min(k * 64 + lane, g.P - 1) * 16, 0, kAuxSc1);
+      bool ready = true;
+#pragma unroll
+      for (int k = 0; k < NKK; ++k) ready = ready && kv[k].w == seq;
+      if (__ballot(!ready) == 0) {
+        sweeps = it + 1;
+        break;
+      }
+      if ((it & 63) == 63) {  // abort / timeout checks every 64 sweeps (each is a round trip)
+        if (t0 == 0) t0 = rtc();
+        else if (rtc() - t0 > kSpinTicks) {
           __hip_atomic_store(g.info + 1, 5, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           return false;
         }
+        if (__hip_atomic_load(g.info + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return false;
       }
     }
-    // global winner: largest key, lowest row
-    const uint64_t key = lane < g.P ? (((uint64_t)gv.y << 32) | gv.x) : 0;
-    const uint64_t gk = dev::wave_max_u64(key);
-    const unsigned pr = dev::wave_min_u32(lane < g.P && key == gk ? gv.z : 0xffffffffu);
-    const int pw = __ffsll((long long)__ballot(lane < g.P && key == gk && gv.z == pr)) - 1;
-    // pivot row -> this wave's private LDS line
-    {
-      const __amdgpu_buffer_rsrc_t rr = rsrc(g.rows + ((int64_t)par * kMaxP + pw) * LW, LW * 8);
-      if (lane < LW / 2) {
-        const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rr, lane * 16, 0, kAuxSc1);
-        *reinterpret_cast<double2*>(&sh.prow[wave][2 * lane]) = make_double2(mkd(v.x, v.y), mkd(v.z, v.w));
-      }
+    lstamp(g, J, 3, __builtin_amdgcn_s_memtime());
+    // 5. global winner (largest key, lowest row); lanes past P hold clamped
+    //    duplicates, which never change the arg-max
+    uint64_t key = u64of(kv[0].x, kv[0].y);
+    unsigned krow = kv[0].z;
+    int kp = lane;
+#pragma unroll
+    for (int k = 1; k < NKK; ++k) {
+      const uint64_t kk = u64of(kv[k].x, kv[k].y);
+      const bool c = kk > key || (kk == key && kk != 0 && kv[k].z < krow);
+      key = c ? kk : key;
+      krow = c ? kv[k].z : krow;
+      kp = c ? min(k * 64 + lane, g.P - 1) : kp;
     }
-    // interchange replay (identical in every wave); wave 0 of workgroup 0
-    // records the LAPACK pivot
+    kp = min(kp, g.P - 1);
+    const int wlw = wave_argmax_lane(key, krow);
+    const int pw = __builtin_amdgcn_readlane(kp, wlw);
+    const unsigned pr = (unsigned)__builtin_amdgcn_readlane((int)krow, wlw);
+    // 6. the winner's row: lanes c < LW read its granules until they are
+    //    current (they were stored before its key, but nothing orders them)
+    const __amdgpu_buffer_rsrc_t rrs = rsrc(g.x.row + (int64_t)(slot + pw) * LW, LW * 16);
+    u32x4 rv;
+    int rl = 0;
+    for (;; ++rl) {
+      rv = __builtin_amdgcn_raw_buffer_load_b128(rrs, (lane & (LW - 1)) * 16, 0, kAuxSc1);
+      if (__ballot(rv.w != seq) == 0) break;
+      if ((rl & 63) == 63 && __hip_atomic_load(g.info + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0)
+        return false;
+    }
+    lstamp(g, J, 4, __builtin_amdgcn_s_memtime());
+    if (lane < LW) sh.prow[lane] = mkd(rv.x, rv.y);
+    // interchange replay; participant 0 records the LAPACK pivot
     const int qpos = table_swap(tb, J, (int)pr, lane);
-    if (blockIdx.x == 0 && wave == 0 && lane == 0) g.ipiv[g.col0 + J] = g.col0 + qpos;
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // own LDS line written (wave-local)
+    if (blockIdx.x == 0 && lane == 0) g.ipiv[g.col0 + J] = g.col0 + qpos;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the pivot row is in LDS (wave-local)
+    lstamp(g, J, 5, __builtin_amdgcn_s_memtime());
+    lstamp(g, J, 7, (unsigned long long)sweeps + 256ull * (rl + 1));
 
-    // 4. multipliers and the rank-1 update of columns J+1.. (next column first)
-    const double* u = &sh.prow[wave][0];
-    const double pv = u[J];
+    // 7. multipliers and the rank-1 update of columns J+1..
+    const double pv = sh.prow[J];
     const bool zero = !(pv != 0.0);
     const double rinv = zero ? 0.0 : recip(pv);
-    if (zero && blockIdx.x == 0 && t == 0 && g.info[0] == 0) atomicCAS(g.info, 0, g.col0 + J + 1);
+    if (zero && blockIdx.x == 0 && lane == 0 && g.info[0] == 0) atomicCAS(g.info, 0, g.col0 + J + 1);
     double l[R];
 #pragma unroll
     for (int i = 0; i < R; ++i) {
-      live[i] = live[i] && (base + t + NT * i != (int)pr);
+      live[i] = live[i] && (base + lane + 64 * i != (int)pr);
       l[i] = live[i] ? a[i][J] * rinv : 0.0;
       a[i][J] = live[i] ? l[i] : a[i][J];
     }
 #pragma unroll
     for (int c = J + 1; c < LW; ++c) {
-      const double uc = u[c];
+      const double uc = sh.prow[c];
 #pragma unroll
       for (int i = 0; i < R; ++i) a[i][c] = fma(-l[i], uc, a[i][c]);
+    }
+    if (g.stamps != nullptr) {
+      asm volatile("" ::"v"(a[R - 1][LW - 1]));
+      lstamp(g, J, 6, __builtin_amdgcn_s_memtime());
     }
     return true;
   }
 
   template <int... J>
   static __device__ __forceinline__ bool factor(double (&a)[R][LW], bool (&live)[R], LeafLds& sh, Table& tb,
-                                                const LeafArgs& g, int t, int lane, int wave, int base,
+                                                const LeafArgs& g, int lane, int base,
                                                 std::integer_sequence<int, J...>) {
-    return (col<J>(a, live, sh, tb, g, t, lane, wave, base) && ...);
+    return (col<J>(a, live, sh, tb, g, lane, base) && ...);
   }
 };
 
-template <int MODE>
-__global__ __launch_bounds__(NT, 1) void leaf_kernel(LeafArgs g) {
+// One wave per workgroup; participant w = blockIdx.x owns rows
+// [256 w, 256 w + 256) of the leaf, lane l the rows 256 w + l + 64 i.
+template <int MODE, int NKK>
+__global__ __launch_bounds__(64, 1) void leaf_kernel(LeafArgs g) {
   __shared__ LeafLds sh;
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  const int base = blockIdx.x * kRowsPerWg;
+  const int lane = threadIdx.x;
+  const int base = blockIdx.x * kRowsPerWave;
   double a[R][LW];
   bool live[R];
 #pragma unroll
   for (int i = 0; i < R; ++i) {
-    const int r = base + t + NT * i;
+    const int r = base + lane + 64 * i;
     live[i] = r < g.m;
     const double2* src = reinterpret_cast<const double2*>(g.A + (int64_t)min(r, g.m - 1) * g.lda);
 #pragma unroll
     for (int c = 0; c < LW; c += 2) {
-      const double2 v = src[c / 2];
-      a[i][c] = v.x;
-      a[i][c + 1] = v.y;
+      const double2 x = src[c / 2];
+      a[i][c] = x.x;
+      a[i][c + 1] = x.y;
     }
   }
 #pragma unroll
-  for (int i = 0; i < R; ++i) sh.dest[t + NT * i] = -1;
+  for (int i = 0; i < R; ++i) sh.dest[lane + 64 * i] = -1;
   Table tb{0, 0, 0};
-  if (!Leaf<MODE>::factor(a, live, sh, tb, g, t, lane, wave, base, std::make_integer_sequence<int, LW>{}))
-    return;
+  if (!Leaf<MODE, NKK>::factor(a, live, sh, tb, g, lane, base, std::make_integer_sequence<int, LW>{})) return;
 
-  // net row movement: wave 0 of workgroup 0 publishes it; every workgroup
-  // maps its own moved rows to their final positions
-  if (wave == 0) {
-    if (blockIdx.x == 0) {
-      if (lane < tb.cnt) {
-        g.pairs[1 + 2 * lane] = tb.tpos;
-        g.pairs[2 + 2 * lane] = tb.trow;
-      }
-      if (lane == 0) g.pairs[0] = tb.cnt;
+  // net row movement (participant 0 publishes it); every participant maps
+  // its own moved rows to their final positions and writes its rows there
+  if (blockIdx.x == 0) {
+    if (lane < tb.cnt) {
+      g.pairs[1 + 2 * lane] = tb.tpos;
+      g.pairs[2 + 2 * lane] = tb.trow;
     }
-    if (lane < tb.cnt && tb.trow >= base && tb.trow < base + kRowsPerWg) sh.dest[tb.trow - base] = tb.tpos;
+    if (lane == 0) g.pairs[0] = tb.cnt;
   }
-  __syncthreads();
+  if (lane < tb.cnt && tb.trow >= base && tb.trow < base + kRowsPerWave) sh.dest[tb.trow - base] = tb.tpos;
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
   for (int i = 0; i < R; ++i) {
-    const int r = base + t + NT * i;
+    const int r = base + lane + 64 * i;
     if (r < g.m) {
-      const int d = sh.dest[t + NT * i];
+      const int d = sh.dest[lane + 64 * i];
       double2* dst = reinterpret_cast<double2*>(g.A + (int64_t)(d < 0 ? r : d) * g.lda);
 #pragma unroll
       for (int c = 0; c < LW; c += 2) dst[c / 2] = make_double2(a[i][c], a[i][c + 1]);
     }
   }
-  // clear the other granule set for the next leaf launch (this launch's
-  // predecessor used it and has finished)
-  if (blockIdx.x == 0 && t < 2 * kMaxP) g.gran[((g.set ^ 1) * 2) * kMaxP + t] = u32x4{0u, 0u, 0u, 0u};
+  // clear this participant's granules of the other set for the next leaf
+  // launch (its predecessor used that set and has finished; within one solve
+  // the number of participants never grows, and the driver zeroes the whole
+  // exchange area before every solve)
+  const int o = (g.set ^ 1) * 2 * kMaxW;
+  if (lane < 2) g.x.key[o + lane * kMaxW + blockIdx.x] = u32x4{0u, 0u, 0u, 0u};
+  for (int e = lane; e < 2 * LW; e += 64)
+    g.x.row[(int64_t)(o + (e / LW) * kMaxW + blockIdx.x) * LW + (e % LW)] = u32x4{0u, 0u, 0u, 0u};
 }
 
 // ---- row interchanges for the other columns + TRSM of a leaf's U rows -----
@@ -369,12 +412,12 @@ __global__ __launch_bounds__(NT, 1) void leaf_kernel(LeafArgs g) {
 // columns right of the panel).  Updating those columns any earlier would mix
 // rows that carry a leaf's update with rows that do not when a later leaf
 // swaps rows across the panel boundary.
-constexpr int kSwThreads = 256;
+constexpr int kSwThreads = 64;  // one wave per workgroup: one CU per 64 columns
 
 struct SwapArgs {
   double* A;
   int64_t lda;
-  int c0, lend, rbeg, rend, trsm_end;
+  int c0, lend, rbeg, rend, trsm_end, nrows;
   const int* pairs;
 };
 
@@ -384,11 +427,25 @@ __global__ __launch_bounds__(kSwThreads) void laswp_trsm_kernel(SwapArgs g) {
   __shared__ int sp[1 + 4 * LW];
   const int t = threadIdx.x;
   const int64_t lda = g.lda;
+  // only the strictly lower part is ever read: copy the whole block, no
+  // select (a select right after each load makes the compiler wait on it)
   for (int e = t; e < LW * LW; e += kSwThreads) {
     const int r = e / LW, c = e % LW;
-    sL[r][c] = c < r ? g.A[(int64_t)r * lda + g.c0 + c] : 0.0;
+    sL[r][c] = g.A[(int64_t)r * lda + g.c0 + c];
   }
-  if (t < 1 + 4 * LW) sp[t] = g.pairs && (t == 0 || t <= 2 * g.pairs[0]) ? g.pairs[t] : 0;
+  // (strided: the workgroup is narrower than the list) entries outside
+  // [0, nrows) are dropped, so a corrupt list can never address past the
+  // system
+  const int np_in = g.pairs ? min(g.pairs[0], 2 * LW) : 0;
+  for (int e = t; e < 1 + 4 * LW; e += kSwThreads) {
+    int v = 0;
+    if (e > 0 && e <= 2 * np_in) {
+      v = g.pairs[e];
+      v = (v >= 0 && v < g.nrows) ? v : -1;
+    }
+    sp[e] = v;
+  }
+  if (t == 0) sp[0] = np_in;
   __syncthreads();
   const int np = sp[0];
   const int nleft = g.lend, nright = g.rend - g.rbeg;
@@ -399,19 +456,26 @@ __global__ __launch_bounds__(kSwThreads) void laswp_trsm_kernel(SwapArgs g) {
   double* col = g.A + c;
   double gsrc[2 * LW];
 #pragma unroll
-  for (int e = 0; e < 2 * LW; ++e) gsrc[e] = e < np ? col[(int64_t)sp[2 + 2 * e] * lda] : 0.0;
+  for (int e = 0; e < 2 * LW; ++e) {
+    // unconditional load of a clamped row and no select: entries past np are
+    // never stored.  (A predicated load, or a select right behind the load,
+    // makes the compiler wait for each one: 64 serial round trips.)
+    gsrc[e] = col[(int64_t)max(sp[2 + 2 * e], 0) * lda];
+  }
   if (!right || c >= g.trsm_end) {
 #pragma unroll
-    for (int e = 0; e < 2 * LW; ++e)
-      if (e < np) col[(int64_t)sp[1 + 2 * e] * lda] = gsrc[e];
+    for (int e = 0; e < 2 * LW; ++e) {
+      const int d = sp[1 + 2 * e];
+      if (e < np && d >= 0 && sp[2 + 2 * e] >= 0) col[(int64_t)d * lda] = gsrc[e];
+    }
     return;
   }
 #pragma unroll
   for (int j = 0; j < LW; ++j) xs[j][t] = col[(int64_t)j * lda];
 #pragma unroll
   for (int e = 0; e < 2 * LW; ++e) {
-    if (e < np) {
-      const int d = sp[1 + 2 * e];
+    const int d = sp[1 + 2 * e];
+    if (e < np && d >= 0 && sp[2 + 2 * e] >= 0) {
       if (d < LW) xs[d][t] = gsrc[e];
       else col[(int64_t)d * lda] = gsrc[e];
     }
@@ -460,13 +524,13 @@ __global__ void fold_info_kernel(int* __restrict__ info, const int* __restrict__
 
 }  // namespace
 
-size_t workspace_bytes() { return (size_t)2 * 2 * kMaxP * 16 + (size_t)2 * kMaxP * LW * 8; }
+size_t workspace_bytes() { return kKeyBytes + kRowBytes; }
 int leaf_width() { return LW; }
-int64_t max_rows() { return (int64_t)kMaxP * kRowsPerWg; }
+int64_t max_rows() { return (int64_t)kMaxW * kRowsPerWave; }
 
 // Factor the m x LW leaf at A (row/column c0 of the system) in place.
 int leaf_factor(double* A, int64_t lda, int64_t m, int64_t c0, int mode, int* ipiv, int* pairs, int* info,
-                void* ws, int set, hipStream_t s) {
+                void* ws, int set, hipStream_t s, unsigned long long* stamps) {
   if (m < LW || m > max_rows()) return GELIM_FAIL(GELIM_E_ARG, "leaf: m out of range");
   if ((reinterpret_cast<uintptr_t>(A) & 15) || (lda & 1)) return GELIM_FAIL(GELIM_E_ARG, "leaf: alignment");
   LeafArgs a{};
@@ -474,17 +538,22 @@ int leaf_factor(double* A, int64_t lda, int64_t m, int64_t c0, int mode, int* ip
   a.lda = lda;
   a.m = (int)m;
   a.col0 = (int)c0;
-  a.P = (int)((m + kRowsPerWg - 1) / kRowsPerWg);
+  a.P = (int)((m + kRowsPerWave - 1) / kRowsPerWave);
   a.set = set & 1;
   a.ipiv = ipiv;
   a.pairs = pairs;
   a.info = info;
-  a.gran = static_cast<u32x4*>(ws);
-  a.rows = reinterpret_cast<double*>(static_cast<char*>(ws) + (size_t)2 * 2 * kMaxP * 16);
-  if (mode == GELIM_PIVOT_PARTIAL)
-    hipLaunchKernelGGL(leaf_kernel<1>, dim3((unsigned)a.P), dim3(NT), 0, s, a);
-  else
-    hipLaunchKernelGGL(leaf_kernel<0>, dim3((unsigned)a.P), dim3(NT), 0, s, a);
+  a.x.key = static_cast<u32x4*>(ws);
+  a.x.row = reinterpret_cast<u32x4*>(static_cast<char*>(ws) + kKeyBytes);
+  a.stamps = stamps;
+#define GELIM_LEAF(NKK)                                                                          \
+  if (mode == GELIM_PIVOT_PARTIAL)                                                               \
+    hipLaunchKernelGGL((leaf_kernel<1, NKK>), dim3((unsigned)a.P), dim3(64), 0, s, a);           \
+  else                                                                                           \
+    hipLaunchKernelGGL((leaf_kernel<0, NKK>), dim3((unsigned)a.P), dim3(64), 0, s, a)
+  if (a.P <= 64) GELIM_LEAF(1);
+  else GELIM_LEAF(2);
+#undef GELIM_LEAF
   HIP_TRY(hipGetLastError());
   return GELIM_OK;
 }
@@ -493,10 +562,11 @@ int leaf_factor(double* A, int64_t lda, int64_t m, int64_t c0, int mode, int* ip
 // [rbeg, rend) of rows [c0, ...), TRSM of rows [c0, c0 + LW) on the right
 // columns below trsm_end.  A: row c0, column 0.
 int laswp_trsm(double* A, int64_t lda, int64_t c0, int64_t lend, int64_t rbeg, int64_t rend, int64_t trsm_end,
-               const int* pairs, hipStream_t s) {
+               int64_t nrows, const int* pairs, hipStream_t s) {
   const int64_t cols = lend + std::max<int64_t>(0, rend - rbeg);
   if (cols <= 0) return GELIM_OK;
-  SwapArgs a{A, lda, (int)c0, (int)lend, (int)rbeg, (int)rend, (int)trsm_end, pairs};
+  if (nrows < LW) return GELIM_FAIL(GELIM_E_ARG, "laswp_trsm: fewer rows than the leaf width");
+  SwapArgs a{A, lda, (int)c0, (int)lend, (int)rbeg, (int)rend, (int)trsm_end, (int)nrows, pairs};
   hipLaunchKernelGGL(laswp_trsm_kernel, dim3((unsigned)((cols + kSwThreads - 1) / kSwThreads)), dim3(kSwThreads), 0,
                      s, a);
   HIP_TRY(hipGetLastError());
@@ -529,7 +599,7 @@ extern "C" int gelim_gpu_leaf_factor(double* dA, int64_t lda, int64_t m, int64_t
   void* ws = nullptr;
   HIP_TRY(hipMallocAsync(&ws, gelim::big::workspace_bytes(), s));
   HIP_TRY(hipMemsetAsync(ws, 0, gelim::big::workspace_bytes(), s));
-  const int rc = gelim::big::leaf_factor(dA, lda, m, c0, pivot, dipiv, dpairs, dinfo, ws, 0, s);
+  const int rc = gelim::big::leaf_factor(dA, lda, m, c0, pivot, dipiv, dpairs, dinfo, ws, 0, s, nullptr);
   HIP_TRY(hipFreeAsync(ws, s));
   return rc;
 }
@@ -538,12 +608,29 @@ extern "C" int gelim_gpu_leaf_factor(double* dA, int64_t lda, int64_t m, int64_t
 // before the first leaf) and the leaf counter's granule set
 extern "C" int gelim_gpu_leaf_factor_ws(double* dA, int64_t lda, int64_t m, int64_t c0, int pivot, int32_t* dipiv,
                                         int32_t* dpairs, int32_t* dinfo, void* ws, int set, void* stream) {
-  return gelim::big::leaf_factor(dA, lda, m, c0, pivot, dipiv, dpairs, dinfo, ws, set, (hipStream_t)stream);
+  return gelim::big::leaf_factor(dA, lda, m, c0, pivot, dipiv, dpairs, dinfo, ws, set, (hipStream_t)stream, nullptr);
+}
+
+// Diagnostic: one leaf with phase stamps (stamps: P * 32 * 8 u64).
+extern "C" int gelim_debug_leaf_stamps(double* dA, int64_t lda, int64_t m, void* ws, unsigned long long* stamps,
+                                       void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  int *ipiv = nullptr, *pairs = nullptr, *info = nullptr;
+  HIP_TRY(hipMallocAsync((void**)&ipiv, 64 * 4, s));
+  HIP_TRY(hipMallocAsync((void**)&pairs, 256 * 4, s));
+  HIP_TRY(hipMallocAsync((void**)&info, 16, s));
+  HIP_TRY(hipMemsetAsync(info, 0, 16, s));
+  HIP_TRY(hipMemsetAsync(ws, 0, gelim::big::workspace_bytes(), s));
+  const int rc = gelim::big::leaf_factor(dA, lda, m, 0, GELIM_PIVOT_PARTIAL, ipiv, pairs, info, ws, 0, s, stamps);
+  HIP_TRY(hipFreeAsync(ipiv, s));
+  HIP_TRY(hipFreeAsync(pairs, s));
+  HIP_TRY(hipFreeAsync(info, s));
+  return rc;
 }
 
 extern "C" int64_t gelim_gpu_leaf_workspace_bytes(void) { return (int64_t)gelim::big::workspace_bytes(); }
 
 extern "C" int gelim_gpu_laswp_trsm(double* dA, int64_t lda, int64_t c0, int64_t lend, int64_t rbeg, int64_t rend,
-                                    int64_t trsm_end, const int32_t* dpairs, void* stream) {
-  return gelim::big::laswp_trsm(dA, lda, c0, lend, rbeg, rend, trsm_end, dpairs, (hipStream_t)stream);
+                                    int64_t trsm_end, int64_t nrows, const int32_t* dpairs, void* stream) {
+  return gelim::big::laswp_trsm(dA, lda, c0, lend, rbeg, rend, trsm_end, nrows, dpairs, (hipStream_t)stream);
 }

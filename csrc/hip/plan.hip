@@ -43,9 +43,9 @@ size_t workspace_bytes();
 int leaf_width();
 int64_t max_rows();
 int leaf_factor(double* A, int64_t lda, int64_t m, int64_t c0, int mode, int* ipiv, int* pairs, int* info,
-                void* ws, int set, hipStream_t s);
+                void* ws, int set, hipStream_t s, unsigned long long* stamps = nullptr);
 int laswp_trsm(double* A, int64_t lda, int64_t c0, int64_t lend, int64_t rbeg, int64_t rend, int64_t trsm_end,
-               const int* pairs, hipStream_t s);
+               int64_t nrows, const int* pairs, hipStream_t s);
 int tail_gemv(const double* A, int64_t lda, int64_t n, int64_t K, const double* x, double* y, double* bnorm,
               hipStream_t s);
 int fold_info(int* info, const int* tinfo, int64_t K, hipStream_t s);
@@ -140,7 +140,7 @@ int enqueue_big(gelim_gauss_plan* p, double* A, double* x, double* bnorm, hipStr
                                  leaf, s));
       // interchanges on every other column (L part, rest of the panel,
       // trailing columns, b); TRSM of the leaf's U rows inside the panel
-      GELIM_TRY(big::laswp_trsm(A + c0 * lda, lda, c0, c0, c0 + LW, n + 1, kend, pr, s));
+      GELIM_TRY(big::laswp_trsm(A + c0 * lda, lda, c0, c0, c0 + LW, n + 1, kend, n - c0, pr, s));
       const int64_t c1 = c0 + LW;
       if (c1 < kend)  // the rest of this outer panel
         GELIM_TRY(dgemm(A + c1 * lda + c1, lda, A + c1 * lda + c0, lda, A + c0 * lda + c1, lda, n - c1, kend - c1, LW,
@@ -149,7 +149,7 @@ int enqueue_big(gelim_gauss_plan* p, double* A, double* x, double* bnorm, hipStr
     // U12 of the outer panel (its rows are final only now): blocked forward
     // substitution with the panel's unit-lower L11, one 32-row block at a time
     for (int64_t r = k; r < kend; r += LW) {
-      GELIM_TRY(big::laswp_trsm(A + r * lda, lda, r, 0, kend, n + 1, n + 1, nullptr, s));
+      GELIM_TRY(big::laswp_trsm(A + r * lda, lda, r, 0, kend, n + 1, n + 1, n - r, nullptr, s));
       if (r + LW < kend)
         GELIM_TRY(dgemm(A + (r + LW) * lda + kend, lda, A + (r + LW) * lda + r, lda, A + r * lda + kend, lda,
                         kend - r - LW, n + 1 - kend, LW, -1.0, s));

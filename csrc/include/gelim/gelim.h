@@ -175,7 +175,7 @@ int gelim_gpu_dgemm(double* dC, int64_t ldc, const double* dA, int64_t lda, cons
 int gelim_gpu_leaf_factor(double* dA, int64_t lda, int64_t m, int64_t c0, int pivot, int32_t* dipiv,
                           int32_t* dpairs, int32_t* dinfo, void* stream);
 int gelim_gpu_laswp_trsm(double* dA, int64_t lda, int64_t c0, int64_t lend, int64_t rbeg, int64_t rend,
-                         int64_t trsm_end, const int32_t* dpairs, void* stream);
+                         int64_t trsm_end, int64_t nrows, const int32_t* dpairs, void* stream);
 int gelim_gpu_gemm_update(double* dC, int64_t ldc, const double* dL,
                           int64_t ldl, const double* dU, int64_t ldu,
                           int64_t M, int64_t N, int64_t K, void* stream);

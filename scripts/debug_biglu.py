@@ -82,7 +82,8 @@ def main() -> None:
                                                ptr(pairs), ptr(info), sh)
             leaf += 1
             _native.check(rc, "leaf")
-            rc = lib.gelim_gpu_laswp_trsm(ptr(G) + 8 * (c0 * lda), lda, c0, c0, c0 + LW, n + 1, kend, ptr(pairs), sh)
+            rc = lib.gelim_gpu_laswp_trsm(ptr(G) + 8 * (c0 * lda), lda, c0, c0, c0 + LW, n + 1, kend, n - c0,
+                                          ptr(pairs), sh)
             _native.check(rc, "laswp")
             ref_leaf(H, c0, kend)
             cmp(f"leaf c0={c0}")
@@ -93,7 +94,7 @@ def main() -> None:
                 cmp(f"  gemm_a c0={c0}")
 
         for r in range(k, kend, LW):
-            rc = lib.gelim_gpu_laswp_trsm(ptr(G) + 8 * (r * lda), lda, r, 0, kend, n + 1, n + 1, None, sh)
+            rc = lib.gelim_gpu_laswp_trsm(ptr(G) + 8 * (r * lda), lda, r, 0, kend, n + 1, n + 1, n - r, None, sh)
             _native.check(rc, "trsm")
             if r + LW < kend:
                 dgemm((r + LW, kend), (r + LW, r), (r, kend), kend - r - LW, n + 1 - kend, LW)

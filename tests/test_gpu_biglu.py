@@ -98,7 +98,7 @@ def test_laswp_trsm_matches_torch(gelim, cuda):
     for e, (d, s) in enumerate(pl):
         pairs[1 + 2 * e], pairs[2 + 2 * e] = d, s
     Ag = A.to(cuda)
-    rc = _native.lib().gelim_gpu_laswp_trsm(ptr(Ag[c0:]), A.shape[1], c0, c0, c0 + 32, ncols, ncols,
+    rc = _native.lib().gelim_gpu_laswp_trsm(ptr(Ag[c0:]), A.shape[1], c0, c0, c0 + 32, ncols, ncols, n - c0,
                                             ptr(pairs.to(cuda)), stream_handle(cuda))
     _native.check(rc, "laswp_trsm")
     torch.cuda.synchronize()

@@ -42,6 +42,7 @@
 
 #include <algorithm>
 #include <cstdint>
+#include <cstdlib>
 #include <utility>
 
 #include "device_common.h"
@@ -114,15 +115,16 @@ struct LeafArgs {
 };
 
 // Diagnostic phase stamp of column J (lane 0 of every participant):
-// 0 start, 1 arg-max done, 2 published, 3 key sweep ready, 4 pivot row
-// loaded, 5 pivot row in LDS, 6 update done, 7 key sweeps + 256 * row loads
+// 0 start, 1 arg-max done, 2 published + pending update applied, 3 key
+// sweep ready, 4 pivot row loaded, 5 pivot row in LDS, 6 multipliers and
+// next column done, 7 key sweeps + 256 * row loads
 __device__ __forceinline__ void lstamp(const LeafArgs& g, int J, int k, unsigned long long v) {
   if (g.stamps != nullptr && threadIdx.x == 0) g.stamps[((int64_t)blockIdx.x * LW + J) * 8 + k] = v;
 }
 
 struct alignas(16) LeafLds {
   double cand[LW];             // this wave's candidate row on its way out
-  double prow[LW];             // the pivot row
+  double prow[2][LW];          // the pivot rows of the last two columns (parity)
   int dest[kRowsPerWave];      // final row of a moved local row (-1: unmoved)
 };
 
@@ -176,12 +178,12 @@ __device__ __forceinline__ int wave_argmax_lane(uint64_t k, unsigned row) {
   return __ffsll((long long)__ballot(c2 && row == mr)) - 1;
 }
 
-template <int MODE, int NKK>
+template <int MODE, int NKK, int NR>
 struct Leaf {
   // one column J of the leaf (compile time); false: hand-off aborted
   template <int J>
-  static __device__ __forceinline__ bool col(double (&a)[R][LW], bool (&live)[R], LeafLds& sh, Table& tb,
-                                             const LeafArgs& g, int lane, int base) {
+  static __device__ __forceinline__ bool col(double (&a)[R][LW], bool (&live)[R], double (&lp)[R], LeafLds& sh,
+                                             Table& tb, const LeafArgs& g, int lane, int base) {
     constexpr int par = J & 1;
     lane = opq(lane);
     const unsigned seq = (unsigned)(J + 1);
@@ -242,17 +244,39 @@ struct Leaf {
         __builtin_amdgcn_raw_buffer_store_b128(u32x4{0u, 0u, 0xffffffffu, seq}, rk, 0, 0, kAuxSc1);
       }
     }
+    // 3b. while the exchange is in flight: the previous pivot's rank-1
+    //     update of columns J+1.. (column J got it already, it is the one
+    //     the candidate above was computed on)
+    if constexpr (J > 0) {
+#pragma unroll
+      for (int c = J + 1; c < LW; ++c) {
+        const double uc = sh.prow[(J - 1) & 1][c];
+#pragma unroll
+        for (int i = 0; i < R; ++i) a[i][c] = fma(-lp[i], uc, a[i][c]);
+      }
+    }
     lstamp(g, J, 2, __builtin_amdgcn_s_memtime());
-    // 4. key sweep: lane p (+ 64 k) reads participant p's key; all loads in
-    //    flight at once (unconditional, clamped: a predicated load is a
-    //    branch with its own vmcnt(0) wait)
+    // 4. sweep: lane p (+ 64 k) reads participant p's key and, when the
+    //    candidate rows fit (NR > 0), every participant's row too -- granule
+    //    p*LW + c sits in load p/2 of lane 32 (p&1) + c -- so the winner's
+    //    row normally arrives with the last key sweep (one round trip per
+    //    column instead of two).  All loads unconditional and in flight at
+    //    once (clamped: a predicated load is a branch with its own vmcnt(0)).
     const __amdgpu_buffer_rsrc_t rks = rsrc(g.x.key + slot, kMaxW * 16);
+    const __amdgpu_buffer_rsrc_t rrw = rsrc(g.x.row + (int64_t)slot * LW, kMaxW * LW * 16);
     u32x4 kv[NKK];
+    u32x4 rw[NR > 0 ? NR : 1];
     unsigned long long t0 = 0;
     int sweeps = 0;
     for (int it = 0;; ++it) {
 #pragma unroll
-      for (int k = 0; k < NKK; ++k) kv[k] = __builtin_amdgcn_raw_buffer_load_b128(rks, min(k * 64 + lane, g.P - 1) * 16, 0, kAuxSc1);
+      for (int k = 0; k < NKK; ++k)
+        kv[k] = __builtin_amdgcn_raw_buffer_load_b128(rks, min(k * 64 + lane, g.P - 1) * 16, 0, kAuxSc1);
+      if constexpr (NR > 0) {
+#pragma unroll
+        for (int k = 0; k < NR; ++k)
+          rw[k] = __builtin_amdgcn_raw_buffer_load_b128(rrw, min(k * 64 + lane, g.P * LW - 1) * 16, 0, kAuxSc1);
+      }
       bool ready = true;
 #pragma unroll
       for (int k = 0; k < NKK; ++k) ready = ready && kv[k].w == seq;
@@ -287,43 +311,62 @@ struct Leaf {
     const int wlw = wave_argmax_lane(key, krow);
     const int pw = __builtin_amdgcn_readlane(kp, wlw);
     const unsigned pr = (unsigned)__builtin_amdgcn_readlane((int)krow, wlw);
-    // 6. the winner's row: lanes c < LW read its granules until they are
-    //    current (they were stored before its key, but nothing orders them)
+    // 6. the winner's row in the lanes of half h = pw & 1 (lane 32 h + c
+    //    holds column c): from the sweep when it carried the rows, re-read
+    //    until every granule is current (the row was stored before the key,
+    //    but nothing orders them)
+    const int h = pw & 1;
+    const bool mine = (lane >> 5) == h;
     const __amdgpu_buffer_rsrc_t rrs = rsrc(g.x.row + (int64_t)(slot + pw) * LW, LW * 16);
     u32x4 rv;
-    int rl = 0;
-    for (;; ++rl) {
+    if constexpr (NR > 0) {
+      rv = rw[0];
+#pragma unroll
+      for (int k = 1; k < NR; ++k) rv = (k == (pw >> 1)) ? rw[k] : rv;
+    } else {
       rv = __builtin_amdgcn_raw_buffer_load_b128(rrs, (lane & (LW - 1)) * 16, 0, kAuxSc1);
-      if (__ballot(rv.w != seq) == 0) break;
-      if ((rl & 63) == 63 && __hip_atomic_load(g.info + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0)
+    }
+    int rl = 0;
+    while (__ballot(mine && rv.w != seq) != 0) {
+      rv = __builtin_amdgcn_raw_buffer_load_b128(rrs, (lane & (LW - 1)) * 16, 0, kAuxSc1);
+      if ((++rl & 63) == 63 && __hip_atomic_load(g.info + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0)
         return false;
     }
     lstamp(g, J, 4, __builtin_amdgcn_s_memtime());
-    if (lane < LW) sh.prow[lane] = mkd(rv.x, rv.y);
+    // the winner published its row before applying the pending update of
+    // pivot J-1 to columns J+1..: apply it here, with the row's own
+    // multiplier (its column J-1) -- the very FMA its owner performs
+    const int cc = lane & (LW - 1);
+    double pval = mkd(rv.x, rv.y);
+    if constexpr (J > 0) {
+      const double lw = mkd((unsigned)__builtin_amdgcn_readlane((int)rv.x, 32 * h + J - 1),
+                            (unsigned)__builtin_amdgcn_readlane((int)rv.y, 32 * h + J - 1));
+      if (mine && cc > J) pval = fma(-lw, sh.prow[(J - 1) & 1][cc], pval);
+    }
+    if (mine) sh.prow[par][cc] = pval;
     // interchange replay; participant 0 records the LAPACK pivot
     const int qpos = table_swap(tb, J, (int)pr, lane);
     if (blockIdx.x == 0 && lane == 0) g.ipiv[g.col0 + J] = g.col0 + qpos;
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the pivot row is in LDS (wave-local)
     lstamp(g, J, 5, __builtin_amdgcn_s_memtime());
-    lstamp(g, J, 7, (unsigned long long)sweeps + 256ull * (rl + 1));
+    lstamp(g, J, 7, (unsigned long long)sweeps + 256ull * rl);
 
-    // 7. multipliers and the rank-1 update of columns J+1..
-    const double pv = sh.prow[J];
+    // 7. multipliers; this pivot's update of column J+1 only (the next
+    //    candidate), the rest of it is pending until the next exchange
+    const double pv = sh.prow[par][J];
     const bool zero = !(pv != 0.0);
     const double rinv = zero ? 0.0 : recip(pv);
     if (zero && blockIdx.x == 0 && lane == 0 && g.info[0] == 0) atomicCAS(g.info, 0, g.col0 + J + 1);
-    double l[R];
 #pragma unroll
     for (int i = 0; i < R; ++i) {
       live[i] = live[i] && (base + lane + 64 * i != (int)pr);
-      l[i] = live[i] ? a[i][J] * rinv : 0.0;
-      a[i][J] = live[i] ? l[i] : a[i][J];
+      lp[i] = live[i] ? a[i][J] * rinv : 0.0;
+      a[i][J] = live[i] ? lp[i] : a[i][J];
     }
+    if constexpr (J + 1 < LW) {
+      const double uc = sh.prow[par][J + 1];
 #pragma unroll
-    for (int c = J + 1; c < LW; ++c) {
-      const double uc = sh.prow[c];
-#pragma unroll
-      for (int i = 0; i < R; ++i) a[i][c] = fma(-l[i], uc, a[i][c]);
+      for (int i = 0; i < R; ++i) a[i][J + 1] = fma(-lp[i], uc, a[i][J + 1]);
     }
     if (g.stamps != nullptr) {
       asm volatile("" ::"v"(a[R - 1][LW - 1]));
@@ -336,13 +379,16 @@ struct Leaf {
   static __device__ __forceinline__ bool factor(double (&a)[R][LW], bool (&live)[R], LeafLds& sh, Table& tb,
                                                 const LeafArgs& g, int lane, int base,
                                                 std::integer_sequence<int, J...>) {
-    return (col<J>(a, live, sh, tb, g, lane, base) && ...);
+    double lp[R];  // multipliers of the pending (previous) pivot
+#pragma unroll
+    for (int i = 0; i < R; ++i) lp[i] = 0.0;
+    return (col<J>(a, live, lp, sh, tb, g, lane, base) && ...);
   }
 };
 
 // One wave per workgroup; participant w = blockIdx.x owns rows
 // [256 w, 256 w + 256) of the leaf, lane l the rows 256 w + l + 64 i.
-template <int MODE, int NKK>
+template <int MODE, int NKK, int NR>
 __global__ __launch_bounds__(64, 1) void leaf_kernel(LeafArgs g) {
   __shared__ LeafLds sh;
   const int lane = threadIdx.x;
@@ -364,7 +410,7 @@ __global__ __launch_bounds__(64, 1) void leaf_kernel(LeafArgs g) {
 #pragma unroll
   for (int i = 0; i < R; ++i) sh.dest[lane + 64 * i] = -1;
   Table tb{0, 0, 0};
-  if (!Leaf<MODE, NKK>::factor(a, live, sh, tb, g, lane, base, std::make_integer_sequence<int, LW>{})) return;
+  if (!Leaf<MODE, NKK, NR>::factor(a, live, sh, tb, g, lane, base, std::make_integer_sequence<int, LW>{})) return;
 
   // net row movement (participant 0 publishes it); every participant maps
   // its own moved rows to their final positions and writes its rows there
@@ -422,74 +468,98 @@ struct SwapArgs {
 };
 
 __global__ __launch_bounds__(kSwThreads) void laswp_trsm_kernel(SwapArgs g) {
-  __shared__ double sL[LW][LW + 1];
+  __shared__ double sLt[LW][LW];        // transposed L11: sLt[i][j] = L[j][i]
   __shared__ double xs[LW][kSwThreads];
-  __shared__ int sp[1 + 4 * LW];
-  const int t = threadIdx.x;
+  __shared__ int sdst[2 * LW];          // validated pair list (dst -1: none)
+  const int lane = threadIdx.x;
   const int64_t lda = g.lda;
-  // only the strictly lower part is ever read: copy the whole block, no
-  // select (a select right after each load makes the compiler wait on it)
-  for (int e = t; e < LW * LW; e += kSwThreads) {
-    const int r = e / LW, c = e % LW;
-    sL[r][c] = g.A[(int64_t)r * lda + g.c0 + c];
+  // one round trip for everything the columns depend on: lane e holds pair
+  // e (dst, src) -- read back with readlane, so row offsets are scalar --
+  // and 16 elements of L11 (every load unconditional, issued together)
+  int cnt = 0, pd = -1, ps = -1;
+  if (g.pairs != nullptr) {
+    cnt = min(g.pairs[0], 2 * LW);
+    pd = g.pairs[1 + 2 * lane];
+    ps = g.pairs[2 + 2 * lane];
   }
-  // (strided: the workgroup is narrower than the list) entries outside
-  // [0, nrows) are dropped, so a corrupt list can never address past the
-  // system
-  const int np_in = g.pairs ? min(g.pairs[0], 2 * LW) : 0;
-  for (int e = t; e < 1 + 4 * LW; e += kSwThreads) {
-    int v = 0;
-    if (e > 0 && e <= 2 * np_in) {
-      v = g.pairs[e];
-      v = (v >= 0 && v < g.nrows) ? v : -1;
-    }
-    sp[e] = v;
+  double lv[LW * LW / kSwThreads];
+#pragma unroll
+  for (int k = 0; k < LW * LW / kSwThreads; ++k) {
+    const int e = lane + kSwThreads * k;
+    lv[k] = g.A[(int64_t)(e / LW) * lda + g.c0 + (e % LW)];
   }
-  if (t == 0) sp[0] = np_in;
-  __syncthreads();
-  const int np = sp[0];
+  const bool pok = lane < cnt && pd >= 0 && pd < g.nrows && ps >= 0 && ps < g.nrows;
+  pd = pok ? pd : -1;
+  ps = pok ? ps : 0;
+  // destinations are read after lanes have diverged: from LDS, never with
+  // readlane (a lane that has left keeps a stale register, and the select
+  // above may be sunk past the divergence)
+  sdst[lane] = pd;
+#pragma unroll
+  for (int k = 0; k < LW * LW / kSwThreads; ++k) {
+    const int e = lane + kSwThreads * k;
+    sLt[e % LW][e / LW] = lv[k];
+  }
   const int nleft = g.lend, nright = g.rend - g.rbeg;
-  const int idx = blockIdx.x * kSwThreads + t;
-  if (idx >= nleft + nright) return;
+  const int idx = blockIdx.x * kSwThreads + lane;
+  const bool any = idx < nleft + nright;
   const bool right = idx >= nleft;
-  const int c = right ? idx - nleft + g.rbeg : idx;
+  const int c = any ? (right ? idx - nleft + g.rbeg : idx) : 0;
   double* col = g.A + c;
+  const bool trsm = any && right && c < g.trsm_end;
+  // gathers: every touched source row, before any destination is written
   double gsrc[2 * LW];
 #pragma unroll
-  for (int e = 0; e < 2 * LW; ++e) {
-    // unconditional load of a clamped row and no select: entries past np are
-    // never stored.  (A predicated load, or a select right behind the load,
-    // makes the compiler wait for each one: 64 serial round trips.)
-    gsrc[e] = col[(int64_t)max(sp[2 + 2 * e], 0) * lda];
+  for (int e = 0; e < 2 * LW; ++e) gsrc[e] = col[(int64_t)__builtin_amdgcn_readlane(ps, e) * lda];
+  double x[LW];
+  if (__ballot(trsm) != 0) {
+#pragma unroll
+    for (int j = 0; j < LW; ++j) x[j] = col[(int64_t)j * lda];
   }
-  if (!right || c >= g.trsm_end) {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // sLt written (single-wave workgroup)
+  if (!any) return;
+  if (!trsm) {
 #pragma unroll
     for (int e = 0; e < 2 * LW; ++e) {
-      const int d = sp[1 + 2 * e];
-      if (e < np && d >= 0 && sp[2 + 2 * e] >= 0) col[(int64_t)d * lda] = gsrc[e];
+      const int d = sdst[e];
+      if (d >= 0) col[(int64_t)d * lda] = gsrc[e];
     }
     return;
   }
+  // top LW rows of the column after the interchanges: staged through LDS
+  // (the destination row is uniform, the register array is not indexable)
 #pragma unroll
-  for (int j = 0; j < LW; ++j) xs[j][t] = col[(int64_t)j * lda];
+  for (int j = 0; j < LW; ++j) xs[j][lane] = x[j];
 #pragma unroll
   for (int e = 0; e < 2 * LW; ++e) {
-    const int d = sp[1 + 2 * e];
-    if (e < np && d >= 0 && sp[2 + 2 * e] >= 0) {
-      if (d < LW) xs[d][t] = gsrc[e];
+    const int d = sdst[e];
+    if (d >= 0) {
+      if (d < LW) xs[d][lane] = gsrc[e];
       else col[(int64_t)d * lda] = gsrc[e];
     }
   }
-  double x[LW];
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
-  for (int j = 0; j < LW; ++j) x[j] = xs[j][t];
+  for (int j = 0; j < LW; ++j) x[j] = xs[j][lane];
+  // forward substitution, column i of L read (uniform, 16-byte LDS reads)
+  // one step ahead of its use
+  double lc[LW];
+#pragma unroll
+  for (int j = 1; j < LW; ++j) lc[j] = sLt[0][j];
 #pragma unroll
   for (int i = 0; i < LW; ++i) {
+    double ln[LW];
+    if (i + 1 < LW) {
+#pragma unroll
+      for (int j = i + 2; j < LW; ++j) ln[j] = sLt[i + 1][j];
+    }
     __builtin_amdgcn_sched_barrier(0);
     const double xi = x[i];
     col[(int64_t)i * lda] = xi;
 #pragma unroll
-    for (int j = i + 1; j < LW; ++j) x[j] = fma(-sL[j][i], xi, x[j]);
+    for (int j = i + 1; j < LW; ++j) x[j] = fma(-lc[j], xi, x[j]);
+#pragma unroll
+    for (int j = i + 2; j < LW; ++j) lc[j] = ln[j];
   }
 }
 
@@ -546,13 +616,17 @@ int leaf_factor(double* A, int64_t lda, int64_t m, int64_t c0, int mode, int* ip
   a.x.key = static_cast<u32x4*>(ws);
   a.x.row = reinterpret_cast<u32x4*>(static_cast<char*>(ws) + kKeyBytes);
   a.stamps = stamps;
-#define GELIM_LEAF(NKK)                                                                          \
-  if (mode == GELIM_PIVOT_PARTIAL)                                                               \
-    hipLaunchKernelGGL((leaf_kernel<1, NKK>), dim3((unsigned)a.P), dim3(64), 0, s, a);           \
-  else                                                                                           \
-    hipLaunchKernelGGL((leaf_kernel<0, NKK>), dim3((unsigned)a.P), dim3(64), 0, s, a)
-  if (a.P <= 64) GELIM_LEAF(1);
-  else GELIM_LEAF(2);
+  // NR: row loads per lane when the sweep carries every candidate row
+  // (P <= 32: at most 16 KiB per sweep), 0 = key sweep then row load
+  // (GELIM_LEAF_2HOP=1).  Measured within noise of each other: the 8192
+  // solve 42.0 vs 43.0 ms, the lone m = 8192 leaf 137.7 vs 130.7 us
+  // (profiles/leaf_fused_vs_2hop.txt)
+  const bool fused = std::getenv("GELIM_LEAF_2HOP") == nullptr;
+  if (fused && a.P <= 8) GELIM_LEAF(1, 4);
+  else if (fused && a.P <= 16) GELIM_LEAF(1, 8);
+  else if (fused && a.P <= 32) GELIM_LEAF(1, 16);
+  else if (a.P <= 64) GELIM_LEAF(1, 0);
+  else GELIM_LEAF(2, 0);
 #undef GELIM_LEAF
   HIP_TRY(hipGetLastError());
   return GELIM_OK;

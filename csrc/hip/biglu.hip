@@ -444,8 +444,8 @@ __global__ __launch_bounds__(64, 1) void leaf_kernel(LeafArgs g) {
 }
 
 // ---- row interchanges for the other columns + TRSM of a leaf's U rows -----
-// One thread per column of [0, lend) (interchanges only: the L part left of
-// the leaf) and of [rbeg, rend) (interchanges, then -- for columns below
+// One thread per column of [lbeg, lend) (interchanges only: the L part left
+// of the leaf) and of [rbeg, rend) (interchanges, then -- for columns below
 // trsm_end -- U12 = L11^-1 A12 on the LW rows starting at row c0, L11 being
 // the leaf at (c0, c0)).  A points at row c0, column 0; rows of the pair
 // list are relative to c0 (pairs == nullptr: no interchanges).  Every
@@ -463,7 +463,7 @@ constexpr int kSwThreads = 64;  // one wave per workgroup: one CU per 64 columns
 struct SwapArgs {
   double* A;
   int64_t lda;
-  int c0, lend, rbeg, rend, trsm_end, nrows;
+  int c0, lbeg, lend, rbeg, rend, trsm_end, nrows;
   const int* pairs;
 };
 
@@ -500,11 +500,11 @@ __global__ __launch_bounds__(kSwThreads) void laswp_trsm_kernel(SwapArgs g) {
     const int e = lane + kSwThreads * k;
     sLt[e % LW][e / LW] = lv[k];
   }
-  const int nleft = g.lend, nright = g.rend - g.rbeg;
+  const int nleft = g.lend - g.lbeg, nright = g.rend - g.rbeg;
   const int idx = blockIdx.x * kSwThreads + lane;
   const bool any = idx < nleft + nright;
   const bool right = idx >= nleft;
-  const int c = any ? (right ? idx - nleft + g.rbeg : idx) : 0;
+  const int c = any ? (right ? idx - nleft + g.rbeg : g.lbeg + idx) : 0;
   double* col = g.A + c;
   const bool trsm = any && right && c < g.trsm_end;
   // gathers: every touched source row, before any destination is written
@@ -560,6 +560,52 @@ __global__ __launch_bounds__(kSwThreads) void laswp_trsm_kernel(SwapArgs g) {
     for (int j = i + 1; j < LW; ++j) x[j] = fma(-lc[j], xi, x[j]);
 #pragma unroll
     for (int j = i + 2; j < LW; ++j) lc[j] = ln[j];
+  }
+}
+
+// ---- a whole outer panel's interchanges on other columns ---------------------
+// The lookahead schedule (plan.hip) applies an outer panel's row movement to
+// the columns it does not own -- the L part left of the panel and the
+// trailing columns the side stream updates -- in ONE launch: per column, the
+// panel's leaf pair lists in order (each a permutation of <= 2 LW rows:
+// every source gathered before any destination is written).  The lists are
+// wave-uniform, so their words are scalar loads (no LDS, no readlane).
+struct PanelSwapArgs {
+  double* A;          // row 0, column 0 of the system
+  int64_t lda;
+  int n;              // rows of the system (list entries are validated against it)
+  int c0;             // diagonal of the panel's first leaf
+  int nleaves;
+  const int* pairs;   // nleaves slots of `slot` ints: [0] count, then (dst, src) relative to the leaf's diagonal
+  int slot;
+  int lbeg, lend, rbeg, rend;  // columns [lbeg, lend) and [rbeg, rend)
+};
+
+__global__ __launch_bounds__(64) void laswp_panel_kernel(PanelSwapArgs g) {
+  const int idx = blockIdx.x * 64 + threadIdx.x;
+  const int nl = g.lend - g.lbeg, nr = g.rend - g.rbeg;
+  const bool any = idx < nl + nr;
+  // lanes past the ranges read a valid column and store nothing (no early
+  // exit: the loop below stays uniform)
+  const int c = any ? (idx < nl ? g.lbeg + idx : g.rbeg + idx - nl) : (nl > 0 ? g.lbeg : g.rbeg);
+  double* col = g.A + c;
+#pragma unroll 1
+  for (int l = 0; l < g.nleaves; ++l) {
+    const int* pr = g.pairs + (int64_t)l * g.slot;
+    const int cnt = min(pr[0], 2 * LW);
+    const int base = g.c0 + l * LW;
+    double v[2 * LW];
+#pragma unroll
+    for (int e = 0; e < 2 * LW; ++e) {
+      const int src = base + pr[2 + 2 * e];
+      const bool ok = e < cnt && src >= base && src < g.n;
+      v[e] = col[(int64_t)(ok ? src : base) * g.lda];
+    }
+#pragma unroll
+    for (int e = 0; e < 2 * LW; ++e) {
+      const int dst = base + pr[1 + 2 * e], src = base + pr[2 + 2 * e];
+      if (any && e < cnt && dst >= base && dst < g.n && src >= base && src < g.n) col[(int64_t)dst * g.lda] = v[e];
+    }
   }
 }
 
@@ -621,6 +667,11 @@ int leaf_factor(double* A, int64_t lda, int64_t m, int64_t c0, int mode, int* ip
   // (GELIM_LEAF_2HOP=1).  Measured within noise of each other: the 8192
   // solve 42.0 vs 43.0 ms, the lone m = 8192 leaf 137.7 vs 130.7 us
   // (profiles/leaf_fused_vs_2hop.txt)
+#define GELIM_LEAF(NKK, NR)                                                                      \
+  if (mode == GELIM_PIVOT_PARTIAL)                                                               \
+    hipLaunchKernelGGL((leaf_kernel<1, NKK, NR>), dim3((unsigned)a.P), dim3(64), 0, s, a);       \
+  else                                                                                           \
+    hipLaunchKernelGGL((leaf_kernel<0, NKK, NR>), dim3((unsigned)a.P), dim3(64), 0, s, a)
   const bool fused = std::getenv("GELIM_LEAF_2HOP") == nullptr;
   if (fused && a.P <= 8) GELIM_LEAF(1, 4);
   else if (fused && a.P <= 16) GELIM_LEAF(1, 8);
@@ -632,17 +683,34 @@ int leaf_factor(double* A, int64_t lda, int64_t m, int64_t c0, int mode, int* ip
   return GELIM_OK;
 }
 
-// Row movement of a leaf (pairs, may be null) on columns [0, lend) and
+// Row movement of a leaf (pairs, may be null) on columns [lbeg, lend) and
 // [rbeg, rend) of rows [c0, ...), TRSM of rows [c0, c0 + LW) on the right
 // columns below trsm_end.  A: row c0, column 0.
-int laswp_trsm(double* A, int64_t lda, int64_t c0, int64_t lend, int64_t rbeg, int64_t rend, int64_t trsm_end,
-               int64_t nrows, const int* pairs, hipStream_t s) {
-  const int64_t cols = lend + std::max<int64_t>(0, rend - rbeg);
+int laswp_trsm(double* A, int64_t lda, int64_t c0, int64_t lbeg, int64_t lend, int64_t rbeg, int64_t rend,
+               int64_t trsm_end, int64_t nrows, const int* pairs, hipStream_t s) {
+  lend = std::max(lend, lbeg);
+  rend = std::max(rend, rbeg);
+  const int64_t cols = (lend - lbeg) + (rend - rbeg);
   if (cols <= 0) return GELIM_OK;
   if (nrows < LW) return GELIM_FAIL(GELIM_E_ARG, "laswp_trsm: fewer rows than the leaf width");
-  SwapArgs a{A, lda, (int)c0, (int)lend, (int)rbeg, (int)rend, (int)trsm_end, (int)nrows, pairs};
+  SwapArgs a{A, lda, (int)c0, (int)lbeg, (int)lend, (int)rbeg, (int)rend, (int)trsm_end, (int)nrows, pairs};
   hipLaunchKernelGGL(laswp_trsm_kernel, dim3((unsigned)((cols + kSwThreads - 1) / kSwThreads)), dim3(kSwThreads), 0,
                      s, a);
+  HIP_TRY(hipGetLastError());
+  return GELIM_OK;
+}
+
+// Row movement of nleaves consecutive leaves (diagonals c0, c0 + LW, ...;
+// pair lists `slot` ints apart) on columns [lbeg, lend) and [rbeg, rend) of
+// the n-row system at A (row 0, column 0).
+int laswp_panel(double* A, int64_t lda, int64_t n, int64_t c0, int nleaves, const int* pairs, int64_t slot,
+                int64_t lbeg, int64_t lend, int64_t rbeg, int64_t rend, hipStream_t s) {
+  lend = std::max(lend, lbeg);
+  rend = std::max(rend, rbeg);
+  const int64_t cols = (lend - lbeg) + (rend - rbeg);
+  if (cols <= 0 || nleaves <= 0) return GELIM_OK;
+  PanelSwapArgs a{A, lda, (int)n, (int)c0, nleaves, pairs, (int)slot, (int)lbeg, (int)lend, (int)rbeg, (int)rend};
+  hipLaunchKernelGGL(laswp_panel_kernel, dim3((unsigned)((cols + 63) / 64)), dim3(64), 0, s, a);
   HIP_TRY(hipGetLastError());
   return GELIM_OK;
 }
@@ -702,9 +770,15 @@ extern "C" int gelim_debug_leaf_stamps(double* dA, int64_t lda, int64_t m, void*
   return rc;
 }
 
+extern "C" int gelim_gpu_laswp_panel(double* dA, int64_t lda, int64_t n, int64_t c0, int nleaves,
+                                     const int32_t* dpairs, int64_t slot, int64_t lbeg, int64_t lend, int64_t rbeg,
+                                     int64_t rend, void* stream) {
+  return gelim::big::laswp_panel(dA, lda, n, c0, nleaves, dpairs, slot, lbeg, lend, rbeg, rend, (hipStream_t)stream);
+}
+
 extern "C" int64_t gelim_gpu_leaf_workspace_bytes(void) { return (int64_t)gelim::big::workspace_bytes(); }
 
 extern "C" int gelim_gpu_laswp_trsm(double* dA, int64_t lda, int64_t c0, int64_t lend, int64_t rbeg, int64_t rend,
                                     int64_t trsm_end, int64_t nrows, const int32_t* dpairs, void* stream) {
-  return gelim::big::laswp_trsm(dA, lda, c0, lend, rbeg, rend, trsm_end, nrows, dpairs, (hipStream_t)stream);
+  return gelim::big::laswp_trsm(dA, lda, c0, 0, lend, rbeg, rend, trsm_end, nrows, dpairs, (hipStream_t)stream);
 }

@@ -44,8 +44,10 @@ int leaf_width();
 int64_t max_rows();
 int leaf_factor(double* A, int64_t lda, int64_t m, int64_t c0, int mode, int* ipiv, int* pairs, int* info,
                 void* ws, int set, hipStream_t s, unsigned long long* stamps = nullptr);
-int laswp_trsm(double* A, int64_t lda, int64_t c0, int64_t lend, int64_t rbeg, int64_t rend, int64_t trsm_end,
-               int64_t nrows, const int* pairs, hipStream_t s);
+int laswp_trsm(double* A, int64_t lda, int64_t c0, int64_t lbeg, int64_t lend, int64_t rbeg, int64_t rend,
+               int64_t trsm_end, int64_t nrows, const int* pairs, hipStream_t s);
+int laswp_panel(double* A, int64_t lda, int64_t n, int64_t c0, int nleaves, const int* pairs, int64_t slot,
+                int64_t lbeg, int64_t lend, int64_t rbeg, int64_t rend, hipStream_t s);
 int tail_gemv(const double* A, int64_t lda, int64_t n, int64_t K, const double* x, double* y, double* bnorm,
               hipStream_t s);
 int fold_info(int* info, const int* tinfo, int64_t K, hipStream_t s);
@@ -94,6 +96,12 @@ struct gelim_gauss_plan {
   void* big_ws = nullptr;                // leaf exchange granules + rows
   int* big_pairs = nullptr;              // per-leaf row movement
   double* big_y = nullptr;               // top right-hand side after the tail
+  // lookahead (GELIM_BIG_LOOKAHEAD=1; default serial, graph-captured): the
+  // trailing updates run on big_side, eagerly launched, optionally masked
+  // off the last GELIM_BIG_RESERVE CUs (default 0: unmasked)
+  bool big_la = false;
+  hipStream_t big_side = nullptr;
+  std::vector<hipEvent_t> big_ev;        // fork, fact[T], next[T], join
   hipGraphExec_t exec = nullptr;
   const void* k_src = nullptr;
   int64_t k_ld = 0;
@@ -123,40 +131,112 @@ constexpr int64_t kBigPairSlot = 1 + 4 * 32 + 3;
 
 int enqueue(gelim_gauss_plan* p, const void* src, int64_t src_ld, void* dx, void* bnorm, hipStream_t s);
 
+// U12 of outer panel [k, kend) on columns [cb, ce) (blocked forward
+// substitution with the panel's unit-lower L11, one leaf-row block at a
+// time), then their trailing update A[kend:, cb:ce) -= L21 U12 (K = kend - k).
+int panel_u12_update(gelim_gauss_plan* p, double* A, int64_t k, int64_t kend, int64_t cb, int64_t ce,
+                     hipStream_t s) {
+  using namespace gelim;
+  const int64_t n = p->n, lda = p->lda, LW = big::leaf_width();
+  if (ce <= cb) return GELIM_OK;
+  for (int64_t r = k; r < kend; r += LW) {
+    GELIM_TRY(big::laswp_trsm(A + r * lda, lda, r, 0, 0, cb, ce, ce, n - r, nullptr, s));
+    if (r + LW < kend)
+      GELIM_TRY(dgemm(A + (r + LW) * lda + cb, lda, A + (r + LW) * lda + r, lda, A + r * lda + cb, lda,
+                      kend - r - LW, ce - cb, LW, -1.0, s));
+  }
+  return dgemm(A + kend * lda + cb, lda, A + kend * lda + k, lda, A + k * lda + cb, lda, n - kend, ce - cb,
+               kend - k, -1.0, s);
+}
+
 // Wide-panel LU of columns [0, big_k) of the working system, then the tail
 // solve and the block back substitution:
 //   x[K..n) = tail solve of A[K:, K:] (already carrying every update),
 //   y = A[0:K, n] - A[0:K, K:n] x[K..n),  x[0..K) = U11^-1 y.
+//
+// Outer panels P_j = [k_j, k_j+1) of kBigNb columns, each factored as
+// 32-column leaves: per leaf the leaf itself (biglu.hip), its row movement
+// on the other columns + the TRSM of its U rows, and a rank-32 GEMM of the
+// columns right of it inside the panel.
+//
+// Serial schedule (GELIM_BIG_LOOKAHEAD=0): after P_j, U12 and one K = 256
+// GEMM update every column right of it -- the leaf chain and the big GEMMs
+// alternate on one stream.
+//
+// Lookahead schedule (default), the leaf chain on the caller's stream
+// ("crit"), the big GEMMs beside it on big_side:
+//   crit, P_j:  every leaf also updates the NEXT panel's columns P_j+1
+//               (swap, TRSM, rank-32 GEMM -- right-looking at nb = 32), so
+//               P_j+1 is ready the moment P_j's last leaf is; before its
+//               first touch of P_j+1 it waits for side j-1's first part.
+//   side, P_j:  after P_j's leaves, first P_j+2's columns (swaps, U12, K = 256
+//               GEMM; event next[j]), then the L part left of P_j (swaps
+//               only) and every column from P_j+3 on (swaps, U12, GEMM).
+// Column sets never overlap between the streams while both run: crit owns
+// P_j and P_j+1, side P_j+2 (until next[j]) and everything else.
 int enqueue_big(gelim_gauss_plan* p, double* A, double* x, double* bnorm, hipStream_t s) {
   using namespace gelim;
   const int64_t n = p->n, lda = p->lda, K = p->big_k, LW = big::leaf_width();
+  const int64_t T = (K + kBigNb - 1) / kBigNb;
+  auto kb = [&](int64_t j) { return std::min(j * kBigNb, K); };  // P_j = [kb(j), kb(j+1))
+  const bool la = p->big_la;
+  hipStream_t side = la ? p->big_side : s;
+  hipEvent_t* ev_fork = la ? &p->big_ev[0] : nullptr;
+  hipEvent_t* ev_fact = la ? &p->big_ev[1] : nullptr;
+  hipEvent_t* ev_next = la ? &p->big_ev[1 + T] : nullptr;
+  hipEvent_t* ev_join = la ? &p->big_ev[1 + 2 * T] : nullptr;
   HIP_TRY(hipMemsetAsync(p->big_ws, 0, big::workspace_bytes(), s));
+  if (la) {
+    HIP_TRY(hipEventRecord(*ev_fork, s));
+    HIP_TRY(hipStreamWaitEvent(side, *ev_fork, 0));
+  }
   int leaf = 0;
-  for (int64_t k = 0; k < K; k += kBigNb) {
-    const int64_t kend = std::min(k + kBigNb, K);
+  for (int64_t j = 0; j < T; ++j) {
+    const int64_t k = kb(j), kend = kb(j + 1);
+    const int64_t cend = la ? kb(j + 2) : n + 1;  // columns the leaves update: P_j (+ P_j+1)
+    const int first_leaf = leaf;
     for (int64_t c0 = k; c0 < kend; c0 += LW, ++leaf) {
       int* pr = p->big_pairs + leaf * kBigPairSlot;
       GELIM_TRY(big::leaf_factor(A + c0 * lda + c0, lda, n - c0, c0, p->pivot, p->piv, pr, p->info, p->big_ws,
                                  leaf, s));
-      // interchanges on every other column (L part, rest of the panel,
-      // trailing columns, b); TRSM of the leaf's U rows inside the panel
-      GELIM_TRY(big::laswp_trsm(A + c0 * lda, lda, c0, c0, c0 + LW, n + 1, kend, n - c0, pr, s));
+      // P_j+1 is side j-1's until next[j-1]
+      if (la && c0 == k && j > 0 && cend > kend) HIP_TRY(hipStreamWaitEvent(s, ev_next[j - 1], 0));
+      // serial: interchanges on every other column (L part, rest of the
+      // panel, trailing columns, b), TRSM inside the panel; lookahead: the
+      // panel's own L part and P_j, P_j+1 (swaps + TRSM)
+      GELIM_TRY(big::laswp_trsm(A + c0 * lda, lda, c0, la ? k : 0, c0, c0 + LW, cend, la ? cend : kend, n - c0, pr,
+                                s));
       const int64_t c1 = c0 + LW;
-      if (c1 < kend)  // the rest of this outer panel
-        GELIM_TRY(dgemm(A + c1 * lda + c1, lda, A + c1 * lda + c0, lda, A + c0 * lda + c1, lda, n - c1, kend - c1, LW,
+      const int64_t gend = la ? cend : kend;
+      if (c1 < gend)
+        GELIM_TRY(dgemm(A + c1 * lda + c1, lda, A + c1 * lda + c0, lda, A + c0 * lda + c1, lda, n - c1, gend - c1, LW,
                         -1.0, s));
     }
-    // U12 of the outer panel (its rows are final only now): blocked forward
-    // substitution with the panel's unit-lower L11, one 32-row block at a time
-    for (int64_t r = k; r < kend; r += LW) {
-      GELIM_TRY(big::laswp_trsm(A + r * lda, lda, r, 0, kend, n + 1, n + 1, n - r, nullptr, s));
-      if (r + LW < kend)
-        GELIM_TRY(dgemm(A + (r + LW) * lda + kend, lda, A + (r + LW) * lda + r, lda, A + r * lda + kend, lda,
-                        kend - r - LW, n + 1 - kend, LW, -1.0, s));
+    if (!la) {
+      // U12 of the outer panel (its rows are final only now) and the
+      // trailing update of every column right of it, b included
+      GELIM_TRY(panel_u12_update(p, A, k, kend, kend, n + 1, s));
+      continue;
     }
-    // trailing update of the outer panel: A22 -= L21 U12, K = kend - k
-    GELIM_TRY(dgemm(A + kend * lda + kend, lda, A + kend * lda + k, lda, A + k * lda + kend, lda, n - kend,
-                    n + 1 - kend, kend - k, -1.0, s));
+    const int nl = leaf - first_leaf;
+    const int* pr0 = p->big_pairs + first_leaf * kBigPairSlot;
+    HIP_TRY(hipEventRecord(ev_fact[j], s));
+    HIP_TRY(hipStreamWaitEvent(side, ev_fact[j], 0));
+    // side, first part: P_j+2 = [kb(j+2), kb(j+3))
+    const int64_t nb0 = kb(j + 2), nb1 = kb(j + 3);
+    if (nb1 > nb0) {
+      GELIM_TRY(big::laswp_panel(A, lda, n, k, nl, pr0, kBigPairSlot, 0, 0, nb0, nb1, side));
+      GELIM_TRY(panel_u12_update(p, A, k, kend, nb0, nb1, side));
+    }
+    HIP_TRY(hipEventRecord(ev_next[j], side));
+    // side, the rest: the L part left of P_j, every column from P_j+3 on
+    const int64_t rb = std::max(nb1, cend);
+    GELIM_TRY(big::laswp_panel(A, lda, n, k, nl, pr0, kBigPairSlot, 0, k, rb, n + 1, side));
+    GELIM_TRY(panel_u12_update(p, A, k, kend, rb, n + 1, side));
+  }
+  if (la) {
+    HIP_TRY(hipEventRecord(*ev_join, side));
+    HIP_TRY(hipStreamWaitEvent(s, *ev_join, 0));
   }
   GELIM_TRY(enqueue(p->tail, A + K * lda + K, lda, x + K, bnorm ? bnorm + K : nullptr, s));
   GELIM_TRY(big::fold_info(p->info, p->tail->info, K, s));
@@ -347,6 +427,34 @@ extern "C" gelim_gauss_plan* gelim_gauss_plan_create(int64_t n, int algo, int pi
     const int64_t nleaves = big_k / lw;
     if (hipMalloc((void**)&p->big_pairs, sizeof(int) * kBigPairSlot * nleaves) != hipSuccess) return fail("pairs");
     if (hipStreamCreateWithFlags(&p->cap, hipStreamNonBlocking) != hipSuccess) return fail("stream");
+    // lookahead (opt-in): trailing updates on a second stream, launched
+    // eagerly (a replayed graph would not keep a stream's CU mask).
+    // Measured at n = 8192 (profiles/big_lookahead_8192.txt): serial 42.0 ms;
+    // lookahead unmasked 42.3 ms -- the leaves run 22 % slower beside the
+    // GEMMs and the crit stream waits for the side's next-panel update every
+    // panel; masked off 32 / 64 CUs 147 / 66 ms -- the masked queue's
+    // kernels never ran beside the leaves (0 us of GEMM under a leaf)
+    const char* el = std::getenv("GELIM_BIG_LOOKAHEAD");
+    p->big_la = el && std::atoi(el) != 0;
+    if (p->big_la) {
+      int dev = 0, ncu = 0;
+      (void)hipGetDevice(&dev);
+      (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+      int reserve = 0;
+      if (const char* er = std::getenv("GELIM_BIG_RESERVE")) reserve = std::max(0, std::atoi(er));
+      if (ncu > 0 && reserve > 0 && reserve < ncu) {
+        std::vector<uint32_t> mask((size_t)(ncu + 31) / 32, 0u);
+        for (int c = 0; c < ncu - reserve; ++c) mask[(size_t)c / 32] |= 1u << (c % 32);
+        if (hipExtStreamCreateWithCUMask(&p->big_side, (uint32_t)mask.size(), mask.data()) != hipSuccess)
+          return fail("CU-masked stream");
+      } else if (hipStreamCreateWithFlags(&p->big_side, hipStreamNonBlocking) != hipSuccess) {
+        return fail("side stream");
+      }
+      const int64_t T = (big_k + kBigNb - 1) / kBigNb;
+      p->big_ev.assign((size_t)(2 * T + 2), nullptr);
+      for (auto& e : p->big_ev)
+        if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return fail("event");
+    }
     p->tail = gelim_gauss_plan_create(n - big_k, algo, pivot, dtype_bytes, 0);
     if (!p->tail) {
       gelim_gauss_plan_destroy(p);
@@ -432,6 +540,9 @@ extern "C" void gelim_gauss_plan_destroy(gelim_gauss_plan* p) {
   if (p->exec) (void)hipGraphExecDestroy(p->exec);
   if (p->cap) (void)hipStreamDestroy(p->cap);
   if (p->side) (void)hipStreamDestroy(p->side);
+  if (p->big_side) (void)hipStreamDestroy(p->big_side);
+  for (auto& e : p->big_ev)
+    if (e) (void)hipEventDestroy(e);
   for (auto* v : {&p->ev_panel, &p->ev_wide})
     for (auto& e : *v)
       if (e) (void)hipEventDestroy(e);
@@ -460,7 +571,7 @@ extern "C" int gelim_gauss_plan_solve(gelim_gauss_plan* p, const void* src, int6
   if (!p || !dx) return GELIM_FAIL(GELIM_E_ARG, "plan_solve: null plan or x");
   if (src && src_ld < p->n + 1) return GELIM_FAIL(GELIM_E_ARG, "plan_solve: src_ld < n+1");
   hipStream_t s = (hipStream_t)stream;
-  if (!p->use_graph) return enqueue(p, src, src_ld, dx, bnorm, s);
+  if (!p->use_graph || p->big_la) return enqueue(p, src, src_ld, dx, bnorm, s);
   const bool hit = p->exec && p->k_src == src && p->k_ld == src_ld && p->k_dx == dx &&
                    p->k_bn == bnorm;
   if (!hit) {

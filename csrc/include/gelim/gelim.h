@@ -176,6 +176,11 @@ int gelim_gpu_leaf_factor(double* dA, int64_t lda, int64_t m, int64_t c0, int pi
                           int32_t* dpairs, int32_t* dinfo, void* stream);
 int gelim_gpu_laswp_trsm(double* dA, int64_t lda, int64_t c0, int64_t lend, int64_t rbeg, int64_t rend,
                          int64_t trsm_end, int64_t nrows, const int32_t* dpairs, void* stream);
+/* a whole outer panel's interchanges (nleaves leaf pair lists, `slot` ints
+ * apart, diagonals c0, c0 + 32, ...) on columns [lbeg, lend) and
+ * [rbeg, rend) of the n-row system at dA (row 0, column 0) */
+int gelim_gpu_laswp_panel(double* dA, int64_t lda, int64_t n, int64_t c0, int nleaves, const int32_t* dpairs,
+                          int64_t slot, int64_t lbeg, int64_t lend, int64_t rbeg, int64_t rend, void* stream);
 int gelim_gpu_gemm_update(double* dC, int64_t ldc, const double* dL,
                           int64_t ldl, const double* dU, int64_t ldu,
                           int64_t M, int64_t N, int64_t K, void* stream);

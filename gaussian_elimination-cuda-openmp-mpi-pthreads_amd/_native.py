@@ -73,6 +73,7 @@ _PROTOS = {
     "gelim_gpu_leaf_workspace_bytes": (_i64, []),
     "gelim_debug_leaf_stamps": (_int, [_vp, _i64, _i64, _vp, _vp, _vp]),
     "gelim_gpu_laswp_trsm": (_int, [_vp, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _vp, _vp]),
+    "gelim_gpu_laswp_panel": (_int, [_vp, _i64, _i64, _i64, _int, _vp, _i64, _i64, _i64, _i64, _i64, _vp]),
     "gelim_gpu_backsub": (_int, [_vp, _i64, _vp, _i64, _vp, _vp, _i64, _int, _vp]),
     "gelim_gauss_plan_create": (_vp, [_i64, _int, _int, _int, _int]),
     "gelim_gauss_plan_destroy": (None, [_vp]),

@@ -218,3 +218,61 @@ def test_memplus_blocked(gelim, cuda):
     xr = torch.linalg.solve(aug[:, :n], aug[:, n])
     err_ref = gelim.ops.gauss.error_metric(xr)
     assert err <= max(20 * err_ref, 1e-12), (err, err_ref)
+
+
+@pytest.mark.parametrize("la,reserve", [("0", "32"), ("1", "32"), ("1", "0"), ("1", "200")])
+@pytest.mark.parametrize("n", [700, 1500, 2600])
+def test_big_schedules_agree(gelim, cuda, monkeypatch, la, reserve, n):
+    """Serial (graph-captured) and lookahead (crit + CU-masked side stream)
+    schedules of the wide-panel engine, several outer panels each
+    (GELIM_BIG_TAIL=256): same pivots, so the same solution to rounding."""
+    monkeypatch.setenv("GELIM_BIG_TAIL", "256")
+    monkeypatch.setenv("GELIM_BIG_LOOKAHEAD", la)
+    monkeypatch.setenv("GELIM_BIG_RESERVE", reserve)
+    _check_solve(gelim, cuda, n, seed=n + 29)
+
+
+def test_big_lookahead_replays_identically(gelim, cuda, monkeypatch):
+    """The eager lookahead schedule is deterministic: replays are bitwise equal."""
+    monkeypatch.setenv("GELIM_BIG_TAIL", "512")
+    n = 3000
+    aug = gelim.random_system(n, seed=3, device=cuda)
+    s = gelim.GaussSolver(n, backend="hip", device=cuda)
+    x = s.solve(aug).clone()
+    for _ in range(3):
+        assert torch.equal(s.solve(aug), x)
+
+
+def test_laswp_panel_matches_sequential(gelim, cuda):
+    """laswp_panel = the leaves' pair lists applied in order (each list a
+    gather-then-scatter permutation), only on the requested column ranges."""
+    from gelim import _native
+    from gelim.utils.tensors import ptr, stream_handle
+
+    torch.manual_seed(4)
+    n, c0, nl, slot = 500, 96, 3, 1 + 4 * 32 + 3
+    ncols = n + 1
+    A = torch.randn(n, ncols + 1, dtype=torch.float64)
+    pairs = torch.zeros(nl * slot, dtype=torch.int32)
+    ref = A.clone()
+    lb, le, rb, re = 10, 80, 300, ncols
+    cols = list(range(lb, le)) + list(range(rb, re))
+    for l in range(nl):
+        base = c0 + 32 * l
+        m = n - base
+        sel = torch.randperm(m)[:50]
+        src = torch.arange(m)
+        src[sel] = sel[torch.randperm(50)]
+        pl = [(d, s) for d, s in enumerate(src.tolist()) if d != s][:64]
+        pairs[l * slot] = len(pl)
+        for e, (d, s) in enumerate(pl):
+            pairs[l * slot + 1 + 2 * e], pairs[l * slot + 2 + 2 * e] = d, s
+        old = ref.clone()
+        for d, s in pl:
+            ref[base + d, cols] = old[base + s, cols]
+    Ag = A.to(cuda)
+    rc = _native.lib().gelim_gpu_laswp_panel(ptr(Ag), A.shape[1], n, c0, nl, ptr(pairs.to(cuda)), slot, lb, le, rb,
+                                             re, stream_handle(cuda))
+    _native.check(rc, "laswp_panel")
+    torch.cuda.synchronize()
+    assert torch.equal(Ag.cpu(), ref)

@@ -33,7 +33,12 @@ constexpr int kBS = 64;
 constexpr int kMaxPersistBlocks = 256;
 constexpr unsigned long long kSpinTicks = 20000000ull;  // 200 ms at 100 MHz
 
-__device__ __forceinline__ int rowof(const int* perm, int i) { return perm ? perm[i] : i; }
+// Row of equation i; a row map entry outside [0, n) (a corrupt map, e.g. one
+// left stale by an aborted factorisation) is clamped, never dereferenced --
+// the persistent kernel reports it through its error word (code 7).
+__device__ __forceinline__ int rowof(const int* perm, int i, int n) {
+  return perm ? min(max(perm[i], 0), n - 1) : i;
+}
 
 __device__ __forceinline__ unsigned long long rtc() {
   unsigned long long t;
@@ -47,7 +52,7 @@ __global__ void copy_y_kernel(const T* __restrict__ U, int64_t ldu, const T* __r
                               double* __restrict__ bnorm, int n, int unit) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const int r = rowof(perm, i);
+  const int r = rowof(perm, i, n);
   const double v = (double)y[(int64_t)r * incy];
   yw[i] = v;
   if (bnorm) bnorm[i] = unit ? v : v / (double)U[(int64_t)r * ldu + i];
@@ -56,11 +61,11 @@ __global__ void copy_y_kernel(const T* __restrict__ U, int64_t ldu, const T* __r
 // Wave 0's copy of a diagonal block: lane l keeps equation i0+l's row
 // (columns i0..i0+nb) and the reciprocal of its diagonal.
 template <typename T>
-__device__ __forceinline__ void load_diag(const T* __restrict__ U, int64_t ldu, const int* perm, int i0,
+__device__ __forceinline__ void load_diag(const T* __restrict__ U, int64_t ldu, const int* perm, int n, int i0,
                                           int nb, int unit, double (&row)[kBS], double& rinv) {
   const int l = threadIdx.x & 63;
   const int lc = min(l, nb - 1);
-  const T* src = U + (int64_t)rowof(perm, i0 + lc) * ldu + i0;
+  const T* src = U + (int64_t)rowof(perm, i0 + lc, n) * ldu + i0;
 #pragma unroll
   for (int c = 0; c < kBS; ++c) row[c] = dev::load_sel(src + min(c, nb - 1), l < nb && c < nb);
   rinv = unit ? 1.0 : 1.0 / (double)src[lc];
@@ -101,7 +106,8 @@ __global__ __launch_bounds__(256) void backsub_persist_kernel(const T* __restric
   const int r0 = b * kBS, rows = min(kBS, n - r0);
   if (t < kBS) {
     const int i = r0 + min(t, rows - 1);
-    const int pr = rowof(perm, i);
+    const int pr = rowof(perm, i, n);
+    if (perm && perm[i] != pr) __hip_atomic_store(err, 7, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     prow[t] = pr;
     const double v = (double)y[(int64_t)pr * incy];
     acc[t] = v;
@@ -109,7 +115,7 @@ __global__ __launch_bounds__(256) void backsub_persist_kernel(const T* __restric
   }
   double drow[kBS];
   double rinv = 1.0;
-  if (wv == 0) load_diag<T>(U, ldu, perm, r0, rows, unit, drow, rinv);
+  if (wv == 0) load_diag<T>(U, ldu, perm, n, r0, rows, unit, drow, rinv);
   __syncthreads();
   // this wave's 16 equations of the block: their physical rows
   int pr16[16];
@@ -171,10 +177,10 @@ __global__ __launch_bounds__(64) void diag_solve_kernel(const T* __restrict__ U,
                                                         const int* __restrict__ perm,
                                                         double* __restrict__ yw,
                                                         double* __restrict__ x, int i0, int nb,
-                                                        int unit) {
+                                                        int unit, int n) {
   double row[kBS];
   double rinv;
-  load_diag<T>(U, ldu, perm, i0, nb, unit, row, rinv);
+  load_diag<T>(U, ldu, perm, n, i0, nb, unit, row, rinv);
   const int l = threadIdx.x & 63;
   const double xv = solve_diag(row, rinv, dev::load_sel(yw + i0 + min(l, nb - 1), l < nb), nb);
   if (l < nb) x[i0 + l] = xv;
@@ -188,7 +194,7 @@ __global__ __launch_bounds__(256) void backsub_step_kernel(const T* __restrict__
                                                            const int* __restrict__ perm,
                                                            double* __restrict__ yw,
                                                            double* __restrict__ x, int i0, int nb,
-                                                           int unit) {
+                                                           int unit, int n) {
   const int lane = threadIdx.x & 63;
   const int wv = threadIdx.x >> 6;
   const int p0 = i0 > kBS ? i0 - kBS : 0;  // the next diagonal block [p0, i0)
@@ -199,7 +205,7 @@ __global__ __launch_bounds__(256) void backsub_step_kernel(const T* __restrict__
 #pragma unroll
     for (int k = 0; k < kRows; ++k) {
       const int r = p0 + wv * kRows + k;
-      v[k] = dev::load_sel(U + (int64_t)rowof(perm, min(r, i0 - 1)) * ldu + i0 + min(lane, nb - 1),
+      v[k] = dev::load_sel(U + (int64_t)rowof(perm, min(r, i0 - 1), n) * ldu + i0 + min(lane, nb - 1),
                            lane < nb && r < i0) * xl;
     }
 #pragma unroll
@@ -212,7 +218,7 @@ __global__ __launch_bounds__(256) void backsub_step_kernel(const T* __restrict__
     if (wv == 0) {
       double row[kBS];
       double rinv;
-      load_diag<T>(U, ldu, perm, p0, i0 - p0, unit, row, rinv);
+      load_diag<T>(U, ldu, perm, n, p0, i0 - p0, unit, row, rinv);
       const int l = lane;
       const double xv = solve_diag(row, rinv, dev::load_sel(yw + p0 + min(l, i0 - p0 - 1), l < i0 - p0), i0 - p0);
       if (l < i0 - p0) x[p0 + l] = xv;
@@ -221,7 +227,7 @@ __global__ __launch_bounds__(256) void backsub_step_kernel(const T* __restrict__
   }
   const int nw = (gridDim.x - 1) * 4;
   for (int r = (blockIdx.x - 1) * 4 + wv; r < p0; r += nw) {
-    double v = dev::load_sel(U + (int64_t)rowof(perm, r) * ldu + i0 + min(lane, nb - 1), lane < nb) * xl;
+    double v = dev::load_sel(U + (int64_t)rowof(perm, r, n) * ldu + i0 + min(lane, nb - 1), lane < nb) * xl;
     v = dev::wave_sum(v);
     if (lane == 0) yw[r] -= v;
   }
@@ -239,7 +245,7 @@ int backsub_impl(const T* U, int64_t ldu, const T* y, int64_t incy, double* x, d
     // that still fits (a 16-byte multiple is the fast memset path)
     const size_t bytes = ((size_t)nblk + 1) * 4;
     const size_t rounded = (bytes + 15) / 16 * 16;
-    HIP_TRY(hipMemsetAsync(flags, 0, rounded <= (size_t)n * sizeof(double) ? rounded : bytes, s));
+    GELIM_TRY(zero_async(flags, rounded <= (size_t)n * sizeof(double) ? rounded : bytes, s));
     hipLaunchKernelGGL(backsub_persist_kernel<T>, dim3((unsigned)nblk), dim3(256), 0, s, U, ldu, y, incy,
                        perm, x, bnorm, (int)n, unit, flags, e);
     HIP_TRY(hipGetLastError());
@@ -250,14 +256,14 @@ int backsub_impl(const T* U, int64_t ldu, const T* y, int64_t incy, double* x, d
   HIP_TRY(hipGetLastError());
   int64_t i0 = (n - 1) / kBS * kBS;
   hipLaunchKernelGGL(diag_solve_kernel<T>, dim3(1), dim3(64), 0, s, U, ldu, perm, yw, x, (int)i0,
-                     (int)(n - i0), unit);
+                     (int)(n - i0), unit, (int)n);
   HIP_TRY(hipGetLastError());
   for (int64_t i1 = n; i0 > 0; i1 = i0, i0 -= kBS) {
     const int nb = (int)(i1 - i0);
     const int64_t rows = i0 > kBS ? i0 - kBS : 0;  // rows above the next block
     const int blocks = 1 + (int)std::min<int64_t>((rows + 3) / 4, 1024);
     hipLaunchKernelGGL(backsub_step_kernel<T>, dim3(blocks), dim3(256), 0, s, U, ldu, perm, yw, x,
-                       (int)i0, nb, unit);
+                       (int)i0, nb, unit, (int)n);
     HIP_TRY(hipGetLastError());
   }
   return GELIM_OK;

@@ -103,6 +103,15 @@ struct gelim_gauss_plan {
   hipStream_t big_side = nullptr;
   std::vector<hipEvent_t> big_ev;        // fork, fact[T], next[T], join
   hipGraphExec_t exec = nullptr;
+  hipGraph_t tpl = nullptr;              // template of exec (GELIM_GRAPH_KEEPTPL=1 keeps it alive)
+  // the graph is captured ONCE on plan-owned buffers: the input is staged
+  // into work and x / bnorm leave through xbuf / bnbuf, by eager copies
+  // outside it (GELIM_GRAPH_LEGACY=1: capture the caller's pointers and
+  // re-capture whenever they change -- see gelim_gauss_plan_solve)
+  bool legacy_graph = false, keep_tpl = false;
+  double* xbuf = nullptr;
+  double* bnbuf = nullptr;
+  hipGraphExec_t exec_bn[2] = {nullptr, nullptr};  // fixed-pointer graphs without / with bnorm
   const void* k_src = nullptr;
   int64_t k_ld = 0;
   void* k_dx = nullptr;
@@ -111,15 +120,50 @@ struct gelim_gauss_plan {
 
 namespace {
 
+// Retired graph executables are destroyed; GELIM_GRAPH_PARK=1 parks them
+// instead (never destroyed while the process runs) -- the experiment that
+// ruled exec destruction out as the cause of the cross-plan corruption
+// (profiles/graph_recapture.txt: it was the captured memset nodes).
+std::vector<hipGraphExec_t>& exec_graveyard() {
+  static std::vector<hipGraphExec_t> g;
+  return g;
+}
+
+void retire_exec(hipGraphExec_t e) {
+  if (!e) return;
+  static const bool park = [] {
+    const char* v = std::getenv("GELIM_GRAPH_PARK");
+    return v && std::atoi(v) != 0;
+  }();
+  if (park) exec_graveyard().push_back(e);
+  else (void)hipGraphExecDestroy(e);
+}
+
 constexpr int64_t kPairSlot = 72;  // 1 + 4*16 ints, padded
 
 // Hybrid hand-off: perm[i] = i for the fused part (rows already in LAPACK
 // order), split + piv[i] for the resident part (its pivot rows are physical
 // rows of the trailing block); the resident kernel's singular column and
 // hand-off error (info[2], info[3]) are folded into info[0], info[1].
+//
+// The resident part's row map is valid only when its kernel ran to the end
+// (info[3] == 0): after an aborted hand-off the entries are whatever the last
+// solve left (already offset by split), so they are replaced by the
+// identity and info[1] keeps the abort code; an entry outside the trailing
+// block is flagged as code 6.  Either way the back substitution never
+// follows a row index outside the system.
 __global__ void hybrid_perm_kernel(int* __restrict__ perm, int n, int split, int* __restrict__ info) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) perm[i] = i < split ? i : split + perm[i];
+  const bool aborted = info[3] != 0;
+  if (i < n) {
+    int v = i;
+    if (i >= split && !aborted) {
+      const int loc = perm[i];
+      if (loc >= 0 && loc < n - split) v = split + loc;
+      else atomicCAS(info + 1, 0, 6);
+    }
+    perm[i] = v;
+  }
   if (i == 0) {
     if (info[0] == 0 && info[2] != 0) info[0] = split + info[2];
     if (info[1] == 0 && info[3] != 0) info[1] = info[3];
@@ -185,7 +229,7 @@ int enqueue_big(gelim_gauss_plan* p, double* A, double* x, double* bnorm, hipStr
   hipEvent_t* ev_fact = la ? &p->big_ev[1] : nullptr;
   hipEvent_t* ev_next = la ? &p->big_ev[1 + T] : nullptr;
   hipEvent_t* ev_join = la ? &p->big_ev[1 + 2 * T] : nullptr;
-  HIP_TRY(hipMemsetAsync(p->big_ws, 0, big::workspace_bytes(), s));
+  GELIM_TRY(zero_async(p->big_ws, big::workspace_bytes(), s));
   if (la) {
     HIP_TRY(hipEventRecord(*ev_fork, s));
     HIP_TRY(hipStreamWaitEvent(side, *ev_fork, 0));
@@ -250,8 +294,8 @@ int enqueue(gelim_gauss_plan* p, const void* src, int64_t src_ld, void* dx, void
   const int64_t n = p->n, lda = p->lda;
   if (p->big_k > 0) {
     if (src)
-      HIP_TRY(hipMemcpy2DAsync(p->work, lda * 8, src, src_ld * 8, (n + 1) * 8, n, hipMemcpyDeviceToDevice, s));
-    HIP_TRY(hipMemsetAsync(p->info, 0, 16, s));
+      GELIM_TRY(copy2d_async(p->work, lda * 8, src, src_ld * 8, (n + 1) * 8, n, s));
+    GELIM_TRY(zero_async(p->info, 16, s));
     return enqueue_big(p, static_cast<double*>(p->work), static_cast<double*>(dx), static_cast<double*>(bnorm), s);
   }
   if (p->algo == GELIM_GPU_BLOCKED && p->resident) {
@@ -259,16 +303,15 @@ int enqueue(gelim_gauss_plan* p, const void* src, int64_t src_ld, void* dx, void
     // leaves U rows at their physical positions and the pivot row of every
     // column in piv; the persistent back substitution follows through piv.
     double* A = static_cast<double*>(p->work);
-    HIP_TRY(hipMemsetAsync(p->info, 0, 16, s));
+    GELIM_TRY(zero_async(p->info, 16, s));
     GELIM_TRY(rlu_factor(static_cast<const double*>(src), src_ld, A, lda, n, p->pivot, p->piv, p->info,
                          p->rws, s));
     return backsub_f64(A, lda, A + n, lda, static_cast<double*>(dx), static_cast<double*>(bnorm), n, 0,
                        p->yw, s, p->piv, p->info + 1);
   }
   if (src)
-    HIP_TRY(hipMemcpy2DAsync(p->work, lda * p->eb, src, src_ld * p->eb, (n + 1) * p->eb, n,
-                             hipMemcpyDeviceToDevice, s));
-  HIP_TRY(hipMemsetAsync(p->info, 0, 16, s));
+    GELIM_TRY(copy2d_async(p->work, lda * p->eb, src, src_ld * p->eb, (n + 1) * p->eb, n, s));
+  GELIM_TRY(zero_async(p->info, 16, s));
   if (p->algo == GELIM_GPU_BLOCKED && p->fused) {
     // One fused launch per step (lu_step): workgroup 0 finishes step i-1 on
     // panel i's columns and factors panel i while the other workgroups apply
@@ -407,6 +450,8 @@ extern "C" gelim_gauss_plan* gelim_gauss_plan_create(int64_t n, int algo, int pi
   p->pivot = pivot;
   p->eb = dtype_bytes;
   p->use_graph = use_graph != 0;
+  if (const char* e = std::getenv("GELIM_GRAPH_LEGACY")) p->legacy_graph = std::atoi(e) != 0;
+  if (const char* e = std::getenv("GELIM_GRAPH_KEEPTPL")) p->keep_tpl = std::atoi(e) != 0;
   const int64_t align = 64 / dtype_bytes;  // 64-byte rows
   // the wide-panel engine's GEMMs read 16-byte chunks that may reach one
   // column past b: keep at least one padding column
@@ -486,14 +531,12 @@ extern "C" gelim_gauss_plan* gelim_gauss_plan_create(int64_t n, int algo, int pi
     const std::string sched = e ? e : "auto";
     const int64_t lim = sched == "resident" ? gelim::rlu_max_n() : sched == "auto" ? 1024 : 0;
     p->resident = algo == GELIM_GPU_BLOCKED && n <= lim && !p->lookahead;
-    // GELIM_HYBRID: 0 turns the hybrid off (pure fused schedule); any other
-    // value keeps the validated 1024-row tail (the resident LU's 2-slot
-    // regime).  Other tails (512 / 640 / 768 / 896 / 1152: 1- and 4-slot
-    // regimes, in-place) are not offered: an A/B sweep over them ended in an
-    // illegal-address fault (profiles/hybrid_tail_sweep.txt) and none of them
-    // is covered by a GPU test.
+    // GELIM_HYBRID: rows of the trailing system handed to the resident LU
+    // (default 1024, its 2-slot regime; 0 = off, pure fused schedule; any
+    // other value up to 2048, rounded to a panel boundary -- 1, 2 and 4
+    // register slots, each covered by a GPU test)
     const char* eh = std::getenv("GELIM_HYBRID");
-    const int64_t tail = (eh && std::atoll(eh) == 0) ? 0 : 1024;
+    const int64_t tail = eh ? std::max<int64_t>(0, std::min<int64_t>(gelim::rlu_max_n(), std::atoll(eh))) : 1024;
     if (algo == GELIM_GPU_BLOCKED && !p->resident && p->fused && tail > 0 && n > tail &&
         tail <= gelim::rlu_max_n() && sched != "fused")
       p->split = n - tail;  // rounded to a panel boundary below
@@ -537,7 +580,11 @@ extern "C" gelim_gauss_plan* gelim_gauss_plan_create(int64_t n, int algo, int pi
 
 extern "C" void gelim_gauss_plan_destroy(gelim_gauss_plan* p) {
   if (!p) return;
-  if (p->exec) (void)hipGraphExecDestroy(p->exec);
+  retire_exec(p->exec);
+  for (auto& e : p->exec_bn) retire_exec(e);
+  if (p->tpl) (void)hipGraphDestroy(p->tpl);
+  (void)hipFree(p->xbuf);
+  (void)hipFree(p->bnbuf);
   if (p->cap) (void)hipStreamDestroy(p->cap);
   if (p->side) (void)hipStreamDestroy(p->side);
   if (p->big_side) (void)hipStreamDestroy(p->big_side);
@@ -572,16 +619,16 @@ extern "C" int gelim_gauss_plan_solve(gelim_gauss_plan* p, const void* src, int6
   if (src && src_ld < p->n + 1) return GELIM_FAIL(GELIM_E_ARG, "plan_solve: src_ld < n+1");
   hipStream_t s = (hipStream_t)stream;
   if (!p->use_graph || p->big_la) return enqueue(p, src, src_ld, dx, bnorm, s);
-  const bool hit = p->exec && p->k_src == src && p->k_ld == src_ld && p->k_dx == dx &&
-                   p->k_bn == bnorm;
-  if (!hit) {
-    if (p->exec) {
-      HIP_TRY(hipGraphExecDestroy(p->exec));
-      p->exec = nullptr;
+  auto capture = [&](const void* csrc, int64_t cld, void* cdx, void* cbn) -> int {
+    retire_exec(p->exec);
+    p->exec = nullptr;
+    if (p->tpl) {
+      HIP_TRY(hipGraphDestroy(p->tpl));
+      p->tpl = nullptr;
     }
     hipGraph_t g = nullptr;
     HIP_TRY(hipStreamBeginCapture(p->cap, hipStreamCaptureModeThreadLocal));
-    int rc = enqueue(p, src, src_ld, dx, bnorm, p->cap);
+    int rc = enqueue(p, csrc, cld, cdx, cbn, p->cap);
     hipError_t e = hipStreamEndCapture(p->cap, &g);
     if (rc != 0) {
       if (g) (void)hipGraphDestroy(g);
@@ -589,14 +636,44 @@ extern "C" int gelim_gauss_plan_solve(gelim_gauss_plan* p, const void* src, int6
     }
     HIP_TRY(e);
     e = hipGraphInstantiate(&p->exec, g, nullptr, nullptr, 0);
-    (void)hipGraphDestroy(g);
+    if (p->keep_tpl) p->tpl = g;
+    else (void)hipGraphDestroy(g);
     HIP_TRY(e);
-    p->k_src = src;
-    p->k_ld = src_ld;
-    p->k_dx = dx;
-    p->k_bn = bnorm;
+    return GELIM_OK;
+  };
+  if (p->legacy_graph) {
+    // round-1 behaviour: the caller's pointers are baked into the graph and
+    // every change re-captures.  With two or more plans alive this corrupts
+    // results and info words on ROCm 7.2 (profiles/graph_recapture.txt)
+    const bool hit = p->exec && p->k_src == src && p->k_ld == src_ld && p->k_dx == dx && p->k_bn == bnorm;
+    if (!hit) {
+      GELIM_TRY(capture(src, src_ld, dx, bnorm));
+      p->k_src = src;
+      p->k_ld = src_ld;
+      p->k_dx = dx;
+      p->k_bn = bnorm;
+    }
+    HIP_TRY(hipGraphLaunch(p->exec, s));
+    return GELIM_OK;
   }
-  HIP_TRY(hipGraphLaunch(p->exec, s));
+  // one graph per plan (and per bnorm on/off), on plan-owned buffers only
+  const int64_t n = p->n;
+  if (!p->xbuf) {
+    HIP_TRY(hipMalloc((void**)&p->xbuf, sizeof(double) * n));
+    HIP_TRY(hipMalloc((void**)&p->bnbuf, sizeof(double) * n));
+  }
+  const bool want_bn = bnorm != nullptr;
+  hipGraphExec_t& ex = p->exec_bn[want_bn ? 1 : 0];
+  if (!ex) {  // captured once, destroyed only with the plan
+    GELIM_TRY(capture(nullptr, 0, p->xbuf, want_bn ? p->bnbuf : nullptr));
+    ex = p->exec;
+    p->exec = nullptr;
+  }
+  if (src)
+    GELIM_TRY(gelim::copy2d_async(p->work, p->lda * p->eb, src, src_ld * p->eb, (n + 1) * p->eb, n, s));
+  HIP_TRY(hipGraphLaunch(ex, s));
+  GELIM_TRY(gelim::copy2d_async(dx, 0, p->xbuf, 0, sizeof(double) * n, 1, s));
+  if (want_bn) GELIM_TRY(gelim::copy2d_async(bnorm, 0, p->bnbuf, 0, sizeof(double) * n, 1, s));
   return GELIM_OK;
 }
 
@@ -605,6 +682,11 @@ extern "C" int gelim_gauss_plan_info(gelim_gauss_plan* p, void* stream) {
   int h[4] = {0, 0, 0, 0};
   HIP_TRY(hipMemcpyAsync(h, p->info, 16, hipMemcpyDeviceToHost, (hipStream_t)stream));
   HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
+  if (h[1] == 8) return GELIM_FAIL(GELIM_E_HIP, "resident LU: an updater read a pivot row outside the system (code 8)");
+  if (h[1] == 6 || h[1] == 7)
+    return GELIM_FAIL(GELIM_E_HIP, std::string("row map out of range (code ") + std::to_string(h[1]) +
+                                       (h[1] == 6 ? "): resident LU pivot outside its block"
+                                                  : "): back substitution row map outside the system"));
   if (h[1] != 0)
     return GELIM_FAIL(GELIM_E_HIP, "GPU hand-off timed out (code " + std::to_string(h[1]) +
                                        "): workgroups of a persistent kernel were not co-resident");

@@ -39,6 +39,7 @@
 
 #include <algorithm>
 #include <cstdint>
+#include <cstdlib>
 #include <utility>
 
 #include "device_common.h"
@@ -71,6 +72,8 @@ struct Args {
   double* pbuf;       // [np][16][16]: each panel's pivot rows (L11 | U11)
   double* ubuf;       // [np][np + 1][16][16]: U12 of (step, strip), column-major
   double* hbuf;       // [np + 1][R*8][NT] double2: strips handed to the engine
+  int* pslot;         // [np][32]: each panel's 16 pivot rows on a 128-byte line of its own
+  int pslot_mode;     // 1: updaters read the pivots from pslot, 0: from piv
   unsigned long long* stamps;  // diagnostics (null in production): realtime per phase
 };
 
@@ -527,6 +530,7 @@ __device__ __forceinline__ void engine(const Args& g, Shared& sh) {
     for (int c = 0; c < kW; ++c) a[i][c] = rp[min(c, n - 1)];
   }
   const __amdgpu_buffer_rsrc_t rpiv = rsrc(g.piv, (uint32_t)n * 4);
+  const __amdgpu_buffer_rsrc_t rps = rsrc(g.pslot, (uint32_t)np * 128);
   for (int j = 0; j < np; ++j) {
     const int k0 = kW * j;
     const int w = min(kW, n - k0);
@@ -581,7 +585,10 @@ __device__ __forceinline__ void engine(const Args& g, Shared& sh) {
       const int pj = sh.sel[J];
       st64(rp, t * 8, J < w ? v : 0.0);
       if (J < w && c >= J && c < w) g.work[(int64_t)pj * g.ldw + k0 + c] = v;
-      if (J < w && c == 0) st32(rpiv, (k0 + J) * 4, pj);
+      if (J < w && c == 0) {
+        st32(rpiv, (k0 + J) * 4, pj);
+        st32(rps, (j * 32 + J) * 4, pj);
+      }
     }
     const __amdgpu_buffer_rsrc_t rl = rsrc(g.lbuf + (int64_t)j * (kPanelBytes / 8), kPanelBytes);
     stamp(g, j * 8 + 2);
@@ -677,13 +684,21 @@ __device__ __forceinline__ void updater(const Args& g, Shared& sh, int s) {
     for (int c = 0; c < kW; ++c) sr[i][c] = rp[min(c, ws - 1)];
   }
   const __amdgpu_buffer_rsrc_t rpiv = rsrc(g.piv, (uint32_t)n * 4);
+  const __amdgpu_buffer_rsrc_t rps = rsrc(g.pslot, (uint32_t)np * 128);
   for (int j = 0; j <= last; ++j) {
     if (!wait_flag(&g.flags[j], g.info + 1, sh, j & 1, 2)) return;
     stamp(g, 8 * np + 2 * (s * np + j));
     const int k0 = kW * j;
     const int wp = min(kW, n - k0);
     // lane J (mod 16) holds the pivot row of column k0 + J
-    const int pv = ld32(rpiv, (k0 + min(lane & 15, wp - 1)) * 4);
+    int pv = g.pslot_mode ? ld32(rps, (j * 32 + min(lane & 15, wp - 1)) * 4)
+                          : ld32(rpiv, (k0 + min(lane & 15, wp - 1)) * 4);
+    // a pivot row outside the system is a broken hand-off: report it (code
+    // 8) and never store through it
+    if (pv < 0 || pv >= n) {
+      __hip_atomic_store(g.info + 1, 8, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      pv = 0;
+    }
     const __amdgpu_buffer_rsrc_t rp = rsrc(g.pbuf + (int64_t)j * 256, 256 * 8);
     if (t < 128) {
       const u32x4 v = ld128(rp, t * 16, 0);
@@ -761,7 +776,7 @@ __global__ __launch_bounds__(NT, 2) void rlu_kernel(Args g) {
 // Workspace of the resident LU for order n (bytes, 256-aligned pieces).
 struct Layout {
   int R = 0, np = 0;
-  size_t flags = 0, lbuf = 0, pbuf = 0, ubuf = 0, hbuf = 0, total = 0;
+  size_t flags = 0, lbuf = 0, pbuf = 0, ubuf = 0, hbuf = 0, pslot = 0, total = 0;
 };
 
 Layout layout(int64_t n) {
@@ -782,6 +797,8 @@ Layout layout(int64_t n) {
   off += up(sizeof(double) * 256 * (size_t)L.np * (L.np + 1));
   L.hbuf = off;
   off += up(panel * (L.np + 1));
+  L.pslot = off;
+  off += up((size_t)128 * L.np);
   L.total = off;
   return L;
 }
@@ -817,8 +834,13 @@ int rlu_factor(const double* src, int64_t lds, double* work, int64_t ldw, int64_
   a.pbuf = reinterpret_cast<double*>(base + L.pbuf);
   a.ubuf = reinterpret_cast<double*>(base + L.ubuf);
   a.hbuf = reinterpret_cast<double*>(base + L.hbuf);
+  a.pslot = reinterpret_cast<int*>(base + L.pslot);
+  {
+    const char* e = std::getenv("GELIM_RLU_PSLOT");
+    a.pslot_mode = e ? std::atoi(e) : 1;
+  }
   a.stamps = stamps;
-  HIP_TRY(hipMemsetAsync(a.flags, 0, L.lbuf - L.flags, s));
+  GELIM_TRY(zero_async(a.flags, L.lbuf - L.flags, s));
   const dim3 grid((unsigned)(L.np + 1)), block(NT);
   const bool part = mode == GELIM_PIVOT_PARTIAL;
   if (L.R == 1) {

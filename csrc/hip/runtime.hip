@@ -11,6 +11,17 @@
 namespace gelim {
 namespace {
 
+__global__ __launch_bounds__(256) void copy2d_words_kernel(unsigned* __restrict__ d, int64_t dp,
+                                                          const unsigned* __restrict__ sp, int64_t spp, int64_t w) {
+  const unsigned* srow = sp + (int64_t)blockIdx.y * spp;
+  unsigned* drow = d + (int64_t)blockIdx.y * dp;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < w; i += (int64_t)gridDim.x * 256) drow[i] = srow[i];
+}
+
+__global__ __launch_bounds__(256) void zero_words_kernel(unsigned* __restrict__ p, int64_t nwords) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < nwords; i += (int64_t)gridDim.x * 256) p[i] = 0u;
+}
+
 template <typename T>
 __global__ void init_synthetic_kernel(T* __restrict__ A, int64_t lda, int n) {
   // A[i][j] = 2*min(i+1, j+1), b[i] = i in column n (P1i:59-69)
@@ -67,6 +78,30 @@ __global__ __launch_bounds__(1024) void error_kernel(const double* __restrict__ 
 }
 
 }  // namespace
+
+int copy2d_async(void* dst, size_t dpitch, const void* src, size_t spitch, size_t width, size_t rows,
+                 struct ihipStream_t* s) {
+  if (width == 0 || rows == 0) return GELIM_OK;
+  if ((width | dpitch | spitch) % 4 || ((uintptr_t)dst | (uintptr_t)src) % 4)
+    return GELIM_FAIL(GELIM_E_ARG, "copy2d_async: not 4-byte aligned");
+  if (rows > 65535) return GELIM_FAIL(GELIM_E_ARG, "copy2d_async: more than 65535 rows");
+  const int64_t w = (int64_t)(width / 4);
+  const unsigned bx = (unsigned)std::min<int64_t>((w + 255) / 256, 64);
+  hipLaunchKernelGGL(copy2d_words_kernel, dim3(bx, (unsigned)rows), dim3(256), 0, s, static_cast<unsigned*>(dst),
+                     (int64_t)(dpitch / 4), static_cast<const unsigned*>(src), (int64_t)(spitch / 4), w);
+  HIP_TRY(hipGetLastError());
+  return GELIM_OK;
+}
+
+int zero_async(void* p, size_t bytes, struct ihipStream_t* s) {
+  if (bytes == 0) return GELIM_OK;
+  if (bytes % 4) return GELIM_FAIL(GELIM_E_ARG, "zero_async: size not a multiple of 4");
+  const int64_t nw = (int64_t)(bytes / 4);
+  const unsigned blocks = (unsigned)std::min<int64_t>((nw + 255) / 256, 1024);
+  hipLaunchKernelGGL(zero_words_kernel, dim3(blocks), dim3(256), 0, s, static_cast<unsigned*>(p), nw);
+  HIP_TRY(hipGetLastError());
+  return GELIM_OK;
+}
 
 int init_synthetic_f64(double* A, int64_t lda, int64_t n, hipStream_t s) {
   dim3 grid((unsigned)((n + 1 + 255) / 256), (unsigned)n);

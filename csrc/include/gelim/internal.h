@@ -12,6 +12,15 @@ namespace gelim {
 // Thread-local error message behind gelim_last_error().
 void set_error(const std::string& msg);
 int fail(int code, const char* file, int line, const std::string& msg);
+// Zero `bytes` (a multiple of 4) of device memory with a kernel.  Used in
+// place of hipMemsetAsync everywhere a solve may be graph-captured: memset
+// nodes of captured graphs were the part of a graph that plan lifecycle
+// operations corrupted on ROCm 7.2 (profiles/graph_recapture.txt).
+int zero_async(void* p, size_t bytes, struct ihipStream_t* s);
+// Row-major 2D copy (rows x width bytes, width a multiple of 4) by a kernel,
+// for the same reason (no memcpy nodes in captured graphs).
+int copy2d_async(void* dst, size_t dpitch, const void* src, size_t spitch, size_t width, size_t rows,
+                 struct ihipStream_t* s);
 
 }  // namespace gelim
 

@@ -105,17 +105,49 @@ def test_hybrid_matches_pure_fused(gelim, cuda, monkeypatch, n):
     assert gelim.ops.gauss.error_metric(x_h) < 1e-7
 
 
-@pytest.mark.parametrize("value", ["512", "1152"])
-def test_hybrid_tail_knob_pinned(gelim, cuda, monkeypatch, value):
-    """Only the validated 1024-row tail is selectable: any non-zero
-    GELIM_HYBRID value runs exactly the default schedule (bitwise)."""
+@pytest.mark.parametrize("tail", [512, 640, 768, 896, 1152, 1536])
+def test_hybrid_tail_sizes(gelim, cuda, monkeypatch, tail):
+    """Every hybrid tail (resident LU in place on the trailing system: 1, 2
+    and 4 register slots) against torch.linalg.solve, replayed three times
+    (bitwise equal) with info checked each time."""
     n = 2048
-    aug = gelim.random_system(n, seed=77, device=cuda)
-    x_d = gelim.GaussSolver(n, backend="hip", device=cuda).solve(aug, check=True).clone()
-    monkeypatch.setenv("GELIM_HYBRID", value)
-    x_v = gelim.GaussSolver(n, backend="hip", device=cuda).solve(aug, check=True)
-    torch.cuda.synchronize()
-    assert torch.equal(x_d, x_v)
+    monkeypatch.setenv("GELIM_HYBRID", str(tail))
+    aug = gelim.random_system(n, seed=tail, device=cuda)
+    s = gelim.GaussSolver(n, backend="hip", device=cuda)
+    x = s.solve(aug, check=True).clone()
+    ref = torch.linalg.solve(aug[:, :n], aug[:, n])
+    assert torch.allclose(x, ref, rtol=1e-8, atol=1e-8 * n), (x - ref).abs().max().item()
+    for _ in range(3):
+        assert torch.equal(s.solve(aug, check=True), x)
+
+
+@pytest.mark.parametrize("n", [1100, 1600, 2048])
+def test_resident_schedule_four_slots(gelim, cuda, monkeypatch, n):
+    """GELIM_SCHEDULE=resident for 1024 < n <= 2048: the 4-slot resident LU
+    (the one variant with register spills) from its own input copy."""
+    monkeypatch.setenv("GELIM_SCHEDULE", "resident")
+    aug = gelim.random_system(n, seed=n + 5, device=cuda)
+    s = gelim.GaussSolver(n, backend="hip", device=cuda)
+    x = s.solve(aug, check=True)
+    ref = torch.linalg.solve(aug[:, :n], aug[:, n])
+    assert torch.allclose(x, ref, rtol=1e-8, atol=1e-8 * n), (x - ref).abs().max().item()
+    assert torch.equal(s.solve(aug, check=True), x)
+
+
+def test_hybrid_tails_interleaved(gelim, cuda, monkeypatch):
+    """The round-1 fault scenario: plans with different tails alive at once,
+    their graphs replayed interleaved on one stream; every replay bitwise
+    equal to the plan's first solve, info clean."""
+    n = 2048
+    aug = gelim.random_system(n, seed=99, device=cuda)
+    plans = []
+    for tail in (1024, 896, 768, 640, 512, 1152):
+        monkeypatch.setenv("GELIM_HYBRID", str(tail))
+        s = gelim.GaussSolver(n, backend="hip", device=cuda)
+        plans.append((s, s.solve(aug, check=True).clone()))
+    for _ in range(3):
+        for s, x in plans:
+            assert torch.equal(s.solve(aug, check=True), x)
 
 
 @pytest.mark.parametrize("zero_col", [100, 1500])

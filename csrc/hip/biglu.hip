@@ -465,6 +465,8 @@ struct SwapArgs {
   int64_t lda;
   int c0, lbeg, lend, rbeg, rend, trsm_end, nrows;
   const int* pairs;
+  const double* L;  // L11 (unit lower, LW x LW) of the TRSM, leading dimension ldl
+  int64_t ldl;
 };
 
 __global__ __launch_bounds__(kSwThreads) void laswp_trsm_kernel(SwapArgs g) {
@@ -486,7 +488,7 @@ __global__ __launch_bounds__(kSwThreads) void laswp_trsm_kernel(SwapArgs g) {
 #pragma unroll
   for (int k = 0; k < LW * LW / kSwThreads; ++k) {
     const int e = lane + kSwThreads * k;
-    lv[k] = g.A[(int64_t)(e / LW) * lda + g.c0 + (e % LW)];
+    lv[k] = g.L[(int64_t)(e / LW) * g.ldl + (e % LW)];
   }
   const bool pok = lane < cnt && pd >= 0 && pd < g.nrows && ps >= 0 && ps < g.nrows;
   pd = pok ? pd : -1;
@@ -685,15 +687,21 @@ int leaf_factor(double* A, int64_t lda, int64_t m, int64_t c0, int mode, int* ip
 
 // Row movement of a leaf (pairs, may be null) on columns [lbeg, lend) and
 // [rbeg, rend) of rows [c0, ...), TRSM of rows [c0, c0 + LW) on the right
-// columns below trsm_end.  A: row c0, column 0.
+// columns below trsm_end.  A: row c0, column 0.  L11 defaults to the leaf
+// (row c0, column c0 of A); the distributed solver passes the broadcast
+// panel's copy.
 int laswp_trsm(double* A, int64_t lda, int64_t c0, int64_t lbeg, int64_t lend, int64_t rbeg, int64_t rend,
-               int64_t trsm_end, int64_t nrows, const int* pairs, hipStream_t s) {
+               int64_t trsm_end, int64_t nrows, const int* pairs, hipStream_t s, const double* L, int64_t ldl) {
   lend = std::max(lend, lbeg);
   rend = std::max(rend, rbeg);
   const int64_t cols = (lend - lbeg) + (rend - rbeg);
   if (cols <= 0) return GELIM_OK;
   if (nrows < LW) return GELIM_FAIL(GELIM_E_ARG, "laswp_trsm: fewer rows than the leaf width");
-  SwapArgs a{A, lda, (int)c0, (int)lbeg, (int)lend, (int)rbeg, (int)rend, (int)trsm_end, (int)nrows, pairs};
+  if (L == nullptr) {  // L11 is the leaf itself: row c0, column c0 of A
+    L = A + c0;
+    ldl = lda;
+  }
+  SwapArgs a{A, lda, (int)c0, (int)lbeg, (int)lend, (int)rbeg, (int)rend, (int)trsm_end, (int)nrows, pairs, L, ldl};
   hipLaunchKernelGGL(laswp_trsm_kernel, dim3((unsigned)((cols + kSwThreads - 1) / kSwThreads)), dim3(kSwThreads), 0,
                      s, a);
   HIP_TRY(hipGetLastError());
@@ -780,5 +788,5 @@ extern "C" int64_t gelim_gpu_leaf_workspace_bytes(void) { return (int64_t)gelim:
 
 extern "C" int gelim_gpu_laswp_trsm(double* dA, int64_t lda, int64_t c0, int64_t lend, int64_t rbeg, int64_t rend,
                                     int64_t trsm_end, int64_t nrows, const int32_t* dpairs, void* stream) {
-  return gelim::big::laswp_trsm(dA, lda, c0, 0, lend, rbeg, rend, trsm_end, nrows, dpairs, (hipStream_t)stream);
+  return gelim::big::laswp_trsm(dA, lda, c0, 0, lend, rbeg, rend, trsm_end, nrows, dpairs, (hipStream_t)stream, nullptr, 0);
 }

@@ -1,0 +1,104 @@
+// Native per-block steps of the distributed Gauss solver
+// (parallel/dist_gauss.py): the owner's factorisation of one outer panel
+// and every rank's application of a broadcast panel to its own columns.
+//
+// What it replaces: the reference's MPI master/worker elimination
+// (OpenMP_and_MPI/gauss_mpi/gauss_internal_input.c:124-255), where rank 0
+// ships whole rows to the workers and back at every pivot.  Here the matrix
+// is column block-cyclic (blocks of D columns, D a multiple of the 32-column
+// leaf) and resident: the owner factors its m x D panel with the wide-panel
+// engine's multi-workgroup leaves (biglu.hip) and broadcasts
+// [panel | leaf pair lists] once; every rank then applies it to its trailing
+// columns -- the leaves' row movement in one launch, U12 = L11^-1 A12 by
+// 32-row blocks, and the trailing update as one K = D fp64 MFMA GEMM
+// (dgemm.hip).  Each call issues the whole launch sequence from C++ on the
+// caller's stream (one ctypes crossing per block step instead of dozens).
+//
+// Storage: a rank's slab holds ALL n rows of its local columns, row-major
+// (row 0 = global row 0), leading dimension ld; local column c of the slab is
+// some global column, the pair lists use global row numbers relative to each
+// leaf's diagonal.  n must be a multiple of 32 (dist_gauss.py pads the system
+// with an identity block).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdint>
+
+#include "gelim/internal.h"
+
+namespace gelim {
+int dgemm(double* C, int64_t ldc, const double* A, int64_t lda, const double* B, int64_t ldb, int64_t M,
+          int64_t N, int64_t K, double alpha, hipStream_t s);
+namespace big {
+int leaf_width();
+int leaf_factor(double* A, int64_t lda, int64_t m, int64_t c0, int mode, int* ipiv, int* pairs, int* info,
+                void* ws, int set, hipStream_t s, unsigned long long* stamps = nullptr);
+int laswp_trsm(double* A, int64_t lda, int64_t c0, int64_t lbeg, int64_t lend, int64_t rbeg, int64_t rend,
+               int64_t trsm_end, int64_t nrows, const int* pairs, hipStream_t s, const double* L, int64_t ldl);
+int laswp_panel(double* A, int64_t lda, int64_t n, int64_t c0, int nleaves, const int* pairs, int64_t slot,
+                int64_t lbeg, int64_t lend, int64_t rbeg, int64_t rend, hipStream_t s);
+}  // namespace big
+}  // namespace gelim
+
+namespace {
+constexpr int64_t kLW = 32;
+constexpr int64_t kSlot = 1 + 4 * 32 + 3;  // ints per leaf pair list (plan.hip's kBigPairSlot)
+}  // namespace
+
+extern "C" int64_t gelim_dist_pair_slot(void) { return kSlot; }
+
+// Factor rows [k, n) x local columns [lc, lc + wg) of the slab A in place
+// (wg a multiple of 32).  Leaf l's pivots go to ipiv[k + 32 l + J] (global
+// rows), its net row movement to pairs + l * slot; info[0] = 1 + the first
+// zero-pivot column (global).  ws: the leaf exchange workspace, zeroed before
+// the first leaf of a solve; leaf0: the solve's running leaf counter.
+extern "C" int gelim_dist_panel_factor(double* A, int64_t lda, int64_t n, int64_t k, int64_t lc, int64_t wg,
+                                       int pivot, int32_t* ipiv, int32_t* pairs, int32_t* info, void* ws, int leaf0,
+                                       void* stream) {
+  using namespace gelim;
+  hipStream_t s = (hipStream_t)stream;
+  if (wg <= 0 || wg % kLW || n % kLW || k + wg > n || (lc & 1) || (lda & 1))
+    return GELIM_FAIL(GELIM_E_ARG, "dist_panel_factor: widths must be multiples of 32 (even offsets)");
+  for (int64_t l = 0; l * kLW < wg; ++l) {
+    const int64_t c0 = k + l * kLW, col = lc + l * kLW;
+    int* pr = pairs + l * kSlot;
+    GELIM_TRY(big::leaf_factor(A + c0 * lda + col, lda, n - c0, c0, pivot, ipiv, pr, info, ws, leaf0 + (int)l, s));
+    // the leaf's row movement on the panel's other columns, TRSM of its U
+    // rows on the panel columns right of it
+    GELIM_TRY(big::laswp_trsm(A + c0 * lda, lda, col, lc, col, col + kLW, lc + wg, lc + wg, n - c0, pr, s, nullptr,
+                              0));
+    const int64_t c1 = col + kLW, r1 = c0 + kLW;
+    if (c1 < lc + wg && r1 < n)
+      GELIM_TRY(dgemm(A + r1 * lda + c1, lda, A + r1 * lda + col, lda, A + c0 * lda + c1, lda, n - r1, lc + wg - c1,
+                      kLW, -1.0, s));
+  }
+  return GELIM_OK;
+}
+
+// Apply a factored panel (its rows [k, n) as a row-major (n - k) x wg block L
+// with leading dimension ldl, and its leaf pair lists) to local columns
+// [cb, ce) of the slab C: the leaves' row movement, U12 = L11^-1 A12 on rows
+// [k, k + wg), A22 -= L21 U12 on rows [k + wg, n).
+extern "C" int gelim_dist_panel_apply(double* C, int64_t ldc, int64_t n, int64_t k, int64_t cb, int64_t ce,
+                                      const double* L, int64_t ldl, int64_t wg, const int32_t* pairs,
+                                      void* stream) {
+  using namespace gelim;
+  hipStream_t s = (hipStream_t)stream;
+  if (ce <= cb) return GELIM_OK;
+  if (wg <= 0 || wg % kLW || n % kLW || k + wg > n || (cb & 1) || (ldc & 1) || (ldl & 1))
+    return GELIM_FAIL(GELIM_E_ARG, "dist_panel_apply: widths must be multiples of 32 (even offsets)");
+  const int nl = (int)(wg / kLW);
+  GELIM_TRY(big::laswp_panel(C, ldc, n, k, nl, pairs, kSlot, 0, 0, cb, ce, s));
+  for (int64_t j = 0; j < nl; ++j) {
+    const int64_t r = k + j * kLW;
+    GELIM_TRY(big::laswp_trsm(C + r * ldc, ldc, 0, 0, 0, cb, ce, ce, n - r, nullptr, s, L + (j * kLW) * ldl + j * kLW,
+                              ldl));
+    if (j + 1 < nl)
+      GELIM_TRY(dgemm(C + (r + kLW) * ldc + cb, ldc, L + ((j + 1) * kLW) * ldl + j * kLW, ldl, C + r * ldc + cb, ldc,
+                      wg - (j + 1) * kLW, ce - cb, kLW, -1.0, s));
+  }
+  if (k + wg < n)
+    GELIM_TRY(dgemm(C + (k + wg) * ldc + cb, ldc, L + wg * ldl, ldl, C + k * ldc + cb, ldc, n - k - wg, ce - cb, wg,
+                    -1.0, s));
+  return GELIM_OK;
+}

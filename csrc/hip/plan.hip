@@ -45,7 +45,8 @@ int64_t max_rows();
 int leaf_factor(double* A, int64_t lda, int64_t m, int64_t c0, int mode, int* ipiv, int* pairs, int* info,
                 void* ws, int set, hipStream_t s, unsigned long long* stamps = nullptr);
 int laswp_trsm(double* A, int64_t lda, int64_t c0, int64_t lbeg, int64_t lend, int64_t rbeg, int64_t rend,
-               int64_t trsm_end, int64_t nrows, const int* pairs, hipStream_t s);
+               int64_t trsm_end, int64_t nrows, const int* pairs, hipStream_t s, const double* L = nullptr,
+               int64_t ldl = 0);
 int laswp_panel(double* A, int64_t lda, int64_t n, int64_t c0, int nleaves, const int* pairs, int64_t slot,
                 int64_t lbeg, int64_t lend, int64_t rbeg, int64_t rend, hipStream_t s);
 int tail_gemv(const double* A, int64_t lda, int64_t n, int64_t K, const double* x, double* y, double* bnorm,

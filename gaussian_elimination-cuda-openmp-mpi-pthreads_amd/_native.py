@@ -73,6 +73,9 @@ _PROTOS = {
     "gelim_gpu_leaf_workspace_bytes": (_i64, []),
     "gelim_debug_leaf_stamps": (_int, [_vp, _i64, _i64, _vp, _vp, _vp]),
     "gelim_gpu_laswp_trsm": (_int, [_vp, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _vp, _vp]),
+    "gelim_dist_pair_slot": (_i64, []),
+    "gelim_dist_panel_factor": (_int, [_vp, _i64, _i64, _i64, _i64, _i64, _int, _vp, _vp, _vp, _vp, _int, _vp]),
+    "gelim_dist_panel_apply": (_int, [_vp, _i64, _i64, _i64, _i64, _i64, _vp, _i64, _i64, _vp, _vp]),
     "gelim_gpu_laswp_panel": (_int, [_vp, _i64, _i64, _i64, _int, _vp, _i64, _i64, _i64, _i64, _i64, _vp]),
     "gelim_gpu_backsub": (_int, [_vp, _i64, _vp, _i64, _vp, _vp, _i64, _int, _vp]),
     "gelim_gauss_plan_create": (_vp, [_i64, _int, _int, _int, _int]),

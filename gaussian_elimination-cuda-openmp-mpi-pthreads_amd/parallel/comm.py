@@ -25,6 +25,16 @@ import torch
 import torch.distributed as dist
 
 
+class _Done:
+    """Handle of a collective that needed no communication."""
+
+    def wait(self) -> bool:
+        return True
+
+    def is_completed(self) -> bool:
+        return True
+
+
 @dataclass
 class Communicator:
     rank: int = 0
@@ -42,6 +52,14 @@ class Communicator:
         if self.distributed:
             dist.broadcast(t, src=self.global_rank(src), group=self.group)
         return t
+
+    def broadcast_async(self, t: torch.Tensor, src: int):
+        """Non-blocking broadcast: returns a handle whose wait() makes the
+        current stream wait for the data (RCCL runs on its own stream, after
+        the work already queued on the current one)."""
+        if self.distributed:
+            return dist.broadcast(t, src=self.global_rank(src), group=self.group, async_op=True)
+        return _Done()
 
     def all_reduce(self, t: torch.Tensor, op: str = "sum") -> torch.Tensor:
         if self.distributed:

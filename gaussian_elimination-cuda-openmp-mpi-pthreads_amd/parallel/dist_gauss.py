@@ -29,8 +29,23 @@ last to first:
   replicated on every rank (the reference's "allgather of the solution").
   => n/S small all_reduces.
 
-Runs on CPU tensors with gloo as well (the native CPU building blocks), which
-is how the multi-rank path is tested without GPUs.
+GPU ranks use the wide-panel engine (D = 256 by default, a multiple of the
+32-column leaf; the system is padded to a multiple of 32 with an identity
+block, which never wins a pivot search): the owner factors its panel with
+the multi-workgroup leaves (csrc/hip/dist_panel.hip, one native call per
+step), the broadcast carries [panel | leaf pair lists], and the per-block
+sequence has lookahead 1 -- the owner of block g+1 applies panel g to that
+block first, factors it and starts its broadcast, which then travels over
+xGMI while every rank (the owner too) applies panel g to the rest of its
+columns:
+
+  rank o(g+1):  [apply g -> block g+1] [factor g+1] [bcast g+1 ...........]
+  every rank:                                       [apply g -> the rest  ]
+                                                                 [wait g+1]
+
+Runs on CPU tensors with gloo as well (the native CPU building blocks, the
+original D = 64 sub-panel path), which is how the multi-rank path is tested
+without GPUs.
 """
 from __future__ import annotations
 
@@ -86,36 +101,78 @@ class ColumnLayout:
         return min(q * self.D, self.nloc(r))
 
 
-class DistributedGauss:
-    """Column block-cyclic distributed solver of one n x n system."""
+LEAF = 32  # leaf width of the wide-panel engine (csrc/hip/biglu.hip)
 
-    def __init__(self, comm: Communicator, n: int, block: int = 64, pivot: str = "partial"):
+
+class DistributedGauss:
+    """Column block-cyclic distributed solver of one n x n system.
+
+    block: columns per block (GPU default 256, a multiple of 32; CPU 64).
+    lookahead: overlap the next panel's broadcast with the trailing update
+    (GPU path; default on with more than one rank -- on one rank there is
+    nothing to hide and the split apply costs 50.8 -> 59.4 ms at n = 8192;
+    off while checkpointing, whose snapshots need quiet block boundaries)."""
+
+    def __init__(self, comm: Communicator, n: int, block: int | None = None, pivot: str = "partial",
+                 lookahead: bool | None = None):
+        if lookahead is None:
+            lookahead = comm.world_size > 1
+        self.device = comm.device
+        self.wide = self.device.type == "cuda"
+        if block is None:
+            block = 256 if self.wide else 64
         if block < 1:
             raise ValueError("block must be >= 1")
-        self.comm, self.n, self.pivot = comm, n, pivot
-        self.layout = ColumnLayout(n, comm.world_size, block)
-        self.device = comm.device
+        if self.wide and block % LEAF:
+            raise ValueError(f"GPU blocks are multiples of the {LEAF}-column leaf (got {block})")
+        self.comm, self.n, self.pivot, self.lookahead = comm, n, pivot, lookahead
+        # GPU: the system is padded to a multiple of the leaf width
+        self.n_pad = -(-n // LEAF) * LEAF if self.wide else n
+        self.layout = ColumnLayout(self.n_pad, comm.world_size, block)
         r = comm.rank
         self.nloc = self.layout.nloc(r)
         self.ld = padded_ld(self.nloc + 1)
         D = self.layout.D
-        self._buf = torch.empty((n + 1) * D, dtype=torch.float64, device=self.device)
-        self._piv = torch.zeros(D + 64, dtype=torch.int32, device=self.device)
         self._info = torch.zeros(4, dtype=torch.int32, device=self.device)
+        if self.wide:
+            lib = _native.lib()
+            self._slot = int(lib.gelim_dist_pair_slot())
+            nl = D // LEAF
+            self._npd = -(-nl * self._slot // 2)  # pair lists, in doubles
+            self._bufs = [torch.empty(self.n_pad * D + self._npd, dtype=torch.float64, device=self.device)
+                          for _ in range(2)]
+            self._pairs = torch.zeros(nl * self._slot, dtype=torch.int32, device=self.device)
+            self._ipiv = torch.zeros(self.n_pad + 64, dtype=torch.int32, device=self.device)
+            self._ws = torch.zeros(int(lib.gelim_gpu_leaf_workspace_bytes()) // 8, dtype=torch.float64,
+                                   device=self.device)
+        else:
+            self._buf = torch.empty((n + 1) * D, dtype=torch.float64, device=self.device)
+            self._piv = torch.zeros(D + 64, dtype=torch.int32, device=self.device)
 
     # -- data placement -----------------------------------------------------
     def empty_local(self) -> torch.Tensor:
-        return torch.zeros((self.n, self.ld), dtype=torch.float64, device=self.device)
+        return torch.zeros((self.n_pad, self.ld), dtype=torch.float64, device=self.device)
+
+    def _pad_identity(self, loc: torch.Tensor) -> None:
+        """Rows / columns n .. n_pad-1 of the padded system: identity."""
+        L, n = self.layout, self.n
+        for g in L.local_blocks(self.comm.rank):
+            c, w = L.local_col(g), L.width(g)
+            for j in range(max(g * L.D, n), g * L.D + w):
+                loc[j, c + j - g * L.D] = 1.0
 
     def scatter_from_global(self, aug: torch.Tensor) -> torch.Tensor:
         """Local storage from a full augmented system present on every rank
         (tests / small problems)."""
-        L = self.layout
+        L, n = self.layout, self.n
         loc = self.empty_local()
         for g in L.local_blocks(self.comm.rank):
             c, w = L.local_col(g), L.width(g)
-            loc[:, c:c + w] = aug[:, g * L.D:g * L.D + w].to(self.device)
-        loc[:, self.nloc] = aug[:, self.n].to(self.device)
+            wr = max(0, min(w, n - g * L.D))
+            if wr:
+                loc[:n, c:c + wr] = aug[:, g * L.D:g * L.D + wr].to(self.device)
+        loc[:n, self.nloc] = aug[:, n].to(self.device)
+        self._pad_identity(loc)
         return loc
 
     def generate_random(self, seed: int = 0) -> torch.Tensor:
@@ -126,9 +183,13 @@ class DistributedGauss:
         loc = self.empty_local()
         lib = _native.lib()
         idx = torch.empty(self.nloc, dtype=torch.float64, device=self.device)
+        idx.zero_()
         for g in L.local_blocks(self.comm.rank):
             c, w = L.local_col(g), L.width(g)
-            view = loc[:, c:c + w]
+            w = max(0, min(w, n - g * L.D))  # real (unpadded) columns of the block
+            if w == 0:
+                continue
+            view = loc[:n, c:c + w]
             if self.device.type == "cuda":
                 _native.check(lib.gelim_gpu_init_random_block(ptr(view), loc.stride(0), 0, n, g * L.D, w,
                                                               seed, stream_handle(self.device)), "init_random_block")
@@ -137,9 +198,11 @@ class DistributedGauss:
                 lib.gelim_init_random_block_f64(ptr(tmp), w, 0, n, g * L.D, w, seed)
                 view.copy_(tmp)
             idx[c:c + w] = torch.arange(g * L.D + 1, g * L.D + w + 1, dtype=torch.float64, device=self.device)
-        b = loc[:, :self.nloc] @ idx if self.nloc else torch.zeros(n, dtype=torch.float64, device=self.device)
+        b = loc[:, :self.nloc] @ idx if self.nloc else torch.zeros(self.n_pad, dtype=torch.float64,
+                                                                   device=self.device)
         self.comm.all_reduce(b)
         loc[:, self.nloc] = b
+        self._pad_identity(loc)
         return loc
 
     # -- factorisation -------------------------------------------------------
@@ -179,6 +242,8 @@ class DistributedGauss:
         its last complete generation (loc is overwritten with the saved slab).
         fault_at_block / GELIM_FAULT_AT_BLOCK: raise InjectedFault on entering
         that block (fault injection for the resume tests)."""
+        if self.wide:
+            return self._factor_wide(loc, ckpt, resume, fault_at_block)
         L, n, r = self.layout, self.n, self.comm.rank
         self._info.zero_()
         g0 = 0
@@ -212,17 +277,101 @@ class DistributedGauss:
                 if m > so + ws:
                     lu.gemm_update(C[so + ws:], buf[so + ws:m, so:so + ws], C[so:so + ws])
 
+    # -- GPU: wide-panel engine with lookahead -----------------------------------
+    def _panel_factor(self, loc: torch.Tensor, g: int, buf: torch.Tensor, leaf: int) -> int:
+        """Owner: factor block g (up to date) in place and pack [panel |
+        pair lists] into buf; returns the next leaf counter."""
+        L, n = self.layout, self.n_pad
+        k, wg, lc = g * L.D, L.width(g), L.local_col(g)
+        m = n - k
+        lib = _native.lib()
+        _native.check(lib.gelim_dist_panel_factor(ptr(loc), loc.stride(0), n, k, lc, wg, lu._pivot_code(self.pivot),
+                                                  ptr(self._ipiv), ptr(self._pairs), ptr(self._info), ptr(self._ws),
+                                                  leaf, stream_handle(self.device)), "dist_panel_factor")
+        buf[:m * wg].view(m, wg).copy_(loc[k:, lc:lc + wg])
+        nl = wg // LEAF
+        buf[m * wg:m * wg + self._npd].view(torch.int32)[:nl * self._slot].copy_(self._pairs[:nl * self._slot])
+        return leaf + nl
+
+    def _bsize(self, g: int) -> int:
+        L = self.layout
+        return (self.n_pad - g * L.D) * L.width(g) + self._npd
+
+    def _panel_apply(self, loc: torch.Tensor, g: int, buf: torch.Tensor, cb: int, ce: int) -> None:
+        """Panel g (from buf) applied to local columns [cb, ce)."""
+        if ce <= cb:
+            return
+        L, n = self.layout, self.n_pad
+        k, wg = g * L.D, L.width(g)
+        m = n - k
+        pairs = buf[m * wg:m * wg + self._npd]
+        _native.check(_native.lib().gelim_dist_panel_apply(ptr(loc), loc.stride(0), n, k, cb, ce, ptr(buf), wg, wg,
+                                                           ptr(pairs), stream_handle(self.device)),
+                      "dist_panel_apply")
+
+    def _factor_wide(self, loc: torch.Tensor, ckpt: Checkpointer | None, resume: bool,
+                     fault_at_block: int | None) -> None:
+        L, r, comm = self.layout, self.comm.rank, self.comm
+        self._info.zero_()
+        self._ws.zero_()
+        g0 = 0
+        if ckpt is not None and resume:
+            st = ckpt.load()
+            if st is not None:
+                loc.copy_(st.loc.to(loc.device))
+                self._info.copy_(st.info.to(self._info.device))
+                g0 = st.block
+        la = self.lookahead and ckpt is None
+        end = self.nloc + 1  # local columns + b
+        leaf = 0
+        B = self._bufs
+        if g0 < L.nblocks:
+            o = L.owner(g0)
+            if r == o:
+                leaf = self._panel_factor(loc, g0, B[g0 & 1], leaf)
+            h = comm.broadcast_async(B[g0 & 1][:self._bsize(g0)], src=o)
+        for g in range(g0, L.nblocks):
+            if la:
+                maybe_inject_fault(g, r, fault_at_block)
+            h.wait()
+            buf = B[g & 1]
+            c0 = L.first_local_col_after(g, r)
+            nxt = g + 1 < L.nblocks
+            if nxt and la:
+                # lookahead: block g+1 first (its owner), its broadcast under the rest
+                o1 = L.owner(g + 1)
+                if r == o1:
+                    w1 = L.width(g + 1)
+                    self._panel_apply(loc, g, buf, c0, c0 + w1)
+                    leaf = self._panel_factor(loc, g + 1, B[(g + 1) & 1], leaf)
+                    c0 += w1
+                h = comm.broadcast_async(B[(g + 1) & 1][:self._bsize(g + 1)], src=o1)
+            self._panel_apply(loc, g, buf, c0, end)
+            if nxt and not la:
+                maybe_inject_fault(g + 1, r, fault_at_block)
+                if ckpt is not None and ckpt.due(g + 1):
+                    ckpt.save(g + 1, loc, self._info)
+                o1 = L.owner(g + 1)
+                if r == o1:
+                    leaf = self._panel_factor(loc, g + 1, B[(g + 1) & 1], leaf)
+                h = comm.broadcast_async(B[(g + 1) & 1][:self._bsize(g + 1)], src=o1)
+
     def info(self) -> int:
-        """First zero-pivot column + 1 over all ranks (0 = non-singular)."""
+        """First zero-pivot column + 1 over all ranks (0 = non-singular): each
+        rank's own first one, combined with a min over the ranks that have
+        one (0 maps to a sentinel past every column)."""
         v = self._info[:1].clone().to(torch.int64)
-        self.comm.all_reduce(v, "max")
-        return int(v.item())
+        sentinel = self.n_pad + 1
+        v = torch.where(v == 0, torch.full_like(v, sentinel), v)
+        self.comm.all_reduce(v, "min")
+        val = int(v.item())
+        return 0 if val == sentinel else val
 
     # -- back substitution ----------------------------------------------------
     def backsolve(self, loc: torch.Tensor) -> torch.Tensor:
         """U x = y with U column-distributed, y replicated; returns x on every
         rank."""
-        L, n, P, D, r = self.layout, self.n, self.comm.world_size, self.layout.D, self.comm.rank
+        L, n, P, D, r = self.layout, self.layout.n, self.comm.world_size, self.layout.D, self.comm.rank
         S = P * D
         nsuper = math.ceil(n / S)
         # one all_gather of every super-block's diagonal columns
@@ -260,4 +409,4 @@ class DistributedGauss:
         self.factor_(loc, ckpt, resume, fault_at_block)
         if self.info() != 0:
             raise _native.SingularMatrixError(_native.E_SINGULAR, "The matrix is singular")
-        return self.backsolve(loc)
+        return self.backsolve(loc)[:self.n]

@@ -105,6 +105,12 @@ class EmulatedComm(Communicator):
         w.wait()
         return t
 
+    def broadcast_async(self, t: torch.Tensor, src: int):
+        """Emulated ranks rendezvous on the host, so the "async" broadcast
+        completes before it returns (no overlap to emulate on one stream)."""
+        self.broadcast(t, src)
+        return _Done()
+
     def all_reduce(self, t: torch.Tensor, op: str = "sum") -> torch.Tensor:
         if not self.distributed:
             return t

@@ -73,3 +73,40 @@ def test_emulated_checkpoint_resume_gpu(tmp_path, cuda):
     resumed = run(tmp_path / "b", resume=True)
     for a, b in zip(clean, resumed):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("P,n,block,la", [(1, 3000, 256, True), (1, 3000, 256, False), (3, 2600, 256, True),
+                                          (4, 1000, 96, True), (2, 1111, 64, False)])
+def test_emulated_dist_gauss_wide(gelim, cuda, P, n, block, la):
+    """The GPU distributed path (wide-panel leaves, native panel steps,
+    lookahead broadcast) against the single-GPU solver: padded n, partial
+    last blocks, with and without lookahead."""
+    def body(c):
+        dg = DistributedGauss(c, n, block=block, lookahead=la)
+        return dg.solve_(dg.generate_random(seed=21))
+
+    xs = run_emulated(P, body, device=cuda, timeout_s=120)
+    ref = gelim.solve(gelim.random_system(n, seed=21, device=cuda), backend="hip")
+    for x in xs:
+        assert x.shape == (n,)
+        assert torch.equal(x, xs[0])
+        assert torch.allclose(x, ref, rtol=1e-8, atol=1e-8 * n)
+
+
+def test_emulated_dist_gauss_singular_min_rank(gelim, cuda):
+    """Two zero columns owned by different ranks: info reports the FIRST
+    one (min over ranks, not max)."""
+    n, block, P = 600, 64, 3
+
+    def body(c):
+        dg = DistributedGauss(c, n, block=block)
+        aug = gelim.random_system(n, seed=8, device=cuda)
+        aug[:, 70] = 0.0   # block 1 (rank 1)
+        aug[:, 450] = 0.0  # block 7 (rank 1) -- and 130 on rank 2 below
+        aug[:, 130] = 0.0  # block 2 (rank 2)
+        loc = dg.scatter_from_global(aug)
+        dg.factor_(loc)
+        return dg.info()
+
+    infos = run_emulated(P, body, device=cuda, timeout_s=120)
+    assert infos == [71] * P

@@ -9,13 +9,24 @@ best 0.509428 s; matmul 2048^2 CUDA V2 end-to-end 0.114906 s.
 One step = one complete solve of a fresh random 2048^2 system on every GPU:
 the pristine system is copied into the solver's working buffer (the
 elimination is in place), eliminated with the blocked LU (register-resident
-panel + fp64 MFMA trailing GEMM) and back-substituted, all replayed from one
-hipGraph.  N GPUs = N ranks (torchrun), each solving its own system per step
-(weak scaling, "dp" over independent systems); the step time is the MAX over
-ranks and `value` is that wall time.  Data: synthetic random U[-1,1) matrices
-(b = A (1..n)), generated on device; weights/checkpoints do not apply.
+panel + fp64 MFMA trailing GEMM) and back-substituted.  N GPUs = N ranks
+(torchrun), each solving its own system per step (weak scaling, "dp" over
+independent systems); the step time is the MAX over ranks and `value` is
+that wall time.  Data: synthetic random U[-1,1) matrices (b = A (1..n)),
+generated on device; weights/checkpoints do not apply.
 
-  python bench.py [--gpus N --steps K --warmup W] [--n 2048] [--extras 0|1]
+Sections after the headline (first-class fields of the same line, each timed
+between device syncs + barriers, max over ranks):
+  matmul_2048           2048^2 fp32, reference timer scope, warm + cold first call
+  dist_gauss_8192(_s)   ONE 8192^2 system over ALL N ranks (strong scaling)
+  dist_matmul_16384(_s) 16384^2 fp32 over ALL N ranks (strong scaling)
+  gauss_8192_1gpu(_s)   one 8192^2 system per GPU on the single-GPU solver
+  hip_pivot_2048        the per-pivot algorithm (fp64, fp32)
+  external_matrices     the reference's .dat matrices vs its best OpenMP times
+  host_seq              sequential denominators (stored unless --measure-seq;
+                        the field says which)
+
+  python bench.py [--gpus N --steps K --warmup W] [--n 2048] [--headline-only]
 
 Output: ONE JSON line on rank 0.
 """
@@ -45,14 +56,42 @@ def parse():
     p.add_argument("--backend", default="hip", choices=["hip", "hip-pivot"])
     p.add_argument("--graph", type=int, default=0, help="replay the solve from a hipGraph (1) or launch eagerly (0)")
     p.add_argument("--no-matmul", action="store_true")
-    p.add_argument("--extras", type=int, default=None,
-                   help="also time the distributed 8192^2 solve and 16384^2 ring matmul "
-                        "(default: on when N > 1; bounded by a watchdog)")
-    p.add_argument("--extras-budget", type=float, default=240.0,
-                   help="seconds the extras may take before the headline line is printed without them")
+    p.add_argument("--headline-only", action="store_true",
+                   help="skip the distributed / 8192 / hip-pivot / external-matrix sections")
+    p.add_argument("--budget", type=float, default=900.0,
+                   help="seconds the sections after the headline may take before the line is printed without "
+                        "the missing ones (a hung collective never costs the headline)")
     p.add_argument("--measure-seq", action="store_true",
                    help="time the reference sequential loops on this host (slow)")
     return p.parse_args()
+
+
+EXTERNAL_OPENMP_BEST_S = {  # BASELINE.md, OpenMP external, best over threads (OpenMP_and_MPI/Report.pdf p.6-7)
+    "jpwh_991": 0.084672, "orsreg_1": 0.600996, "sherman5": 1.957547, "saylr4": 2.956282, "sherman3": 11.584218,
+}
+
+
+def _timed(comm, torch, dev, fn, reps: int = 1) -> float:
+    """Wall time of `reps` calls of fn, bracketed by device sync + barrier on
+    both sides, MAX over ranks."""
+    torch.cuda.synchronize(dev)
+    comm.barrier()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        fn()
+    torch.cuda.synchronize(dev)
+    comm.barrier()
+    t = torch.tensor([(time.perf_counter() - t0) / reps], dtype=torch.float64, device=dev)
+    comm.all_reduce(t, "max")
+    return t.item()
+
+
+def _section(out: dict, key: str, fn) -> None:
+    """Run one bench section; a failure is recorded, never fatal."""
+    try:
+        out[key] = fn()
+    except Exception as e:  # noqa: BLE001
+        out[key] = {"error": repr(e)[:300]}
 
 
 def main() -> None:
@@ -70,7 +109,25 @@ def main() -> None:
     rank, N = comm.rank, comm.world_size
     n = args.n
 
-    # -- Gauss: one independent system per GPU --------------------------------
+    # a watchdog prints whatever has been measured if a section hangs (a
+    # stuck collective), so the headline line is never lost
+    import threading
+
+    result: dict = {}
+    printed = threading.Event()
+
+    def emit() -> None:
+        if rank == 0 and not printed.is_set():
+            printed.set()
+            print(json.dumps(result), flush=True)
+
+    def watchdog() -> None:
+        result["watchdog"] = f"sections after the headline did not finish within {args.budget:.0f} s"
+        emit()
+        sys.stdout.flush()
+        os._exit(0)
+
+    # -- headline: one independent 2048^2 system per GPU ----------------------
     src = gelim.random_system(n, seed=1234 + rank, device=dev)
     solver = gelim.GaussSolver(n, backend=args.backend, pivot="partial", device=dev, use_graph=bool(args.graph))
     x = None
@@ -92,103 +149,207 @@ def main() -> None:
     err = torch.tensor([gelim.ops.gauss.error_metric(x)], dtype=torch.float64, device=dev)
     comm.all_reduce(err, "max")
     info = solver.info()
+    solver.close()
+    del src, x
 
-    # -- matmul 2048^2 fp32 (reference timer semantics) ------------------------
-    mm = None
+    result.update({
+        "metric": "wall-clock sec per 2048x2048 Gauss-elim solve (fp64, partial pivoting, "
+                  "elimination + back-substitution) [BASELINE: wall-clock sec + speedup-vs-sequential, "
+                  "2048x2048 Gauss-elim & matmul]",
+        "value": step_s,
+        "unit": "s",
+        "n_gpus": N,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": step_s * 1e3,
+        "higher_is_better": False,
+        "scaling": "weak",
+        "vs_baseline": step_s / BASELINE_GAUSS_S,
+        "speedup_vs_baseline": BASELINE_GAUSS_S / step_s,
+        "dtype": "fp64 (Gauss, reference precision); fp32 (matmul)",
+        "data": "synthetic random U[-1,1) systems generated on device, b = A(1..n); reference .dat matrices "
+                "for external_matrices",
+        "config": {"model": f"gauss_elim_{n}x{n}_partial_pivot_{args.backend}", "global_batch": N,
+                   "seq_len": n, "parallelism": f"dp{N} (one independent system per GPU per step)"},
+        "throughput_solves_per_s": N / step_s,
+        "gflops_per_gpu": (2.0 / 3.0) * n ** 3 / step_s * 1e-9,
+        "max_error": err.item(),
+        "singular": info != 0,
+    })
+    timer = threading.Timer(args.budget, watchdog)
+    timer.daemon = True
+    timer.start()
+
     if not args.no_matmul:
-        A, B = gelim.ops.matmul.reference_inputs(2048)
-        A, B = A.pin_memory(), B.pin_memory()
-        Ch = torch.empty_like(A).pin_memory()
-        model = gelim.MatMul("mfma", dev)
-        for _ in range(2):
-            model.run_reference_style(A, B, Ch)
-        runs = [model.run_reference_style(A, B, Ch) for _ in range(5)]
-        e2e = sorted(r.end_to_end_s for r in runs)[len(runs) // 2]
-        ker = sorted(r.kernel_s for r in runs)[len(runs) // 2]
-        ref = A.double() @ B.double()
-        rel = ((Ch.double() - ref).abs().max() / ref.abs().max()).item()
-        # same timer scope, transfers overlapped with the GEMM in row chunks
-        for _ in range(2):
-            model.run_pipelined(A, B, Ch)
-        pruns = [model.run_pipelined(A, B, Ch) for _ in range(5)]
-        pe2e = sorted(r.end_to_end_s for r in pruns)[len(pruns) // 2]
-        prel = ((Ch.double() - ref).abs().max() / ref.abs().max()).item()
-        best = min(e2e, pe2e)
-        mm = {"n": 2048, "end_to_end_s": best, "end_to_end_serial_s": e2e, "end_to_end_pipelined_s": pe2e,
-              "kernel_s": ker, "kernel_tflops": 2 * 2048 ** 3 / ker * 1e-12,
-              "vs_reference_cuda_v2": BASELINE_MATMUL_S / best, "max_rel_err": max(rel, prel)}
+        _section(result, "matmul_2048", lambda: bench_matmul(gelim, torch, dev))
+    if not args.headline_only:
+        # strong scaling over ALL ranks: the BASELINE.json multi-GPU configs
+        _section(result, "dist_gauss_8192", lambda: bench_dist_gauss(comm, gelim, torch, 8192))
+        _section(result, "dist_matmul_16384", lambda: bench_dist_matmul(comm, gelim, torch, 16384))
+        # single-GPU large systems (each rank its own: weak)
+        _section(result, "gauss_8192_1gpu", lambda: bench_single(comm, gelim, torch, 8192, seed=77 + rank))
+        _section(result, "hip_pivot_2048", lambda: bench_pivot(comm, gelim, torch, n))
+        _section(result, "external_matrices", lambda: bench_external(comm, gelim, torch))
+    for key, short in (("dist_gauss_8192", "dist_gauss_8192_s"), ("dist_matmul_16384", "dist_matmul_16384_s"),
+                       ("gauss_8192_1gpu", "gauss_8192_1gpu_s")):
+        v = result.get(key)
+        if isinstance(v, dict) and "time_s" in v:
+            result[short] = v["time_s"]
 
-    # -- speedup vs the reference's sequential loops on THIS host --------------
+    # -- speedup vs the reference's sequential loops --------------------------
     seq = None
     if args.measure_seq and rank == 0:
         seq = measure_host_seq(n)
+        seq["source"] = "measured in this run on this host"
     elif HOST_SEQ_FILE.exists():
         seq = json.loads(HOST_SEQ_FILE.read_text())
-
-    solver.close()
-    out = None
-    if rank == 0:
-        out = {
-            "metric": "wall-clock sec per 2048x2048 Gauss-elim solve (fp64, partial pivoting, "
-                      "elimination + back-substitution) [BASELINE: wall-clock sec + speedup-vs-sequential, "
-                      "2048x2048 Gauss-elim & matmul]",
-            "value": step_s,
-            "unit": "s",
-            "n_gpus": N,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": step_s * 1e3,
-            "higher_is_better": False,
-            "scaling": "weak",
-            "vs_baseline": step_s / BASELINE_GAUSS_S,
-            "speedup_vs_baseline": BASELINE_GAUSS_S / step_s,
-            "dtype": "fp64 (Gauss, reference precision); fp32 (matmul)",
-            "data": "synthetic random U[-1,1) systems generated on device, b = A(1..n)",
-            "config": {"model": f"gauss_elim_{n}x{n}_partial_pivot_{args.backend}", "global_batch": N,
-                       "seq_len": n, "parallelism": f"dp{N} (one independent system per GPU per step)"},
-            "throughput_solves_per_s": N / step_s,
-            "gflops_per_gpu": (2.0 / 3.0) * n ** 3 / step_s * 1e-9,
-            "max_error": err.item(),
-            "singular": info != 0,
-            "matmul_2048": mm,
-        }
-        if seq:
-            out["host_seq"] = seq
-            if "gauss_2048_s" in seq and n == 2048:
-                out["speedup_vs_seq"] = seq["gauss_2048_s"] / step_s
-            if mm and "matmul_2048_s" in seq:
-                mm["speedup_vs_seq_end_to_end"] = seq["matmul_2048_s"] / mm["end_to_end_s"]
-                mm["speedup_vs_seq_kernel"] = seq["matmul_2048_s"] / mm["kernel_s"]
-
-    # -- distributed configs of BASELINE.json (N > 1), after the headline
-    #    timing; a watchdog prints the headline line without them if the
-    #    collectives do not finish in time, so they can never cost the line
-    want_extras = (N > 1) if args.extras is None else bool(args.extras)
-    if want_extras and N > 1:
-        import threading
-
-        printed = threading.Event()
-
-        def emit(extras: dict) -> None:
-            if rank == 0 and not printed.is_set():
-                printed.set()
-                out["extras"] = extras
-                print(json.dumps(out), flush=True)
-
-        def watchdog() -> None:
-            emit({"error": f"extras did not finish within {args.extras_budget:.0f} s"})
-            sys.stdout.flush()
-            os._exit(0)
-
-        timer = threading.Timer(args.extras_budget, watchdog)
-        timer.daemon = True
-        timer.start()
-        extras = run_extras(comm, gelim, torch)
-        timer.cancel()
-        emit(extras)
-    elif rank == 0:
-        print(json.dumps(out), flush=True)
+        seq["source"] = (f"STORED: {HOST_SEQ_FILE.relative_to(ROOT)} (measured {seq.get('measured_at', '?')} on "
+                         f"{seq.get('host', '?')}), not re-measured in this run; --measure-seq re-measures")
+    if seq and rank == 0:
+        result["host_seq"] = seq
+        if "gauss_2048_s" in seq and n == 2048:
+            result["speedup_vs_seq"] = seq["gauss_2048_s"] / step_s
+        mm = result.get("matmul_2048")
+        if isinstance(mm, dict) and "end_to_end_s" in mm and "matmul_2048_s" in seq:
+            mm["speedup_vs_seq_end_to_end"] = seq["matmul_2048_s"] / mm["end_to_end_s"]
+            mm["speedup_vs_seq_kernel"] = seq["matmul_2048_s"] / mm["kernel_s"]
+    timer.cancel()
+    emit()
     C.destroy()
+
+
+def bench_matmul(gelim, torch, dev) -> dict:
+    """2048^2 fp32 matmul with the reference's timer scope (allocation, H2D,
+    kernel, D2H, free).  cold = the very first call of the process (module
+    load, first allocations); warm = median of 5 after 2 warmups."""
+    A, B = gelim.ops.matmul.reference_inputs(2048)
+    A, B = A.pin_memory(), B.pin_memory()
+    Ch = torch.empty_like(A).pin_memory()
+    model = gelim.MatMul("mfma", dev)
+    cold = model.run_reference_style(A, B, Ch).end_to_end_s
+    for _ in range(2):
+        model.run_reference_style(A, B, Ch)
+    runs = [model.run_reference_style(A, B, Ch) for _ in range(5)]
+    e2e = sorted(r.end_to_end_s for r in runs)[len(runs) // 2]
+    ker = sorted(r.kernel_s for r in runs)[len(runs) // 2]
+    ref = A.double() @ B.double()
+    rel = ((Ch.double() - ref).abs().max() / ref.abs().max()).item()
+    for _ in range(2):
+        model.run_pipelined(A, B, Ch)
+    pruns = [model.run_pipelined(A, B, Ch) for _ in range(5)]
+    pe2e = sorted(r.end_to_end_s for r in pruns)[len(pruns) // 2]
+    prel = ((Ch.double() - ref).abs().max() / ref.abs().max()).item()
+    best = min(e2e, pe2e)
+    return {"n": 2048, "end_to_end_s": best, "end_to_end_serial_s": e2e, "end_to_end_pipelined_s": pe2e,
+            "end_to_end_cold_first_call_s": cold, "kernel_s": ker, "kernel_tflops": 2 * 2048 ** 3 / ker * 1e-12,
+            "vs_reference_cuda_v2": BASELINE_MATMUL_S / best,
+            "vs_reference_cuda_v2_cold": BASELINE_MATMUL_S / cold, "max_rel_err": max(rel, prel)}
+
+
+def bench_dist_gauss(comm, gelim, torch, n: int) -> dict:
+    """The 8192^2 system distributed over ALL ranks (strong scaling; column
+    block-cyclic, wide-panel leaves, RCCL broadcast with lookahead); second
+    solve timed."""
+    from gelim.parallel import DistributedGauss
+
+    dev = comm.device
+    dg = DistributedGauss(comm, n)
+    holder = {}
+
+    def run():
+        holder["x"] = dg.solve_(holder.pop("loc"))
+
+    for _ in range(2):
+        holder["loc"] = dg.generate_random(seed=99)
+        dt = _timed(comm, torch, dev, run)
+    x = holder["x"]
+    return {"time_s": dt, "error": gelim.ops.gauss.error_metric(x), "ranks": comm.world_size,
+            "tflops_total": (2.0 / 3.0) * n ** 3 / dt * 1e-12, "block": dg.layout.D,
+            "lookahead": dg.lookahead, "layout": "1-D column block-cyclic"}
+
+
+def bench_dist_matmul(comm, gelim, torch, n: int) -> dict:
+    """16384^2 fp32 matmul over ALL ranks (strong): A/C row blocks, B
+    gathered in column chunks (all_gather_into_tensor) under the MFMA GEMM;
+    the single-link ring timed alongside when there is more than one rank."""
+    from gelim.parallel import allgather_matmul, ring_matmul
+
+    dev, P, r = comm.device, comm.world_size, comm.rank
+    g = torch.Generator(device=dev).manual_seed(1 + r)
+    Aloc = torch.randn(n // P, n, generator=g, device=dev)
+    Bloc = torch.randn(n // P, n, generator=g, device=dev)
+    out = {}
+    for name, fn in (("allgather", allgather_matmul), ("ring", ring_matmul)):
+        if name == "ring" and P == 1:
+            continue
+        fn(comm, Aloc, Bloc)
+        dt = _timed(comm, torch, dev, lambda: fn(comm, Aloc, Bloc), reps=2)
+        out[name] = {"time_s": dt, "tflops_total": 2 * n ** 3 / dt * 1e-12}
+    out["time_s"] = out["allgather"]["time_s"]
+    out["algo"] = "allgather (chunked all_gather_into_tensor of B overlapped with the MFMA GEMM)"
+    out["ranks"] = P
+    return out
+
+
+def bench_single(comm, gelim, torch, n: int, seed: int) -> dict:
+    """One n^2 system per GPU on the single-GPU solver (n > 2048: wide-panel
+    leaves + fp64 MFMA GEMM + the 2048 engine on the tail)."""
+    dev = comm.device
+    aug = gelim.random_system(n, seed=seed, device=dev)
+    s = gelim.GaussSolver(n, backend="hip", device=dev)
+    holder = {}
+    s.solve(aug)
+    dt = _timed(comm, torch, dev, lambda: holder.__setitem__("x", s.solve(aug)), reps=3)
+    res = {"time_s": dt, "tflops": (2.0 / 3.0) * n ** 3 / dt * 1e-12,
+           "error": gelim.ops.gauss.error_metric(holder["x"]), "singular": s.info() != 0}
+    s.close()
+    return res
+
+
+def bench_pivot(comm, gelim, torch, n: int) -> dict:
+    """The reference's per-pivot algorithm on the GPU (hip-pivot: one pivot
+    search + one elimination launch per column, graph-replayed), fp64 and
+    fp32, zero-pivot (internal programs) and partial pivoting."""
+    dev = comm.device
+    aug = gelim.random_system(n, seed=5, device=dev)
+    out = {}
+    for dtype, tag in ((torch.float64, "fp64"), (torch.float32, "fp32")):
+        s = gelim.GaussSolver(n, backend="hip-pivot", pivot="partial", dtype=dtype, device=dev)
+        a = aug.to(dtype)
+        holder = {}
+        s.solve(a)
+        dt = _timed(comm, torch, dev, lambda: holder.__setitem__("x", s.solve(a)), reps=3)
+        out[tag] = {"time_s": dt, "error": gelim.ops.gauss.error_metric(holder["x"])}
+        s.close()
+    return out
+
+
+def bench_external(comm, gelim, torch) -> dict:
+    """GPU solve time of the reference's external .dat matrices (the
+    Matrix-Market inputs of gauss_external_input, shipped as data/*.coo.npz)
+    next to the reference's best OpenMP time.  The timed solve includes the
+    copy-in of the system (like the headline)."""
+    dev = comm.device
+    out = {}
+    if comm.rank == 0:
+        for name, ref_s in EXTERNAL_OPENMP_BEST_S.items():
+            A = gelim.utils.io.load_fixture(name)
+            n = A.shape[0]
+            aug = gelim.augment_with_rhs(A).to(dev)
+            s = gelim.GaussSolver(n, backend="hip", device=dev)
+            x = s.solve(aug, check=True)
+            torch.cuda.synchronize(dev)
+            t0 = time.perf_counter()
+            for _ in range(3):
+                x = s.solve(aug)
+            torch.cuda.synchronize(dev)
+            dt = (time.perf_counter() - t0) / 3
+            out[name] = {"n": n, "time_s": dt, "error": gelim.ops.gauss.error_metric(x),
+                         "reference_openmp_best_s": ref_s, "speedup_vs_reference_openmp": ref_s / dt}
+            s.close()
+            del aug, A
+    comm.barrier()
+    return out
 
 
 def measure_host_seq(n: int) -> dict:
@@ -212,59 +373,6 @@ def measure_host_seq(n: int) -> dict:
            "cpus": os.cpu_count(), "measured_at": time.strftime("%Y-%m-%dT%H:%M:%S")}
     del torch
     return res
-
-
-def run_extras(comm, gelim, torch, n_gauss: int = 8192, n_mm: int = 16384) -> dict:
-    """Distributed configs of BASELINE.json: 8192^2 Gauss (column block-cyclic,
-    one RCCL panel broadcast per 64-column block) and 16384^2 fp32 ring matmul
-    (B blocks rotated with isend/irecv, overlapped with the MFMA GEMM).
-    Each is run twice and the second (warm) run is reported; wall time
-    bracketed by barrier + device sync, max over ranks."""
-    out = {}
-    dev = comm.device
-
-    def sync():
-        if dev.type == "cuda":
-            torch.cuda.synchronize(dev)
-        comm.barrier()
-
-    def tmax(dt: float) -> float:
-        t = torch.tensor([dt], dtype=torch.float64, device=dev)
-        comm.all_reduce(t, "max")
-        return t.item()
-
-    try:
-        from gelim.parallel import DistributedGauss, ring_matmul
-
-        n = n_gauss
-        dg = DistributedGauss(comm, n, block=64)
-        for _ in range(2):
-            loc = dg.generate_random(seed=99)
-            sync()
-            t0 = time.perf_counter()
-            x = dg.solve_(loc)
-            sync()
-            dt = tmax(time.perf_counter() - t0)
-        out[f"dist_gauss_{n}"] = {"time_s": dt, "error": gelim.ops.gauss.error_metric(x),
-                                   "gflops_total": (2.0 / 3.0) * n ** 3 / dt * 1e-9,
-                                   "layout": "1-D column block-cyclic, D=64"}
-        del dg, loc, x
-        M = K = Nn = n_mm
-        P = comm.world_size
-        g = torch.Generator().manual_seed(1 + comm.rank)
-        Aloc = torch.randn(M // P, K, generator=g).to(dev)
-        Bloc = torch.randn(K // P, Nn, generator=g).to(dev)
-        for _ in range(2):
-            sync()
-            t0 = time.perf_counter()
-            ring_matmul(comm, Aloc, Bloc)
-            sync()
-            dt = tmax(time.perf_counter() - t0)
-        out[f"dist_matmul_{n_mm}"] = {"time_s": dt, "tflops_total": 2 * M * K * Nn / dt * 1e-12,
-                                      "algo": "ring (B all-gather overlapped with MFMA)"}
-    except Exception as e:  # report, never kill the headline line
-        out["error"] = repr(e)
-    return out
 
 
 if __name__ == "__main__":

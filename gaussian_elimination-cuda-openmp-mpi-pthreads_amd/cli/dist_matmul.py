@@ -19,14 +19,14 @@ import torch
 
 from ..ops.matmul import reference_inputs
 from ..parallel import comm as C
-from ..parallel.dist_matmul import grid_shape, make_summa_groups, ring_matmul, summa_matmul
+from ..parallel.dist_matmul import allgather_matmul, grid_shape, make_summa_groups, ring_matmul, summa_matmul
 from ..utils.report import json_line
 
 
 def parse(argv=None):
     p = argparse.ArgumentParser(prog="gelim.cli.dist_matmul")
     p.add_argument("size", type=int)
-    p.add_argument("--algo", default="ring", choices=["ring", "summa"])
+    p.add_argument("--algo", default="allgather", choices=["allgather", "ring", "summa"])
     p.add_argument("--device", default=None)
     p.add_argument("--warmup", type=int, default=1)
     p.add_argument("--verify", action="store_true", help="check against a float64 reference on rank 0")
@@ -40,12 +40,13 @@ def main(argv=None) -> int:
     dev, P, r, n = comm.device, comm.world_size, comm.rank, args.size
     try:
         A, B = reference_inputs(n)
-        if args.algo == "ring":
+        if args.algo in ("ring", "allgather"):
             if n % P:
-                raise SystemExit(f"ring: size {n} must be divisible by the {P} ranks")
+                raise SystemExit(f"{args.algo}: size {n} must be divisible by the {P} ranks")
             h = n // P
             a_loc, b_loc = A[r * h:(r + 1) * h].to(dev), B[r * h:(r + 1) * h].to(dev)
-            run = lambda: ring_matmul(comm, a_loc, b_loc)  # noqa: E731
+            fn = ring_matmul if args.algo == "ring" else allgather_matmul
+            run = lambda: fn(comm, a_loc, b_loc)  # noqa: E731
         else:
             pr, pc = grid_shape(P)
             if n % pr or n % pc:

@@ -75,6 +75,14 @@ class Communicator:
             out.view(-1).copy_(t.reshape(-1))
         return out
 
+    def all_gather_async(self, out: torch.Tensor, t: torch.Tensor):
+        """Non-blocking all_gather_into_tensor (see broadcast_async)."""
+        if self.distributed:
+            return dist.all_gather_into_tensor(out.view(-1), t.contiguous().view(-1), group=self.group,
+                                               async_op=True)
+        out.view(-1).copy_(t.reshape(-1))
+        return _Done()
+
     def barrier(self) -> None:
         if self.distributed:
             if self.backend == "nccl":

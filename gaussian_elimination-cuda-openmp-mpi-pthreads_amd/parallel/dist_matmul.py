@@ -3,7 +3,14 @@
 The reference has no distributed matmul; BASELINE.json asks for a 16384^2
 fp32 multiply across the 8 GPUs of one node.  Two decompositions:
 
-ring_matmul (1-D, default)
+allgather_matmul (1-D, default)
+  A and C row-partitioned, B row-partitioned into P k-blocks.  B is gathered
+  in column chunks with all_gather_into_tensor -- one RCCL collective per
+  chunk, which spreads over every xGMI link of the node (the ring below
+  drives ONE neighbour link per step) -- and chunk c+1's gather runs on the
+  RCCL stream while the MFMA GEMM computes C[:, chunk c] = A_loc @ B[:, c].
+
+ring_matmul (1-D)
   A and C row-partitioned, B row-partitioned into P k-blocks.  P steps: each
   rank multiplies its A slice against the B block it currently holds
   (accumulating into C with the MFMA kernel) while that block is passed to
@@ -72,6 +79,42 @@ def ring_matmul(comm: Communicator, A_loc: torch.Tensor, B_loc: torch.Tensor, ke
             # the send of `cur` has completed (waited) before its buffer is
             # received into again two steps later
             cur = nxt
+    return C
+
+
+def allgather_matmul(comm: Communicator, A_loc: torch.Tensor, B_loc: torch.Tensor, chunks: int = 4,
+                     kernel: str = "mfma") -> torch.Tensor:
+    """A_loc: (M/P, K) rows of A; B_loc: (K/P, N) rows of B (equal blocks,
+    rank order).  Returns C_loc = A_loc @ B (M/P, N).  B travels as `chunks`
+    column chunks, each gathered (async) while the previous one multiplies."""
+    P = comm.world_size
+    kb, N = B_loc.shape
+    if A_loc.shape[1] != kb * P:
+        raise ValueError("allgather_matmul needs K divisible by the world size")
+    C = torch.empty((A_loc.shape[0], N), dtype=torch.float32, device=A_loc.device)
+    if P == 1:
+        matmul_acc_(C, A_loc, B_loc, accumulate=False, kernel=kernel)
+        return C
+    chunks = max(1, min(chunks, N))
+    bounds = [N * c // chunks for c in range(chunks + 1)]
+    wmax = max(bounds[c + 1] - bounds[c] for c in range(chunks))
+    send = [torch.empty((kb, wmax), dtype=torch.float32, device=A_loc.device) for _ in range(2)]
+    recv = [torch.empty((P * kb, wmax), dtype=torch.float32, device=A_loc.device) for _ in range(2)]
+
+    def post(c: int):
+        w = bounds[c + 1] - bounds[c]
+        snd = send[c % 2][:, :w]
+        snd.copy_(B_loc[:, bounds[c]:bounds[c + 1]])
+        out = recv[c % 2].view(-1)[:P * kb * w]
+        return comm.all_gather_async(out, snd.contiguous()), out.view(P * kb, w)
+
+    pending = post(0)
+    for c in range(chunks):
+        h, Bc = pending
+        h.wait()
+        if c + 1 < chunks:
+            pending = post(c + 1)  # on the RCCL stream while chunk c multiplies
+        matmul_acc_(C[:, bounds[c]:bounds[c + 1]], A_loc, Bc, accumulate=False, kernel=kernel)
     return C
 
 

@@ -105,6 +105,10 @@ class EmulatedComm(Communicator):
         w.wait()
         return t
 
+    def all_gather_async(self, out: torch.Tensor, t: torch.Tensor):
+        self.all_gather(out, t)
+        return _Done()
+
     def broadcast_async(self, t: torch.Tensor, src: int):
         """Emulated ranks rendezvous on the host, so the "async" broadcast
         completes before it returns (no overlap to emulate on one stream)."""

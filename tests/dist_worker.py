@@ -44,7 +44,7 @@ def matmul(rank, world, port, outdir, M, K, N, algo, device):
     import torch
 
     from gelim.parallel import comm as C
-    from gelim.parallel.dist_matmul import grid_shape, ring_matmul, summa_matmul
+    from gelim.parallel.dist_matmul import allgather_matmul, grid_shape, ring_matmul, summa_matmul
 
     try:
         comm = _init(rank, world, port, device)
@@ -52,11 +52,12 @@ def matmul(rank, world, port, outdir, M, K, N, algo, device):
         A = torch.randn(M, K, generator=g)
         B = torch.randn(K, N, generator=g)
         dev = comm.device
-        if algo == "ring":
+        if algo in ("ring", "allgather"):
             rows = M // world
             kb = K // world
-            C_loc = ring_matmul(comm, A[rank * rows:(rank + 1) * rows].to(dev).contiguous(),
-                                B[rank * kb:(rank + 1) * kb].to(dev).contiguous())
+            fn = ring_matmul if algo == "ring" else allgather_matmul
+            C_loc = fn(comm, A[rank * rows:(rank + 1) * rows].to(dev).contiguous(),
+                       B[rank * kb:(rank + 1) * kb].to(dev).contiguous())
         else:
             pr, pc = grid_shape(world)
             i, j = divmod(rank, pc)

@@ -53,7 +53,7 @@ def test_dist_gauss_reference_matrix_cpu(tmp_path, gelim):
 
 
 @pytest.mark.parametrize("world,algo", [(2, "ring"), (4, "ring"), (3, "ring"), (4, "summa"), (2, "summa"),
-                                        (6, "summa")])
+                                        (6, "summa"), (2, "allgather"), (3, "allgather"), (4, "allgather")])
 def test_dist_matmul_cpu(tmp_path, world, algo):
     M, K, N = 48, 72, 60
     codes = _spawn(dist_worker.matmul, world, _port(), str(tmp_path), M, K, N, algo, "cpu")
@@ -65,7 +65,7 @@ def test_dist_matmul_cpu(tmp_path, world, algo):
     B = torch.randn(K, N, generator=g)
     ref = A @ B
     parts = [torch.load(tmp_path / f"c{r}.pt") for r in range(world)]
-    if algo == "ring":
+    if algo in ("ring", "allgather"):
         C = torch.cat(parts, 0)
     else:
         from gelim.parallel.dist_matmul import grid_shape

@@ -74,13 +74,16 @@ EXTERNAL_OPENMP_BEST_S = {  # BASELINE.md, OpenMP external, best over threads (O
 def _timed(comm, torch, dev, fn, reps: int = 1) -> float:
     """Wall time of `reps` calls of fn, bracketed by device sync + barrier on
     both sides, MAX over ranks."""
-    torch.cuda.synchronize(dev)
-    comm.barrier()
+    def sync():
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+        comm.barrier()
+
+    sync()
     t0 = time.perf_counter()
     for _ in range(reps):
         fn()
-    torch.cuda.synchronize(dev)
-    comm.barrier()
+    sync()
     t = torch.tensor([(time.perf_counter() - t0) / reps], dtype=torch.float64, device=dev)
     comm.all_reduce(t, "max")
     return t.item()

@@ -131,8 +131,9 @@ def test_fault_env_hook(tmp_path, monkeypatch):
 
 
 def test_bench_extras_on_emulated_ranks(gelim):
-    """bench.py's distributed extras (run for N > 1) on 2 emulated CPU ranks
-    at reduced sizes: both configs report, none errors."""
+    """bench.py's strong-scaling sections (distributed Gauss and matmul over
+    all ranks) on 2 emulated CPU ranks at reduced sizes: both report, none
+    errors."""
     import importlib.util
 
     from conftest import ROOT
@@ -140,8 +141,11 @@ def test_bench_extras_on_emulated_ranks(gelim):
     spec = importlib.util.spec_from_file_location("bench_mod", ROOT / "bench.py")
     bench = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(bench)
-    res = run_emulated(2, lambda c: bench.run_extras(c, gelim, torch, n_gauss=192, n_mm=64))
-    for r in res:
-        assert "error" not in r, r
-        assert r["dist_gauss_192"]["error"] < 1e-9
-        assert r["dist_matmul_64"]["tflops_total"] > 0
+
+    def body(c):
+        return (bench.bench_dist_gauss(c, gelim, torch, 192), bench.bench_dist_matmul(c, gelim, torch, 64))
+
+    res = run_emulated(2, body)
+    for g, m in res:
+        assert g["error"] < 1e-9 and g["ranks"] == 2
+        assert m["allgather"]["tflops_total"] > 0 and m["ring"]["tflops_total"] > 0

@@ -237,7 +237,15 @@ template <typename T>
 int backsub_impl(const T* U, int64_t ldu, const T* y, int64_t incy, double* x, double* bnorm,
                  int64_t n, int unit, double* yw, hipStream_t s, const int* perm, int* err) {
   const int64_t nblk = (n + kBS - 1) / kBS;
-  if (nblk <= kMaxPersistBlocks) {
+  // the persistent form needs every block resident (flag hand-offs);
+  // checked once per (type, block count)
+  bool persist = nblk <= kMaxPersistBlocks;
+  if (persist) {
+    int per = 0;
+    persist = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, backsub_persist_kernel<T>, 256, 0) == hipSuccess &&
+              coresident(per, nblk);
+  }
+  if (persist) {
     // flags (+ the error word when the caller has none) live in yw
     unsigned* flags = reinterpret_cast<unsigned*>(yw);
     int* e = err ? err : reinterpret_cast<int*>(flags + nblk);

@@ -54,12 +54,16 @@ int tail_gemv(const double* A, int64_t lda, int64_t n, int64_t K, const double* 
 int fold_info(int* info, const int* tinfo, int64_t K, hipStream_t s);
 }  // namespace big
 int64_t rlu_max_n();
+bool rlu_coresident(int64_t n);
 size_t rlu_workspace_bytes(int64_t n);
 int rlu_factor(const double* src, int64_t lds, double* work, int64_t ldw, int64_t n, int mode,
                int* piv, int* info, void* ws, hipStream_t s, unsigned long long* stamps = nullptr);
 template <typename T>
-int pivot_elimination(T* A, int64_t lda, int64_t n, int mode, T* mcol, int* info,
-                      hipStream_t s);
+int pivot_elimination(T* A, int64_t lda, int64_t n, int mode, T* mcol, int* info, hipStream_t s, int* ipiv,
+                      double* diag);
+template <typename T>
+int pivot_lower_resolve(const T* A, int64_t lda, int64_t n, const int* ipiv, const double* diag, const double* c,
+                        T* y, hipStream_t s);
 }  // namespace gelim
 
 struct gelim_gauss_plan {
@@ -71,6 +75,8 @@ struct gelim_gauss_plan {
   int* info = nullptr;
   double* yw = nullptr;
   void* mcol = nullptr;
+  double* diag = nullptr;                // hip-pivot: pivot values of the stored factors
+  void* ry = nullptr;                    // hip-pivot re-solve: L~^-1 P c (plan dtype)
   double* tmp = nullptr;
   hipStream_t cap = nullptr;
   hipStream_t side = nullptr;            // lookahead: wide trailing updates
@@ -408,13 +414,13 @@ int enqueue(gelim_gauss_plan* p, const void* src, int64_t src_ld, void* dx, void
   if (p->eb == 8) {
     double* A = static_cast<double*>(p->work);
     GELIM_TRY(pivot_elimination<double>(A, lda, n, p->pivot, static_cast<double*>(p->mcol),
-                                        p->info, s));
+                                        p->info, s, p->piv, p->diag));
     return backsub_f64(A, lda, A + n, lda, static_cast<double*>(dx),
                        static_cast<double*>(bnorm), n, 1, p->yw, s);
   }
   float* A = static_cast<float*>(p->work);
   GELIM_TRY(pivot_elimination<float>(A, lda, n, p->pivot, static_cast<float*>(p->mcol), p->info,
-                                     s));
+                                     s, p->piv, p->diag));
   return backsub_f32(A, lda, A + n, lda, static_cast<double*>(dx), static_cast<double*>(bnorm), n,
                      1, p->yw, s);
 }
@@ -514,6 +520,8 @@ extern "C" gelim_gauss_plan* gelim_gauss_plan_create(int64_t n, int algo, int pi
   if (hipMalloc((void**)&p->info, 16) != hipSuccess) return fail("info");
   if (hipMalloc((void**)&p->yw, (size_t)n * sizeof(double)) != hipSuccess) return fail("yw");
   if (hipMalloc(&p->mcol, (size_t)n * dtype_bytes) != hipSuccess) return fail("mcol");
+  if (hipMalloc((void**)&p->diag, (size_t)n * sizeof(double)) != hipSuccess) return fail("diag");
+  if (hipMalloc(&p->ry, (size_t)n * dtype_bytes) != hipSuccess) return fail("ry");
   if (hipMalloc((void**)&p->tmp, (size_t)2 * 32 * (n + 1) * sizeof(double)) != hipSuccess)
     return fail("tmp");
   if (hipStreamCreateWithFlags(&p->cap, hipStreamNonBlocking) != hipSuccess) return fail("stream");
@@ -531,7 +539,7 @@ extern "C" gelim_gauss_plan* gelim_gauss_plan_create(int64_t n, int algo, int pi
     const char* e = std::getenv("GELIM_SCHEDULE");
     const std::string sched = e ? e : "auto";
     const int64_t lim = sched == "resident" ? gelim::rlu_max_n() : sched == "auto" ? 1024 : 0;
-    p->resident = algo == GELIM_GPU_BLOCKED && n <= lim && !p->lookahead;
+    p->resident = algo == GELIM_GPU_BLOCKED && n <= lim && !p->lookahead && gelim::rlu_coresident(n);
     // GELIM_HYBRID: rows of the trailing system handed to the resident LU
     // (default 1024, its 2-slot regime; 0 = off, pure fused schedule; any
     // other value up to 2048, rounded to a panel boundary -- 1, 2 and 4
@@ -539,7 +547,7 @@ extern "C" gelim_gauss_plan* gelim_gauss_plan_create(int64_t n, int algo, int pi
     const char* eh = std::getenv("GELIM_HYBRID");
     const int64_t tail = eh ? std::max<int64_t>(0, std::min<int64_t>(gelim::rlu_max_n(), std::atoll(eh))) : 1024;
     if (algo == GELIM_GPU_BLOCKED && !p->resident && p->fused && tail > 0 && n > tail &&
-        tail <= gelim::rlu_max_n() && sched != "fused")
+        tail <= gelim::rlu_max_n() && sched != "fused" && gelim::rlu_coresident(tail))
       p->split = n - tail;  // rounded to a panel boundary below
   }
   if (algo == GELIM_GPU_BLOCKED) {
@@ -603,6 +611,8 @@ extern "C" void gelim_gauss_plan_destroy(gelim_gauss_plan* p) {
   (void)hipFree(p->info);
   (void)hipFree(p->yw);
   (void)hipFree(p->mcol);
+  (void)hipFree(p->diag);
+  (void)hipFree(p->ry);
   (void)hipFree(p->tmp);
   (void)hipFree(p->big_ws);
   (void)hipFree(p->big_pairs);
@@ -676,6 +686,26 @@ extern "C" int gelim_gauss_plan_solve(gelim_gauss_plan* p, const void* src, int6
   GELIM_TRY(gelim::copy2d_async(dx, 0, p->xbuf, 0, sizeof(double) * n, 1, s));
   if (want_bn) GELIM_TRY(gelim::copy2d_async(bnorm, 0, p->bnbuf, 0, sizeof(double) * n, 1, s));
   return GELIM_OK;
+}
+
+// Re-solve A x = c with the factors the last hip-pivot solve left in the
+// plan (O(n^2): permutation + lower solve + unit upper back substitution);
+// c and x are fp64 device vectors.  The refinement loop of
+// GaussSolver.solve_refined uses it instead of re-factoring.
+extern "C" int gelim_gauss_plan_resolve(gelim_gauss_plan* p, const double* c, double* x, void* stream) {
+  using namespace gelim;
+  if (!p || !c || !x) return GELIM_FAIL(GELIM_E_ARG, "plan_resolve: null argument");
+  if (p->algo != GELIM_GPU_PIVOT) return GELIM_FAIL(GELIM_E_ARG, "plan_resolve: only the hip-pivot plan keeps its factors");
+  hipStream_t s = (hipStream_t)stream;
+  const int64_t n = p->n, lda = p->lda;
+  if (p->eb == 8) {
+    const double* A = static_cast<const double*>(p->work);
+    GELIM_TRY(pivot_lower_resolve<double>(A, lda, n, p->piv, p->diag, c, static_cast<double*>(p->ry), s));
+    return backsub_f64(A, lda, static_cast<const double*>(p->ry), 1, x, nullptr, n, 1, p->yw, s);
+  }
+  const float* A = static_cast<const float*>(p->work);
+  GELIM_TRY(pivot_lower_resolve<float>(A, lda, n, p->piv, p->diag, c, static_cast<float*>(p->ry), s));
+  return backsub_f32(A, lda, static_cast<const float*>(p->ry), 1, x, nullptr, n, 1, p->yw, s);
 }
 
 extern "C" int gelim_gauss_plan_info(gelim_gauss_plan* p, void* stream) {

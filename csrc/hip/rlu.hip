@@ -808,6 +808,20 @@ Layout layout(int64_t n) {
 
 int64_t rlu_max_n() { return 2048; }
 
+// The np + 1 workgroups of the resident LU hand panels and strips to each
+// other through flags: they must all be resident at once.
+bool rlu_coresident(int64_t n) {
+  using namespace rlu;
+  const Layout L = layout(n);
+  if (!L.R) return false;
+  int per = 0;
+  hipError_t e = hipSuccess;
+  if (L.R == 1) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, rlu_kernel<1, 1>, NT, 0);
+  else if (L.R == 2) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, rlu_kernel<2, 1>, NT, 0);
+  else e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, rlu_kernel<4, 1>, NT, 0);
+  return e == hipSuccess && coresident(per, L.np + 1);
+}
+
 size_t rlu_workspace_bytes(int64_t n) { return rlu::layout(n).total; }
 
 // Factor the augmented system src (n x (n+1), ld lds; NULL = work already

@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 
 #include "device_common.h"
 #include "gelim/internal.h"
@@ -16,6 +17,19 @@ __global__ __launch_bounds__(256) void copy2d_words_kernel(unsigned* __restrict_
   const unsigned* srow = sp + (int64_t)blockIdx.y * spp;
   unsigned* drow = d + (int64_t)blockIdx.y * dp;
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < w; i += (int64_t)gridDim.x * 256) drow[i] = srow[i];
+}
+
+// r[i] = aug[i][n] - sum_j aug[i][j] x[j] (fp64; one wave per row)
+__global__ __launch_bounds__(256) void residual_kernel(const double* __restrict__ aug, int64_t ld, int n,
+                                                       const double* __restrict__ x, double* __restrict__ r) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= n) return;
+  const double* a = aug + (int64_t)row * ld;
+  double s = 0.0;
+  for (int j = lane; j < n; j += 64) s = fma(a[j], x[j], s);
+  s = dev::wave_sum(s);
+  if (lane == 0) r[row] = a[n] - s;
 }
 
 __global__ __launch_bounds__(256) void zero_words_kernel(unsigned* __restrict__ p, int64_t nwords) {
@@ -91,6 +105,22 @@ int copy2d_async(void* dst, size_t dpitch, const void* src, size_t spitch, size_
                      (int64_t)(dpitch / 4), static_cast<const unsigned*>(src), (int64_t)(spitch / 4), w);
   HIP_TRY(hipGetLastError());
   return GELIM_OK;
+}
+
+int residual_f64(const double* aug, int64_t ld, int64_t n, const double* x, double* r, hipStream_t s) {
+  hipLaunchKernelGGL(residual_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, s, aug, ld, (int)n, x, r);
+  HIP_TRY(hipGetLastError());
+  return GELIM_OK;
+}
+
+bool coresident(int per_cu, int64_t grid) {
+  if (const char* e = std::getenv("GELIM_FORCE_NONPERSISTENT"))
+    if (std::atoi(e) != 0) return false;
+  int dev = 0, cus = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return false;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return false;
+  const int64_t usable = per_cu > 1 ? per_cu - 1 : per_cu;
+  return usable * (int64_t)cus >= grid;
 }
 
 int zero_async(void* p, size_t bytes, struct ihipStream_t* s) {
@@ -205,4 +235,11 @@ extern "C" int gelim_gpu_error_metric(const double* dx, int64_t n, double* d_err
                      (int)n, d_err);
   HIP_TRY(hipGetLastError());
   return GELIM_OK;
+}
+
+// r = b - A x for an augmented fp64 system (the refinement residual).
+extern "C" int gelim_gpu_residual(const double* daug, int64_t ld, int64_t n, const double* dx, double* dr,
+                                  void* stream) {
+  if (n <= 0 || ld < n + 1) return GELIM_FAIL(GELIM_E_ARG, "residual: bad n / ld");
+  return gelim::residual_f64(daug, ld, n, dx, dr, (hipStream_t)stream);
 }

@@ -214,6 +214,11 @@ int gelim_gauss_plan_solve(gelim_gauss_plan* p, const void* d_src_aug,
 /* Reads back the info word (synchronises the stream). 0 = non-singular,
  * k>0: first zero pivot at column k-1. */
 int gelim_gauss_plan_info(gelim_gauss_plan* p, void* stream);
+/* hip-pivot plans keep their factors: re-solve A x = c (fp64 device vectors)
+ * in O(n^2) after a solve */
+int gelim_gauss_plan_resolve(gelim_gauss_plan* p, const double* d_c, double* d_x, void* stream);
+/* r = b - A x of an augmented fp64 system (b in column n) */
+int gelim_gpu_residual(const double* d_aug, int64_t ld, int64_t n, const double* d_x, double* d_r, void* stream);
 
 /* ---- GPU fp32 matmul --------------------------------------------------- */
 /* C (M x N) = A (M x K) * B (K x N), row-major, ld = cols. */

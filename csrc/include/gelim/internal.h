@@ -17,6 +17,12 @@ int fail(int code, const char* file, int line, const std::string& msg);
 // nodes of captured graphs were the part of a graph that plan lifecycle
 // operations corrupted on ROCm 7.2 (profiles/graph_recapture.txt).
 int zero_async(void* p, size_t bytes, struct ihipStream_t* s);
+// Co-residency guard of the persistent (flag hand-off) kernels: true when
+// `grid` workgroups of a kernel that the occupancy API admits `per_cu` times
+// per CU all fit at once (one block of margin per CU above one, as the API
+// can overstate the SGPR-limited count by one); GELIM_FORCE_NONPERSISTENT=1
+// forces false (tests of the fallback schedules).
+bool coresident(int per_cu, int64_t grid);
 // Row-major 2D copy (rows x width bytes, width a multiple of 4) by a kernel,
 // for the same reason (no memcpy nodes in captured graphs).
 int copy2d_async(void* dst, size_t dpitch, const void* src, size_t spitch, size_t width, size_t rows,

@@ -79,6 +79,8 @@ _PROTOS = {
     "gelim_gpu_laswp_panel": (_int, [_vp, _i64, _i64, _i64, _int, _vp, _i64, _i64, _i64, _i64, _i64, _vp]),
     "gelim_gpu_backsub": (_int, [_vp, _i64, _vp, _i64, _vp, _vp, _i64, _int, _vp]),
     "gelim_gauss_plan_create": (_vp, [_i64, _int, _int, _int, _int]),
+    "gelim_gauss_plan_resolve": (_int, [_vp, _vp, _vp, _vp]),
+    "gelim_gpu_residual": (_int, [_vp, _i64, _i64, _vp, _vp, _vp]),
     "gelim_gauss_plan_destroy": (None, [_vp]),
     "gelim_gauss_plan_lda": (_i64, [_vp]),
     "gelim_gauss_plan_work": (_vp, [_vp]),

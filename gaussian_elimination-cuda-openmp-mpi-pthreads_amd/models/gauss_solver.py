@@ -103,19 +103,33 @@ class GaussSolver:
 
     __call__ = solve
 
+    def resolve(self, c: torch.Tensor) -> torch.Tensor:
+        """hip-pivot only: solve A x = c with the factors of the LAST solve
+        (O(n^2): permutation, lower and unit-upper triangular solves on the
+        GPU; c fp64 on the device)."""
+        if self.backend != "hip-pivot":
+            raise ValueError("only the hip-pivot plan keeps its factors")
+        c = c.to(self.device, torch.float64).contiguous()
+        x = torch.empty(self.n, dtype=torch.float64, device=self.device)
+        _native.check(_native.lib().gelim_gauss_plan_resolve(self._plan, ptr(c), ptr(x), stream_handle(self.device)),
+                      "plan_resolve")
+        return x
+
     def solve_refined(self, aug: torch.Tensor, max_steps: int = 5, tol: float | None = None,
                       check: bool = False):
         """Mixed-precision iterative refinement.
 
-        The elimination runs in the solver's dtype (fp32 on `hip-pivot`, or
-        fp64 anywhere); the residual r = b - A x and the accumulated x are
-        always fp64.  Each step re-solves A d = r / s with the same matrix
-        (s = ||r||_inf keeps r inside fp32's exponent range) and adds s·d to x.
-        Stops after `max_steps` corrections, once ||s·d||_inf <=
-        tol·||x||_inf (tol defaults to 4·eps64), or when a correction fails
-        to shrink ||r||_inf (refinement diverges once cond(A)·eps of the
-        factor dtype reaches 1; x is then never worse than the plain solve).
-        Returns (x, accepted_steps).
+        The elimination runs ONCE in the solver's dtype (fp32 on `hip-pivot`,
+        or fp64); the residual r = b - A x (native fp64 kernel) and the
+        accumulated x are fp64.  Each step solves A d = r / s with the STORED
+        factors (`resolve`, O(n^2): s = ||r||_inf keeps r inside fp32's
+        exponent range) and adds s·d to x -- so the refinement costs one
+        factorisation plus O(n^2) per step.  Backends whose plans keep no
+        factors (the blocked LU) re-solve instead.  Stops after `max_steps`
+        corrections, once ||s·d||_inf <= tol·||x||_inf (tol defaults to
+        4·eps64), or when a correction fails to shrink ||r||_inf (refinement
+        diverges once cond(A)·eps of the factor dtype reaches 1; x is then
+        never worse than the plain solve).  Returns (x, accepted_steps).
 
         The reference has no refinement (its fp64 loops are one-shot,
         `OpenMP_and_MPI/gauss_openmp/gauss_external_input.c:150-200`); this is
@@ -124,19 +138,33 @@ class GaussSolver:
         """
         n = self.n
         dev = self.device
-        A = aug[:, :n].to(dev, torch.float64)
-        b = aug[:, n].to(dev, torch.float64)
+        aug64 = aug[:, :n + 1].to(dev, torch.float64).contiguous()
         work = aug[:, :n + 1].to(dev, self.dtype).contiguous()
         tol = 4 * torch.finfo(torch.float64).eps if tol is None else tol
+        stored = self.gpu and self.backend == "hip-pivot"
+
+        def residual(xv: torch.Tensor) -> torch.Tensor:
+            if self.gpu:
+                r = torch.empty(n, dtype=torch.float64, device=dev)
+                _native.check(_native.lib().gelim_gpu_residual(ptr(aug64), aug64.stride(0), n, ptr(xv), ptr(r),
+                                                               stream_handle(dev)), "residual")
+                return r
+            return aug64[:, n] - aug64[:, :n] @ xv
+
+        def correction(rs: torch.Tensor) -> torch.Tensor:
+            if stored:
+                return self.resolve(rs)
+            work[:, n] = rs.to(self.dtype)
+            return self.solve(work, check=check).to(torch.float64)
+
         x = self.solve(work, check=check).to(torch.float64)
-        r = b - A @ x
+        r = residual(x)
         s = float(r.abs().max())
         steps = 0
         while steps < max_steps and s > 0.0 and s == s:
-            work[:, n] = (r / s).to(self.dtype)
-            d = self.solve(work, check=check).to(torch.float64) * s
+            d = correction(r / s) * s
             xn = x + d
-            rn = b - A @ xn
+            rn = residual(xn)
             sn = float(rn.abs().max())
             if not sn < s:  # diverging (cond(A)·eps of the factor dtype >= 1): keep the better x
                 break

@@ -201,3 +201,60 @@ def test_fp64_refined_hip(gelim, cuda):
     x, steps = s.solve_refined(aug, max_steps=2, check=True)
     assert steps >= 1
     assert gelim.ops.gauss.error_metric(x) < 1e-10
+
+
+@pytest.mark.parametrize("n", [700, 2048, 3000])
+def test_forced_nonpersistent_fallback(gelim, cuda, monkeypatch, n):
+    """GELIM_FORCE_NONPERSISTENT=1 makes every co-residency check fail: the
+    plan must pick the non-persistent schedules (fused steps instead of the
+    resident LU / hybrid tail, per-block back substitution launches) and
+    still match torch."""
+    monkeypatch.setenv("GELIM_FORCE_NONPERSISTENT", "1")
+    aug = gelim.random_system(n, seed=n + 17, device=cuda)
+    x = gelim.GaussSolver(n, backend="hip", device=cuda).solve(aug, check=True)
+    ref = torch.linalg.solve(aug[:, :n], aug[:, n])
+    assert torch.allclose(x, ref, rtol=1e-8, atol=1e-8 * n), (x - ref).abs().max().item()
+
+
+@pytest.mark.parametrize("dtype,tol", [(torch.float64, 1e-9), (torch.float32, 2e-3)])
+@pytest.mark.parametrize("n", [100, 1000])
+def test_pivot_plan_resolve(gelim, cuda, dtype, tol, n):
+    """hip-pivot keeps its factors: resolve(c) solves A x = c for a NEW
+    right-hand side in O(n^2), matching torch (fp32 factors: fp32 accuracy)."""
+    aug = gelim.random_system(n, seed=n, device=cuda)
+    s = gelim.GaussSolver(n, backend="hip-pivot", dtype=dtype, device=cuda)
+    s.solve(aug.to(dtype), check=True)
+    A = aug[:, :n]
+    for k in range(3):
+        c = torch.randn(n, dtype=torch.float64, device=cuda, generator=torch.Generator(cuda).manual_seed(k))
+        x = s.resolve(c)
+        ref = torch.linalg.solve(A, c)
+        assert ((x - ref).abs().max() / ref.abs().max()).item() < tol
+
+
+def test_refinement_steps_are_quadratic(gelim, cuda):
+    """One refinement step (residual + resolve) costs a small fraction of the
+    fp32 factorisation it reuses (no re-factoring per step)."""
+    import time
+
+    n = 2048
+    aug = gelim.random_system(n, seed=3, device=cuda)
+    s = gelim.GaussSolver(n, backend="hip-pivot", dtype=torch.float32, device=cuda)
+    a32 = aug.to(torch.float32)
+    s.solve(a32)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    s.solve(a32)
+    torch.cuda.synchronize()
+    t_factor = time.perf_counter() - t0
+    c = aug[:, n].clone()
+    s.resolve(c)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(5):
+        s.resolve(c)
+    torch.cuda.synchronize()
+    t_step = (time.perf_counter() - t0) / 5
+    assert t_step < t_factor / 10, (t_step, t_factor)
+    x, steps = s.solve_refined(aug, max_steps=8)
+    assert steps >= 1 and gelim.ops.gauss.error_metric(x) < 1e-9

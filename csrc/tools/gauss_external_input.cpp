@@ -18,6 +18,7 @@
 
 #include <cmath>
 #include <cstdint>
+#include <string>
 #include <vector>
 
 #include "cli_common.h"
@@ -87,6 +88,9 @@ int main(int argc, char* argv[]) {
     const long nprocs = sysconf(_SC_NPROCESSORS_ONLN);
     printf("Setting CPU Affinity : %s\n", (affinity && num_threads <= nprocs) ? "Yes" : "No");
   }
+  if (cli::is_gpu(backend) && npos == 2)
+    printf("note: the thread count %d is ignored by the GPU backends (one GPU per process; for N GPUs run "
+           "`torchrun --nproc-per-node N -m gelim.cli.dist_gauss --file <matrix>`)\n", num_threads);
 
   // initMatrix + initRHS on the host, in the reference's order (P1e:296-297)
   const bool gpu = cli::is_gpu(backend);
@@ -131,10 +135,13 @@ int main(int argc, char* argv[]) {
     const double t0 = cli::wall();
     run();
     elapsed = cli::wall() - t0;
-    if (gelim_gauss_plan_info(plan, s) != 0) {
+    // > 0: 1 + the first zero-pivot column; < 0: a GPU error, not "singular"
+    const int info = gelim_gauss_plan_info(plan, s);
+    if (info > 0) {
       fprintf(stderr, "The matrix is singular\n");
       exit(-1);
     }
+    if (info < 0) cli::die("plan_info");
     CLI_HIP(hipMemcpy(X.data(), dx, n * sizeof(double), hipMemcpyDeviceToHost));
     printf("Device: %s ; Backend: %s ; dtype: f64\n", cli::device_name().c_str(),
            cli::backend_name(backend));
@@ -149,8 +156,10 @@ int main(int argc, char* argv[]) {
   fprintf(stdout, "Error: %e\n", error);
   if (json)
     printf("{\"program\": \"gauss_external_input\", \"file\": \"%s\", \"n\": %lld, "
-           "\"backend\": \"%s\", \"threads\": %d, \"dtype\": \"f64\", \"time_s\": %.9f, "
+           "\"backend\": \"%s\", \"threads\": %s, \"gpus\": %d, \"dtype\": \"f64\", \"time_s\": %.9f, "
            "\"error\": %.6e}\n",
-           fname, (long long)n, cli::backend_name(backend), num_threads, elapsed, error);
+           fname, (long long)n, cli::backend_name(backend),
+           cli::is_gpu(backend) ? "null" : std::to_string(num_threads).c_str(), cli::is_gpu(backend) ? 1 : 0,
+           elapsed, error);
   return 0;
 }

@@ -22,6 +22,7 @@
 #include <cassert>
 #include <cmath>
 #include <cstdint>
+#include <string>
 #include <vector>
 
 #include "cli_common.h"
@@ -99,6 +100,9 @@ int main(int argc, char* argv[]) {
     printf("\nMatrix Size: %d ; Threads: %d; Block Size: %d\n", nsize, num_threads, 16);
   else
     printf("\nMatrix Size: %d ; Threads: %d\n", nsize, num_threads);
+  if (cli::is_gpu(backend) && threads_given)
+    printf("note: -t %d is ignored by the GPU backends (one GPU per process; for N GPUs run "
+           "`torchrun --nproc-per-node N -m gelim.cli.dist_gauss`)\n", num_threads);
   if (backend == cli::PTH_V3) {
     const long nprocs = sysconf(_SC_NPROCESSORS_ONLN);
     printf("Setting CPU Affinity : %s\n", (affinity && num_threads <= nprocs) ? "Yes" : "No");
@@ -142,10 +146,14 @@ int main(int argc, char* argv[]) {
     const double t0 = cli::wall();
     run();
     elapsed = cli::wall() - t0;
-    if (gelim_gauss_plan_info(plan, s) != 0) {
+    // > 0: 1 + the first zero-pivot column; < 0: a GPU error (hand-off
+    // timeout, corrupt row map ...), never reported as "singular"
+    const int info = gelim_gauss_plan_info(plan, s);
+    if (info > 0) {
       printf("The matrix is singular\n");
       exit(-1);
     }
+    if (info < 0) cli::die("plan_info");
     CLI_HIP(hipMemcpy(C.data(), dx, n * sizeof(double), hipMemcpyDeviceToHost));
     if (verify) CLI_HIP(hipMemcpy(B.data(), dbn, n * sizeof(double), hipMemcpyDeviceToHost));
     printf("Device: %s ; Backend: %s ; dtype: %s\n", cli::device_name().c_str(),
@@ -169,11 +177,12 @@ int main(int argc, char* argv[]) {
       double e = std::abs(C[i] - ex);
       if (e > err) err = e;
     }
+    const std::string thr = cli::is_gpu(backend) ? "null" : std::to_string(num_threads);
     printf("{\"program\": \"gauss_internal_input\", \"n\": %lld, \"backend\": \"%s\", "
-           "\"threads\": %d, \"dtype\": \"%s\", \"time_s\": %.9f, \"gflops\": %.3f, "
+           "\"threads\": %s, \"gpus\": %d, \"dtype\": \"%s\", \"time_s\": %.9f, \"gflops\": %.3f, "
            "\"max_abs_err\": %.3e}\n",
-           (long long)n, cli::backend_name(backend), num_threads, dtype == 8 ? "f64" : "f32",
-           elapsed, (2.0 / 3.0) * (double)n * n * n / elapsed * 1e-9, err);
+           (long long)n, cli::backend_name(backend), thr.c_str(), cli::is_gpu(backend) ? 1 : 0,
+           dtype == 8 ? "f64" : "f32", elapsed, (2.0 / 3.0) * (double)n * n * n / elapsed * 1e-9, err);
   }
   return 0;
 }

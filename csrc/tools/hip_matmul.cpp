@@ -26,6 +26,7 @@
 #include <algorithm>
 #include <cmath>
 #include <iostream>
+#include <string>
 #include <vector>
 
 #include "cli_common.h"
@@ -183,12 +184,16 @@ int main(int argc, char* argv[]) {
   }
   if (json) {
     const double flops = 2.0 * (double)nsize * nsize * nsize;
+    char rel_buf[32];
+    snprintf(rel_buf, sizeof(rel_buf), "%.3e", max_rel);
+    const std::string rel_str = rel_buf;
     printf("{\"program\": \"hip_matmul\", \"n\": %lld, \"kernel\": %d, \"gpu_time_s\": %.9f, "
            "\"gpu_kernel_s\": %.9f, \"kernel_tflops\": %.3f, \"seq_time_s\": %.6f, "
            "\"omp_time_s\": %.6f, \"speedup_vs_seq\": %.3f, \"kernel_speedup_vs_seq\": %.3f, "
-           "\"max_rel_err\": %.3e}\n",
+           "\"max_rel_err\": %s}\n",
            (long long)nsize, kernel, gpu_s, ks, flops / ks * 1e-12, seq_s, omp_s,
-           seq_s > 0 ? seq_s / gpu_s : -1.0, seq_s > 0 ? seq_s / ks : -1.0, max_rel);
+           seq_s > 0 ? seq_s / gpu_s : -1.0, seq_s > 0 ? seq_s / ks : -1.0,
+           verify ? rel_str.c_str() : "null");  // null: not verified (no --verify)
   }
   (void)hipHostFree(A);
   (void)hipHostFree(B);

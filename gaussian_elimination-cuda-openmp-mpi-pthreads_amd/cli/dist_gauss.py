@@ -43,7 +43,11 @@ def parse(argv=None):
     p = argparse.ArgumentParser(prog="gelim.cli.dist_gauss", description=__doc__.split("\n\n")[0])
     p.add_argument("file", nargs="?", help=".dat or .coo.npz matrix (external mode)")
     p.add_argument("-s", "--size", type=int, default=2048, help="order of the synthetic system (internal mode)")
-    p.add_argument("--block", type=int, default=64, help="column block width D of the block-cyclic layout")
+    p.add_argument("--block", type=int, default=None,
+                   help="column block width D of the block-cyclic layout (default: 256 on GPUs, 64 on CPUs)")
+    p.add_argument("-t", "--threads", type=int, default=None, metavar="N",
+                   help="the reference's -t: here the number of ranks (GPUs) -- set by the launcher "
+                        "(torchrun --nproc-per-node N); a mismatch is reported, not silently ignored")
     p.add_argument("--pivot", default="partial", choices=["partial", "zero"])
     p.add_argument("--device", default=None, help="cpu | cuda (default: cuda when visible)")
     p.add_argument("--warmup", type=int, default=0, help="untimed solves before the timed one")
@@ -70,10 +74,14 @@ def synthetic_local(dg: DistributedGauss) -> torch.Tensor:
     loc = dg.empty_local()
     i = torch.arange(1, n + 1, dtype=torch.float64, device=dg.device).view(n, 1)
     for g in L.local_blocks(dg.comm.rank):
-        c, w = L.local_col(g), L.width(g)
+        c = L.local_col(g)
+        w = max(0, min(L.width(g), n - g * L.D))  # real columns (GPU ranks pad to a multiple of 32)
+        if w == 0:
+            continue
         j = torch.arange(g * L.D + 1, g * L.D + w + 1, dtype=torch.float64, device=dg.device).view(1, w)
-        loc[:, c:c + w] = 2.0 * torch.minimum(i, j)
-    loc[:, dg.nloc] = torch.arange(n, dtype=torch.float64, device=dg.device)
+        loc[:n, c:c + w] = 2.0 * torch.minimum(i, j)
+    loc[:n, dg.nloc] = torch.arange(n, dtype=torch.float64, device=dg.device)
+    dg._pad_identity(loc)
     return loc
 
 
@@ -93,6 +101,11 @@ def main(argv=None) -> int:
 
 def run(args, comm) -> int:
     dev = comm.device
+    if args.threads is not None and args.threads != comm.world_size and comm.rank == 0:
+        print(f"note: -t {args.threads} requests {args.threads} ranks but this job has {comm.world_size} "
+              f"(launch with `torchrun --nproc-per-node {args.threads} -m gelim.cli.dist_gauss ...`, or "
+              f"--emulate {args.threads} for threads on one device); running with {comm.world_size}",
+              file=sys.stderr, flush=True)
 
     def sync():
         if dev.type == "cuda":
@@ -123,7 +136,7 @@ def run(args, comm) -> int:
                     print(f"Max error vs exact solution: {err:e}")
                 if args.json:
                     json_line({"program": "dist_gauss_internal", "n": n, "ranks": comm.world_size,
-                                     "block": args.block, "time_s": dt, "max_abs_error": err,
+                                     "block": dg.layout.D, "time_s": dt, "max_abs_error": err,
                                      "backend": comm.backend, "device": dev.type})
         else:
             A = load_global(args.file)
@@ -146,7 +159,7 @@ def run(args, comm) -> int:
                 print(f"Error: {err:e}", flush=True)
                 if args.json:
                     json_line({"program": "dist_gauss_external", "file": args.file, "n": n,
-                                     "ranks": comm.world_size, "block": args.block, "time_s": dt,
+                                     "ranks": comm.world_size, "block": dg.layout.D, "time_s": dt,
                                      "error": err, "backend": comm.backend, "device": dev.type})
     except _native.SingularMatrixError:
         if comm.rank == 0:

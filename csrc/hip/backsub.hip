@@ -91,6 +91,63 @@ __device__ __forceinline__ double solve_diag(const double (&row)[kBS], double ri
   return xv;
 }
 
+// Bounded poll of flag c by lane 0 of the calling wave (wave-uniform result).
+__device__ __forceinline__ bool poll_flag(unsigned* flags, int c, int* err, bool nap) {
+  int good = 1;
+  if (__lane_id() == 0) {
+    if (__hip_atomic_load(&flags[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
+      const unsigned long long t0 = rtc();
+      while (__hip_atomic_load(&flags[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
+        if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0 || rtc() - t0 > kSpinTicks) {
+          __hip_atomic_store(err, 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          good = 0;
+          break;
+        }
+        if (nap) __builtin_amdgcn_s_sleep(1);
+      }
+    }
+  }
+  return __shfl(good, 0) != 0;
+}
+
+// acc -= U[rows of this block, block c] . x_c, row = lane: the U block was
+// prefetched into u[] before the poll; x_c (stored write-through by its
+// producer) is read with one agent-scope load per lane and broadcast with
+// readlane.
+template <typename T>
+__device__ __forceinline__ bool apply_block(const T* __restrict__ U, int64_t ldu, int pr, int c, int n,
+                                            const double* __restrict__ x, unsigned* flags, int* err, bool nap,
+                                            double& acc) {
+  const int lane = __lane_id();
+  const int c0 = c * kBS, cw = min(kBS, n - c0);
+  double u[kBS];
+  const T* urow = U + (int64_t)pr * ldu + c0;
+#pragma unroll
+  for (int k = 0; k < kBS; ++k) u[k] = (double)urow[min(k, cw - 1)];
+  if (!poll_flag(flags, c, err, nap)) return false;
+  const double xl = __builtin_bit_cast(
+      double, __hip_atomic_load(reinterpret_cast<const unsigned long long*>(x + c0 + min(lane, cw - 1)),
+                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  const uint64_t xb = __builtin_bit_cast(uint64_t, xl);
+  const int xlo = (int)(unsigned)xb, xhi = (int)(unsigned)(xb >> 32);
+#pragma unroll
+  for (int k = 0; k < kBS; ++k) {
+    if (k < cw) {
+      const double xk = __builtin_bit_cast(double, ((uint64_t)(unsigned)__builtin_amdgcn_readlane(xhi, k) << 32) |
+                                                        (unsigned)__builtin_amdgcn_readlane(xlo, k));
+      acc = fma(-u[k], xk, acc);
+    }
+  }
+  return true;
+}
+
+// Block b (64 equations, lane = equation) of the persistent back
+// substitution.  Wave 0 owns the critical path: it keeps the diagonal
+// triangle in registers, takes the LAST hand-off (block b+1) itself and then
+// solves the triangle; waves 1..3 take the blocks below b+1 (their x are
+// published earlier) round-robin in the background and hand their partial
+// sums over through LDS behind one barrier.  Every load of a U block is
+// issued before its flag is polled.
 template <typename T>
 __global__ __launch_bounds__(256) void backsub_persist_kernel(const T* __restrict__ U, int64_t ldu,
                                                               const T* __restrict__ y, int64_t incy,
@@ -98,76 +155,39 @@ __global__ __launch_bounds__(256) void backsub_persist_kernel(const T* __restric
                                                               double* __restrict__ x,
                                                               double* __restrict__ bnorm, int n,
                                                               int unit, unsigned* flags, int* err) {
-  __shared__ double acc[kBS];
-  __shared__ int prow[kBS];
-  __shared__ int ok[2];
+  __shared__ double part[4][kBS];
   const int b = blockIdx.x, nb = gridDim.x;
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int r0 = b * kBS, rows = min(kBS, n - r0);
-  if (t < kBS) {
-    const int i = r0 + min(t, rows - 1);
-    const int pr = rowof(perm, i, n);
-    if (perm && perm[i] != pr) __hip_atomic_store(err, 7, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    prow[t] = pr;
-    const double v = (double)y[(int64_t)pr * incy];
-    acc[t] = v;
-    if (bnorm && t < rows) bnorm[i] = unit ? v : v / (double)U[(int64_t)pr * ldu + i];
-  }
-  double drow[kBS];
-  double rinv = 1.0;
-  if (wv == 0) load_diag<T>(U, ldu, perm, n, r0, rows, unit, drow, rinv);
-  __syncthreads();
-  // this wave's 16 equations of the block: their physical rows
-  int pr16[16];
-#pragma unroll
-  for (int k = 0; k < 16; ++k) pr16[k] = prow[min(wv * 16 + k, rows - 1)];
-  int it = 0;
-  for (int c = nb - 1; c > b; --c, ++it) {
-    const int c0 = c * kBS, cw = min(kBS, n - c0);
-    const int cl = c0 + min(lane, cw - 1);
-    // U[b rows, block c] does not depend on x: in flight before the wait
-    double uv[16];
-#pragma unroll
-    for (int k = 0; k < 16; ++k) uv[k] = (double)U[(int64_t)pr16[k] * ldu + cl];
-    if (t == 0) {
-      int good = 1;
-      if (__hip_atomic_load(&flags[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
-        const unsigned long long t0 = rtc();
-        while (__hip_atomic_load(&flags[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
-          if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0 ||
-              rtc() - t0 > kSpinTicks) {
-            __hip_atomic_store(err, 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            good = 0;
-            break;
-          }
-          __builtin_amdgcn_s_sleep(1);
-        }
-      }
-      ok[it & 1] = good;
-    }
-    __syncthreads();
-    if (!ok[it & 1]) return;
-    // x_c was stored write-through by its producer: agent-scope loads
-    const double xl = lane < cw
-                          ? __builtin_bit_cast(double, __hip_atomic_load(reinterpret_cast<unsigned long long*>(x + c0 + lane),
-                                                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
-                          : 0.0;
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-      const double v = dev::wave_sum(uv[k] * xl);
-      if (lane == 0 && wv * 16 + k < rows) acc[wv * 16 + k] -= v;
-    }
-  }
-  __syncthreads();
+  const int i = r0 + min(lane, rows - 1);
+  const int pr = rowof(perm, i, n);
+  if (wv == 0 && perm && lane < rows && perm[i] != pr)
+    __hip_atomic_store(err, 7, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  double acc = 0.0;
+  bool ok = true;
   if (wv == 0) {
-    const double xv = solve_diag(drow, rinv, acc[min(lane, rows - 1)], rows);
+    double drow[kBS];
+    double rinv = 1.0;
+    load_diag<T>(U, ldu, perm, n, r0, rows, unit, drow, rinv);
+    const double v = (double)y[(int64_t)pr * incy];
+    if (bnorm && lane < rows) bnorm[i] = unit ? v : v / (double)U[(int64_t)pr * ldu + i];
+    if (b + 1 < nb) ok = apply_block<T>(U, ldu, pr, b + 1, n, x, flags, err, false, acc);
+    __syncthreads();
+    if (!ok) return;
+    double yv = v + acc + part[1][lane] + part[2][lane] + part[3][lane];
+    const double xv = solve_diag(drow, rinv, yv, rows);
     if (lane < rows)
       __hip_atomic_store(reinterpret_cast<unsigned long long*>(x + r0 + lane), __builtin_bit_cast(unsigned long long, xv),
                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (lane == 0) __hip_atomic_store(&flags[b], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return;
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  // background waves: blocks nb-1 .. b+2, wave 1 + (nb-1-c) % 3
+  for (int c = nb - 1 - (wv - 1); c >= b + 2 && ok; c -= 3)
+    ok = apply_block<T>(U, ldu, pr, c, n, x, flags, err, true, acc);
+  part[wv][lane] = acc;  // 0 when the wave had no block
   __syncthreads();
-  if (t == 0) __hip_atomic_store(&flags[b], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // ---- fallback: one launch per block ----------------------------------------

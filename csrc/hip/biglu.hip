@@ -178,6 +178,19 @@ __device__ __forceinline__ int wave_argmax_lane(uint64_t k, unsigned row) {
   return __ffsll((long long)__ballot(c2 && row == mr)) - 1;
 }
 
+// First live column of a candidate row at column J: J - 1 (the row's own
+// multiplier of the pending update) and everything right of it.
+template <int J>
+constexpr int kLive = J > 0 ? J - 1 : 0;
+
+// Granule index g = participant * LW + column of a row sweep at column J,
+// with dead columns redirected to the participant's first live one: the
+// lanes then share that line and the sweep moves only the live bytes.
+template <int J>
+__device__ __forceinline__ int live_granule(int g) {
+  return (g % LW) < kLive<J> ? g - (g % LW) + kLive<J> : g;
+}
+
 template <int MODE, int NKK, int NR>
 struct Leaf {
   // one column J of the leaf (compile time); false: hand-off aborted
@@ -232,7 +245,10 @@ struct Leaf {
             }
           }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // wave-local LDS hand-off
-        if (lane < LW) {
+        // only columns J-1.. of the candidate row matter from column J on
+        // (J-1: the row's own multiplier of the pending update): the dead
+        // granules are neither stored nor read
+        if (lane < LW && lane >= kLive<J>) {
           const double x = sh.cand[lane];
           const __amdgpu_buffer_rsrc_t rr = rsrc(g.x.row + (int64_t)(slot + blockIdx.x) * LW, LW * 16);
           __builtin_amdgcn_raw_buffer_store_b128(u32x4{lo32(x), hi32(x), wrow, seq}, rr, lane * 16, 0, kAuxSc1);
@@ -275,7 +291,8 @@ struct Leaf {
       if constexpr (NR > 0) {
 #pragma unroll
         for (int k = 0; k < NR; ++k)
-          rw[k] = __builtin_amdgcn_raw_buffer_load_b128(rrw, min(k * 64 + lane, g.P * LW - 1) * 16, 0, kAuxSc1);
+          rw[k] = __builtin_amdgcn_raw_buffer_load_b128(rrw, min(live_granule<J>(k * 64 + lane), g.P * LW - 1) * 16, 0,
+                                                        kAuxSc1);
       }
       bool ready = true;
 #pragma unroll
@@ -324,11 +341,11 @@ struct Leaf {
 #pragma unroll
       for (int k = 1; k < NR; ++k) rv = (k == (pw >> 1)) ? rw[k] : rv;
     } else {
-      rv = __builtin_amdgcn_raw_buffer_load_b128(rrs, (lane & (LW - 1)) * 16, 0, kAuxSc1);
+      rv = __builtin_amdgcn_raw_buffer_load_b128(rrs, max(lane & (LW - 1), kLive<J>) * 16, 0, kAuxSc1);
     }
     int rl = 0;
-    while (__ballot(mine && rv.w != seq) != 0) {
-      rv = __builtin_amdgcn_raw_buffer_load_b128(rrs, (lane & (LW - 1)) * 16, 0, kAuxSc1);
+    while (__ballot(mine && (lane & (LW - 1)) >= kLive<J> && rv.w != seq) != 0) {
+      rv = __builtin_amdgcn_raw_buffer_load_b128(rrs, max(lane & (LW - 1), kLive<J>) * 16, 0, kAuxSc1);
       if ((++rl & 63) == 63 && __hip_atomic_load(g.info + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0)
         return false;
     }

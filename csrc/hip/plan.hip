@@ -177,7 +177,15 @@ __global__ void hybrid_perm_kernel(int* __restrict__ perm, int n, int split, int
   }
 }
 
-constexpr int64_t kBigNb = 256;          // outer panel width of the wide-panel engine
+// outer panel width of the wide-panel engine: 256 (GELIM_BIG_NB = 256 | 512)
+int64_t big_nb() {
+  static const int64_t nb = [] {
+    const char* e = std::getenv("GELIM_BIG_NB");
+    const int64_t v = e ? std::atoll(e) : 256;
+    return (v == 512 || v == 128) ? v : int64_t(256);
+  }();
+  return nb;
+}
 constexpr int64_t kBigPairSlot = 1 + 4 * 32 + 3;
 
 int enqueue(gelim_gauss_plan* p, const void* src, int64_t src_ld, void* dx, void* bnorm, hipStream_t s);
@@ -205,7 +213,7 @@ int panel_u12_update(gelim_gauss_plan* p, double* A, int64_t k, int64_t kend, in
 //   x[K..n) = tail solve of A[K:, K:] (already carrying every update),
 //   y = A[0:K, n] - A[0:K, K:n] x[K..n),  x[0..K) = U11^-1 y.
 //
-// Outer panels P_j = [k_j, k_j+1) of kBigNb columns, each factored as
+// Outer panels P_j = [k_j, k_j+1) of big_nb() columns, each factored as
 // 32-column leaves: per leaf the leaf itself (biglu.hip), its row movement
 // on the other columns + the TRSM of its U rows, and a rank-32 GEMM of the
 // columns right of it inside the panel.
@@ -228,8 +236,9 @@ int panel_u12_update(gelim_gauss_plan* p, double* A, int64_t k, int64_t kend, in
 int enqueue_big(gelim_gauss_plan* p, double* A, double* x, double* bnorm, hipStream_t s) {
   using namespace gelim;
   const int64_t n = p->n, lda = p->lda, K = p->big_k, LW = big::leaf_width();
-  const int64_t T = (K + kBigNb - 1) / kBigNb;
-  auto kb = [&](int64_t j) { return std::min(j * kBigNb, K); };  // P_j = [kb(j), kb(j+1))
+  const int64_t nbw = big_nb();
+  const int64_t T = (K + nbw - 1) / nbw;
+  auto kb = [&](int64_t j) { return std::min(j * nbw, K); };  // P_j = [kb(j), kb(j+1))
   const bool la = p->big_la;
   hipStream_t side = la ? p->big_side : s;
   hipEvent_t* ev_fork = la ? &p->big_ev[0] : nullptr;
@@ -502,7 +511,7 @@ extern "C" gelim_gauss_plan* gelim_gauss_plan_create(int64_t n, int algo, int pi
       } else if (hipStreamCreateWithFlags(&p->big_side, hipStreamNonBlocking) != hipSuccess) {
         return fail("side stream");
       }
-      const int64_t T = (big_k + kBigNb - 1) / kBigNb;
+      const int64_t T = (big_k + big_nb() - 1) / big_nb();
       p->big_ev.assign((size_t)(2 * T + 2), nullptr);
       for (auto& e : p->big_ev)
         if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return fail("event");

@@ -4,16 +4,21 @@
 //             one workgroup per output row, threads stride the columns.
 //  NAIVE_ELEM (K2 parity, CUDA_and_OpenMP/Version-2/cuda_matmul.cu:89-101):
 //             2-D grid, one thread per output element.
-//  MFMA       (K3', absent in the reference): 128x128x16 LDS-tiled GEMM on
-//             the exact-fp32 matrix cores (v_mfma_f32_32x32x2_f32), LDS
-//             double-buffered with one barrier per K-step, XCD-aware tile
-//             order.  4 wave64s per workgroup in a 2x2 arrangement, each wave
-//             owns a 64x64 sub-tile = 2x2 MFMA blocks (64 accumulator VGPRs).
-//             LDS holds A transposed ([k][m]) and B as is ([k][n]) so both
-//             fragment reads are unit-stride across lanes (conflict-free).
+//  MFMA       (K3', absent in the reference): LDS-tiled GEMM on the exact-fp32
+//             matrix cores (v_mfma_f32_32x32x2_f32), LDS double-buffered with
+//             one barrier per K-step, XCD-aware tile order.  4 wave64s per
+//             workgroup in a 2x2 arrangement; 64x64x16 tiles (one 32x32 MFMA
+//             block per wave, four workgroups per CU) or, when there are at
+//             least 2 such tiles per CU, 128x128x32 tiles (2x2 blocks per
+//             wave).  LDS holds A transposed ([k][m]) and B as is ([k][n]), so
+//             both fragment reads are unit-stride across lanes; rows padded
+//             by 4 floats (PMC: ~14 % LDS bank-conflict cycles remain on the
+//             transposed A stores, profiles/pmc_counters_2048.txt).
 // The naive kernels use 64-bit indexing (the reference's int products
 // overflow for n > 46340).
 #include <hip/hip_runtime.h>
+
+#include <cstdlib>
 
 #include "device_common.h"
 #include "gelim/internal.h"
@@ -51,26 +56,32 @@ __global__ void naive_elem_kernel(Mat p) {
   *c = p.acc ? *c + temp : temp;
 }
 
-// 64 x 64 tiles: 1024 workgroups at 2048^2, four co-resident per CU, so one
-// workgroup's LDS store + barrier hides under the others' MFMAs.  Measured
-// at 2048^2: 128x128 179 us, 128x64 170 us, 64x64 166 us (103.8 TFLOP/s);
-// BK = 32 is no better at either tile size.
-constexpr int BM = 64, BN = 64, BK = 16;
-constexpr int WM = BM / 2, WN = BN / 2;  // rows / columns per wave (2 x 2 waves)
+// Two tile shapes, picked per problem by the number of tiles per CU:
+//  * 64 x 64 x 16 when 128 x 128 tiles would leave fewer than 2 per CU (2048^2:
+//    1024 workgroups, four co-resident per CU, so one workgroup's LDS store +
+//    barrier hides under the others' MFMAs: 128x128 179 us, 128x64 170 us,
+//    64x64 166 us at 2048^2);
+//  * 128 x 128 x 32 (each wave 64 x 64 = 2 x 2 MFMA blocks: half the LDS
+//    fragment reads per MFMA) for larger problems, two workgroups per CU.
 constexpr int kMmThreads = 256;
 constexpr int APAD = 4, BPAD = 4;
 
-// float4s per thread for one A (BM x BK, k fastest) / B (BK x BN) tile
-constexpr int kFA = BM * BK / 4 / kMmThreads, kFB = BK * BN / 4 / kMmThreads;
-static_assert(kFA * 4 * kMmThreads == BM * BK && kFB * 4 * kMmThreads == BK * BN, "tile / threads");
-
-struct Frag {
-  float4 a[kFA];  // A tile: row = idx / (BK/4), k = 4 (idx % (BK/4)), idx = t + 256 h
-  float4 b[kFB];  // B tile: k = idx / (BN/4), col = 4 (idx % (BN/4))
+template <int BM, int BN, int BK>
+struct Tile {
+  static constexpr int WM = BM / 2, WN = BN / 2;  // rows / columns per wave (2 x 2 waves)
+  // float4s per thread for one A (BM x BK, k fastest) / B (BK x BN) tile
+  static constexpr int kFA = BM * BK / 4 / kMmThreads, kFB = BK * BN / 4 / kMmThreads;
+  static_assert(kFA * 4 * kMmThreads == BM * BK && kFB * 4 * kMmThreads == BK * BN, "tile / threads");
+  struct Frag {
+    float4 a[kFA];  // A tile: row = idx / (BK/4), k = 4 (idx % (BK/4)), idx = t + 256 h
+    float4 b[kFB];  // B tile: k = idx / (BN/4), col = 4 (idx % (BN/4))
+  };
 };
 
-template <bool CHECK>
-__device__ __forceinline__ void load_tiles(Frag& f, const Mat& p, int m0, int n0, int k0) {
+template <bool CHECK, int BM, int BN, int BK>
+__device__ __forceinline__ void load_tiles(typename Tile<BM, BN, BK>::Frag& f, const Mat& p, int m0, int n0,
+                                           int k0) {
+  constexpr int kFA = Tile<BM, BN, BK>::kFA, kFB = Tile<BM, BN, BK>::kFB;
   const float* __restrict__ A = p.A;
   const float* __restrict__ B = p.B;
   const int M = p.M, N = p.N, K = p.K;
@@ -106,8 +117,10 @@ __device__ __forceinline__ void load_tiles(Frag& f, const Mat& p, int m0, int n0
   }
 }
 
-__device__ __forceinline__ void store_tiles(const Frag& f, float (*As)[BM + APAD],
+template <int BM, int BN, int BK>
+__device__ __forceinline__ void store_tiles(const typename Tile<BM, BN, BK>::Frag& f, float (*As)[BM + APAD],
                                             float (*Bs)[BN + BPAD]) {
+  constexpr int kFA = Tile<BM, BN, BK>::kFA, kFB = Tile<BM, BN, BK>::kFB;
   const int t = threadIdx.x;
 #pragma unroll
   for (int h = 0; h < kFA; ++h) {
@@ -126,8 +139,10 @@ __device__ __forceinline__ void store_tiles(const Frag& f, float (*As)[BM + APAD
   }
 }
 
-template <bool CHECK>
+template <bool CHECK, int BM, int BN, int BK>
 __global__ __launch_bounds__(kMmThreads, 2) void mfma_gemm_kernel(Mat p, int tiles_n, int ntiles) {
+  using TL = Tile<BM, BN, BK>;
+  constexpr int WM = TL::WM, WN = TL::WN;
   const int M = p.M, N = p.N, K = p.K;
   __shared__ __attribute__((aligned(16))) float As[2][BK][BM + APAD];
   __shared__ __attribute__((aligned(16))) float Bs[2][BK][BN + BPAD];
@@ -152,15 +167,15 @@ __global__ __launch_bounds__(kMmThreads, 2) void mfma_gemm_kernel(Mat p, int til
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-  Frag f;
-  load_tiles<CHECK>(f, p, m0, n0, 0);
-  store_tiles(f, As[0], Bs[0]);
+  typename TL::Frag f;
+  load_tiles<CHECK, BM, BN, BK>(f, p, m0, n0, 0);
+  store_tiles<BM, BN, BK>(f, As[0], Bs[0]);
   __syncthreads();
 
   const int nk = (K + BK - 1) / BK;
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
-    if (kt + 1 < nk) load_tiles<CHECK>(f, p, m0, n0, (kt + 1) * BK);
+    if (kt + 1 < nk) load_tiles<CHECK, BM, BN, BK>(f, p, m0, n0, (kt + 1) * BK);
 #pragma unroll
     for (int k = 0; k < BK; k += 2) {
       const int kk = k + kh;
@@ -175,7 +190,7 @@ __global__ __launch_bounds__(kMmThreads, 2) void mfma_gemm_kernel(Mat p, int til
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(ai[i], bj, acc[i][j], 0, 0, 0);
       }
     }
-    if (kt + 1 < nk) store_tiles(f, As[cur ^ 1], Bs[cur ^ 1]);
+    if (kt + 1 < nk) store_tiles<BM, BN, BK>(f, As[cur ^ 1], Bs[cur ^ 1]);
     __syncthreads();
   }
 
@@ -195,6 +210,11 @@ __global__ __launch_bounds__(kMmThreads, 2) void mfma_gemm_kernel(Mat p, int til
       }
     }
 }
+
+template <int M_, int N_, int K_>
+struct Shape {
+  static constexpr int BM = M_, BN = N_, BK = K_;
+};
 
 }  // namespace
 
@@ -218,16 +238,27 @@ int matmul_f32(const float* A, int64_t lda, const float* B, int64_t ldb, float* 
       break;
     }
     case GELIM_MM_MFMA: {
-      const int tiles_m = (int)((M + BM - 1) / BM), tiles_n = (int)((N + BN - 1) / BN);
-      const int ntiles = tiles_m * tiles_n;
-      const bool aligned = (M % BM == 0) && (N % BN == 0) && (K % BK == 0) && (lda % 4 == 0) &&
-                           (ldb % 4 == 0) && ((uintptr_t)A % 16 == 0) && ((uintptr_t)B % 16 == 0);
-      if (aligned)
-        hipLaunchKernelGGL(mfma_gemm_kernel<false>, dim3(ntiles), dim3(kMmThreads), 0, s, p,
-                           tiles_n, ntiles);
-      else
-        hipLaunchKernelGGL(mfma_gemm_kernel<true>, dim3(ntiles), dim3(kMmThreads), 0, s, p,
-                           tiles_n, ntiles);
+      int cus = 256, dev = 0;
+      (void)hipGetDevice(&dev);
+      (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+      const int64_t big_tiles = ((M + 127) / 128) * ((N + 127) / 128);
+      const char* ev = std::getenv("GELIM_SGEMM_TILE");
+      const bool big = ev ? std::atoi(ev) == 128 : big_tiles >= 2 * (int64_t)cus;
+      auto launch = [&](auto tag) {
+        constexpr int BM = decltype(tag)::BM, BN = decltype(tag)::BN, BK = decltype(tag)::BK;
+        const int tiles_m = (int)((M + BM - 1) / BM), tiles_n = (int)((N + BN - 1) / BN);
+        const int ntiles = tiles_m * tiles_n;
+        const bool aligned = (M % BM == 0) && (N % BN == 0) && (K % BK == 0) && (lda % 4 == 0) &&
+                             (ldb % 4 == 0) && ((uintptr_t)A % 16 == 0) && ((uintptr_t)B % 16 == 0);
+        if (aligned)
+          hipLaunchKernelGGL((mfma_gemm_kernel<false, BM, BN, BK>), dim3(ntiles), dim3(kMmThreads), 0, s, p,
+                             tiles_n, ntiles);
+        else
+          hipLaunchKernelGGL((mfma_gemm_kernel<true, BM, BN, BK>), dim3(ntiles), dim3(kMmThreads), 0, s, p,
+                             tiles_n, ntiles);
+      };
+      if (big) launch(Shape<128, 128, 32>{});
+      else launch(Shape<64, 64, 16>{});
       break;
     }
     default:

@@ -628,6 +628,68 @@ __global__ __launch_bounds__(64) void laswp_panel_kernel(PanelSwapArgs g) {
   }
 }
 
+// ---- U12 of a whole outer panel in one launch --------------------------------
+// U12 = L11^-1 A12 for the nb (<= 256, multiple of LW) rows of an outer panel,
+// L11 unit lower.  One workgroup per 32 columns keeps its nb x 32 block of
+// A12 in LDS for the whole forward substitution: per 32-row block j, the
+// diagonal 32x32 solve (lane = column, registers) and the update of the
+// rows below (VALU, L staged in LDS, the solved block in registers).  This
+// replaces nb/32 alternating launches (32-row TRSM, then a K = 32 GEMM of
+// the rows below) -- 15 launches per 256-column panel.
+constexpr int kTrNb = 256;                    // max rows
+constexpr int kTrCols = 32;                   // columns per workgroup
+
+struct PanelTrsmArgs {
+  double* C;          // row 0 of the panel's rows, first column of the range
+  int64_t ldc;
+  int ncols, nb;
+  const double* L;    // L11 (nb x nb, unit lower), leading dimension ldl
+  int64_t ldl;
+};
+
+__global__ __launch_bounds__(256) void panel_trsm_kernel(PanelTrsmArgs g) {
+  extern __shared__ double trsm_lds[];
+  double (*X)[kTrCols + 1] = reinterpret_cast<double (*)[kTrCols + 1]>(trsm_lds);                  // [nb][33]
+  double (*Ls)[LW + 1] = reinterpret_cast<double (*)[LW + 1]>(trsm_lds + kTrNb * (kTrCols + 1));   // [nb][33]
+  const int t = threadIdx.x, col = t & 31, rg = t >> 5;  // 8 row groups
+  const int c0 = blockIdx.x * kTrCols;
+  const bool cok = c0 + col < g.ncols;
+  const int nb = g.nb;
+  double* cp = g.C + c0 + (cok ? col : 0);
+  for (int r = rg; r < nb; r += 8) X[r][col] = cok ? cp[(int64_t)r * g.ldc] : 0.0;
+  for (int j0 = 0; j0 < nb; j0 += LW) {
+    // L rows [j0, nb) x columns [j0, j0 + 32) into LDS
+    for (int e = t; e < (nb - j0) * LW; e += 256) Ls[e / LW][e % LW] = g.L[(int64_t)(j0 + e / LW) * g.ldl + j0 + e % LW];
+    __syncthreads();
+    if (t < kTrCols) {  // diagonal block, lane = column
+      double x[LW];
+#pragma unroll
+      for (int i = 0; i < LW; ++i) x[i] = X[j0 + i][col];
+#pragma unroll
+      for (int i = 0; i < LW; ++i)
+#pragma unroll
+        for (int r = i + 1; r < LW; ++r) x[r] = fma(-Ls[r][i], x[i], x[r]);
+#pragma unroll
+      for (int i = 0; i < LW; ++i) X[j0 + i][col] = x[i];
+    }
+    __syncthreads();
+    if (j0 + LW < nb) {
+      double xj[LW];
+#pragma unroll
+      for (int i = 0; i < LW; ++i) xj[i] = X[j0 + i][col];
+      for (int r = j0 + LW + rg; r < nb; r += 8) {
+        double acc = X[r][col];
+#pragma unroll
+        for (int i = 0; i < LW; ++i) acc = fma(-Ls[r - j0][i], xj[i], acc);
+        X[r][col] = acc;
+      }
+    }
+    __syncthreads();
+  }
+  if (cok)
+    for (int r = rg; r < nb; r += 8) cp[(int64_t)r * g.ldc] = X[r][col];
+}
+
 // ---- block back substitution helpers ----------------------------------------
 // y[i] = A[i][n] - sum_{j >= K} A[i][j] x[j] for the top K rows (x[K..n) is
 // the solved tail), bnorm[i] = A[i][n] / A[i][i] (the reference's normalised
@@ -740,6 +802,32 @@ int laswp_panel(double* A, int64_t lda, int64_t n, int64_t c0, int nleaves, cons
   return GELIM_OK;
 }
 
+// U12 = L11^-1 C for the nb rows of C (ldc) over ncols columns, L11 the unit
+// lower nb x nb block at L (ldl); nb <= 256, a multiple of 32.
+// GELIM_TRSM_FUSED=0: the per-32-row-block TRSM + GEMM sequence instead
+bool trsm_fused() {
+  static const bool v = [] {
+    const char* e = std::getenv("GELIM_TRSM_FUSED");
+    return !(e && std::atoi(e) == 0);
+  }();
+  return v;
+}
+
+int panel_trsm(double* C, int64_t ldc, int64_t ncols, int64_t nb, const double* L, int64_t ldl, hipStream_t s) {
+  if (ncols <= 0) return GELIM_OK;
+  if (nb <= 0 || nb > kTrNb || nb % LW) return GELIM_FAIL(GELIM_E_ARG, "panel_trsm: nb must be a multiple of 32 <= 256");
+  PanelTrsmArgs a{C, ldc, (int)ncols, (int)nb, L, ldl};
+  const size_t lds = sizeof(double) * (size_t)kTrNb * (kTrCols + 1) * 2;
+  static bool attr = [] {
+    return hipFuncSetAttribute((const void*)panel_trsm_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)(sizeof(double) * (size_t)kTrNb * (kTrCols + 1) * 2)) == hipSuccess;
+  }();
+  (void)attr;
+  hipLaunchKernelGGL(panel_trsm_kernel, dim3((unsigned)((ncols + kTrCols - 1) / kTrCols)), dim3(256), lds, s, a);
+  HIP_TRY(hipGetLastError());
+  return GELIM_OK;
+}
+
 int tail_gemv(const double* A, int64_t lda, int64_t n, int64_t K, const double* x, double* y, double* bnorm,
               hipStream_t s) {
   if (K <= 0) return GELIM_OK;
@@ -799,6 +887,11 @@ extern "C" int gelim_gpu_laswp_panel(double* dA, int64_t lda, int64_t n, int64_t
                                      const int32_t* dpairs, int64_t slot, int64_t lbeg, int64_t lend, int64_t rbeg,
                                      int64_t rend, void* stream) {
   return gelim::big::laswp_panel(dA, lda, n, c0, nleaves, dpairs, slot, lbeg, lend, rbeg, rend, (hipStream_t)stream);
+}
+
+extern "C" int gelim_gpu_panel_trsm(double* dC, int64_t ldc, int64_t ncols, int64_t nb, const double* dL, int64_t ldl,
+                                    void* stream) {
+  return gelim::big::panel_trsm(dC, ldc, ncols, nb, dL, ldl, (hipStream_t)stream);
 }
 
 extern "C" int64_t gelim_gpu_leaf_workspace_bytes(void) { return (int64_t)gelim::big::workspace_bytes(); }

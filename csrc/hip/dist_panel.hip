@@ -37,6 +37,8 @@ int laswp_trsm(double* A, int64_t lda, int64_t c0, int64_t lbeg, int64_t lend, i
                int64_t trsm_end, int64_t nrows, const int* pairs, hipStream_t s, const double* L, int64_t ldl);
 int laswp_panel(double* A, int64_t lda, int64_t n, int64_t c0, int nleaves, const int* pairs, int64_t slot,
                 int64_t lbeg, int64_t lend, int64_t rbeg, int64_t rend, hipStream_t s);
+int panel_trsm(double* C, int64_t ldc, int64_t ncols, int64_t nb, const double* L, int64_t ldl, hipStream_t s);
+bool trsm_fused();
 }  // namespace big
 }  // namespace gelim
 
@@ -89,13 +91,17 @@ extern "C" int gelim_dist_panel_apply(double* C, int64_t ldc, int64_t n, int64_t
     return GELIM_FAIL(GELIM_E_ARG, "dist_panel_apply: widths must be multiples of 32 (even offsets)");
   const int nl = (int)(wg / kLW);
   GELIM_TRY(big::laswp_panel(C, ldc, n, k, nl, pairs, kSlot, 0, 0, cb, ce, s));
-  for (int64_t j = 0; j < nl; ++j) {
-    const int64_t r = k + j * kLW;
-    GELIM_TRY(big::laswp_trsm(C + r * ldc, ldc, 0, 0, 0, cb, ce, ce, n - r, nullptr, s, L + (j * kLW) * ldl + j * kLW,
-                              ldl));
-    if (j + 1 < nl)
-      GELIM_TRY(dgemm(C + (r + kLW) * ldc + cb, ldc, L + ((j + 1) * kLW) * ldl + j * kLW, ldl, C + r * ldc + cb, ldc,
-                      wg - (j + 1) * kLW, ce - cb, kLW, -1.0, s));
+  if (big::trsm_fused() && wg <= 256) {
+    GELIM_TRY(big::panel_trsm(C + k * ldc + cb, ldc, ce - cb, wg, L, ldl, s));
+  } else {
+    for (int64_t j = 0; j < nl; ++j) {
+      const int64_t r = k + j * kLW;
+      GELIM_TRY(big::laswp_trsm(C + r * ldc, ldc, 0, 0, 0, cb, ce, ce, n - r, nullptr, s,
+                                L + (j * kLW) * ldl + j * kLW, ldl));
+      if (j + 1 < nl)
+        GELIM_TRY(dgemm(C + (r + kLW) * ldc + cb, ldc, L + ((j + 1) * kLW) * ldl + j * kLW, ldl, C + r * ldc + cb,
+                        ldc, wg - (j + 1) * kLW, ce - cb, kLW, -1.0, s));
+    }
   }
   if (k + wg < n)
     GELIM_TRY(dgemm(C + (k + wg) * ldc + cb, ldc, L + wg * ldl, ldl, C + k * ldc + cb, ldc, n - k - wg, ce - cb, wg,

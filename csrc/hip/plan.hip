@@ -49,6 +49,8 @@ int laswp_trsm(double* A, int64_t lda, int64_t c0, int64_t lbeg, int64_t lend, i
                int64_t ldl = 0);
 int laswp_panel(double* A, int64_t lda, int64_t n, int64_t c0, int nleaves, const int* pairs, int64_t slot,
                 int64_t lbeg, int64_t lend, int64_t rbeg, int64_t rend, hipStream_t s);
+int panel_trsm(double* C, int64_t ldc, int64_t ncols, int64_t nb, const double* L, int64_t ldl, hipStream_t s);
+bool trsm_fused();
 int tail_gemv(const double* A, int64_t lda, int64_t n, int64_t K, const double* x, double* y, double* bnorm,
               hipStream_t s);
 int fold_info(int* info, const int* tinfo, int64_t K, hipStream_t s);
@@ -198,11 +200,15 @@ int panel_u12_update(gelim_gauss_plan* p, double* A, int64_t k, int64_t kend, in
   using namespace gelim;
   const int64_t n = p->n, lda = p->lda, LW = big::leaf_width();
   if (ce <= cb) return GELIM_OK;
-  for (int64_t r = k; r < kend; r += LW) {
-    GELIM_TRY(big::laswp_trsm(A + r * lda, lda, r, 0, 0, cb, ce, ce, n - r, nullptr, s));
-    if (r + LW < kend)
-      GELIM_TRY(dgemm(A + (r + LW) * lda + cb, lda, A + (r + LW) * lda + r, lda, A + r * lda + cb, lda,
-                      kend - r - LW, ce - cb, LW, -1.0, s));
+  if (big::trsm_fused()) {
+    GELIM_TRY(big::panel_trsm(A + k * lda + cb, lda, ce - cb, kend - k, A + k * lda + k, lda, s));
+  } else {
+    for (int64_t r = k; r < kend; r += LW) {
+      GELIM_TRY(big::laswp_trsm(A + r * lda, lda, r, 0, 0, cb, ce, ce, n - r, nullptr, s));
+      if (r + LW < kend)
+        GELIM_TRY(dgemm(A + (r + LW) * lda + cb, lda, A + (r + LW) * lda + r, lda, A + r * lda + cb, lda,
+                        kend - r - LW, ce - cb, LW, -1.0, s));
+    }
   }
   return dgemm(A + kend * lda + cb, lda, A + kend * lda + k, lda, A + k * lda + cb, lda, n - kend, ce - cb,
                kend - k, -1.0, s);

@@ -179,6 +179,10 @@ int gelim_gpu_laswp_trsm(double* dA, int64_t lda, int64_t c0, int64_t lend, int6
 /* a whole outer panel's interchanges (nleaves leaf pair lists, `slot` ints
  * apart, diagonals c0, c0 + 32, ...) on columns [lbeg, lend) and
  * [rbeg, rend) of the n-row system at dA (row 0, column 0) */
+/* U12 = L11^-1 C: nb (<= 256, multiple of 32) rows of C over ncols columns,
+ * L11 the unit-lower nb x nb block at dL */
+int gelim_gpu_panel_trsm(double* dC, int64_t ldc, int64_t ncols, int64_t nb, const double* dL, int64_t ldl,
+                         void* stream);
 int gelim_gpu_laswp_panel(double* dA, int64_t lda, int64_t n, int64_t c0, int nleaves, const int32_t* dpairs,
                           int64_t slot, int64_t lbeg, int64_t lend, int64_t rbeg, int64_t rend, void* stream);
 int gelim_gpu_gemm_update(double* dC, int64_t ldc, const double* dL,

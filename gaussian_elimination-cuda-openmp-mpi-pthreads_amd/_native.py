@@ -76,6 +76,7 @@ _PROTOS = {
     "gelim_dist_pair_slot": (_i64, []),
     "gelim_dist_panel_factor": (_int, [_vp, _i64, _i64, _i64, _i64, _i64, _int, _vp, _vp, _vp, _vp, _int, _vp]),
     "gelim_dist_panel_apply": (_int, [_vp, _i64, _i64, _i64, _i64, _i64, _vp, _i64, _i64, _vp, _vp]),
+    "gelim_gpu_panel_trsm": (_int, [_vp, _i64, _i64, _i64, _vp, _i64, _vp]),
     "gelim_gpu_laswp_panel": (_int, [_vp, _i64, _i64, _i64, _int, _vp, _i64, _i64, _i64, _i64, _i64, _vp]),
     "gelim_gpu_backsub": (_int, [_vp, _i64, _vp, _i64, _vp, _vp, _i64, _int, _vp]),
     "gelim_gauss_plan_create": (_vp, [_i64, _int, _int, _int, _int]),

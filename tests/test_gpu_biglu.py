@@ -276,3 +276,24 @@ def test_laswp_panel_matches_sequential(gelim, cuda):
     _native.check(rc, "laswp_panel")
     torch.cuda.synchronize()
     assert torch.equal(Ag.cpu(), ref)
+
+
+@pytest.mark.parametrize("nb,ncols", [(256, 1000), (32, 70), (160, 33), (256, 8193)])
+def test_panel_trsm_matches_torch(gelim, cuda, nb, ncols):
+    """The one-launch U12 = L11^-1 A12 of an outer panel (nb rows, unit lower
+    L11) against torch's triangular solve."""
+    from gelim import _native
+    from gelim.utils.tensors import ptr, stream_handle
+
+    torch.manual_seed(nb + ncols)
+    ld = ncols + 6
+    L = torch.randn(nb, nb + 4, dtype=torch.float64) * 0.1
+    C = torch.randn(nb, ld, dtype=torch.float64)
+    L11 = torch.tril(L[:, :nb], -1) + torch.eye(nb, dtype=torch.float64)
+    ref = torch.linalg.solve_triangular(L11, C[:, :ncols], upper=False, unitriangular=True)
+    Cg, Lg = C.to(cuda), L.to(cuda)
+    rc = _native.lib().gelim_gpu_panel_trsm(ptr(Cg), ld, ncols, nb, ptr(Lg), nb + 4, stream_handle(cuda))
+    _native.check(rc, "panel_trsm")
+    torch.cuda.synchronize()
+    assert torch.allclose(Cg.cpu()[:, :ncols], ref, rtol=1e-11, atol=1e-11)
+    assert torch.equal(Cg.cpu()[:, ncols:], C[:, ncols:])

@@ -647,19 +647,23 @@ struct PanelTrsmArgs {
   int64_t ldl;
 };
 
-__global__ __launch_bounds__(256) void panel_trsm_kernel(PanelTrsmArgs g) {
+constexpr int kTrThreads = 512;                // 16 row groups of 32 columns
+constexpr int kTrGroups = kTrThreads / kTrCols;
+
+__global__ __launch_bounds__(kTrThreads) void panel_trsm_kernel(PanelTrsmArgs g) {
   extern __shared__ double trsm_lds[];
   double (*X)[kTrCols + 1] = reinterpret_cast<double (*)[kTrCols + 1]>(trsm_lds);                  // [nb][33]
-  double (*Ls)[LW + 1] = reinterpret_cast<double (*)[LW + 1]>(trsm_lds + kTrNb * (kTrCols + 1));   // [nb][33]
-  const int t = threadIdx.x, col = t & 31, rg = t >> 5;  // 8 row groups
+  // L rows [j0, nb) x 32 columns, rows 16-byte aligned (34 doubles)
+  double (*Ls)[LW + 2] = reinterpret_cast<double (*)[LW + 2]>(trsm_lds + kTrNb * (kTrCols + 1));
+  const int t = threadIdx.x, col = t & 31, rg = t >> 5;
   const int c0 = blockIdx.x * kTrCols;
   const bool cok = c0 + col < g.ncols;
   const int nb = g.nb;
   double* cp = g.C + c0 + (cok ? col : 0);
-  for (int r = rg; r < nb; r += 8) X[r][col] = cok ? cp[(int64_t)r * g.ldc] : 0.0;
+  for (int r = rg; r < nb; r += kTrGroups) X[r][col] = cok ? cp[(int64_t)r * g.ldc] : 0.0;
   for (int j0 = 0; j0 < nb; j0 += LW) {
-    // L rows [j0, nb) x columns [j0, j0 + 32) into LDS
-    for (int e = t; e < (nb - j0) * LW; e += 256) Ls[e / LW][e % LW] = g.L[(int64_t)(j0 + e / LW) * g.ldl + j0 + e % LW];
+    for (int e = t; e < (nb - j0) * LW; e += kTrThreads)
+      Ls[e / LW][e % LW] = g.L[(int64_t)(j0 + e / LW) * g.ldl + j0 + e % LW];
     __syncthreads();
     if (t < kTrCols) {  // diagonal block, lane = column
       double x[LW];
@@ -677,17 +681,27 @@ __global__ __launch_bounds__(256) void panel_trsm_kernel(PanelTrsmArgs g) {
       double xj[LW];
 #pragma unroll
       for (int i = 0; i < LW; ++i) xj[i] = X[j0 + i][col];
-      for (int r = j0 + LW + rg; r < nb; r += 8) {
+      for (int r = j0 + LW + rg; r < nb; r += kTrGroups) {
+        // the row's 32 multipliers: 16 uniform 16-byte LDS reads, then the
+        // dot product from registers
+        const double2* lr = reinterpret_cast<const double2*>(&Ls[r - j0][0]);
+        double l[LW];
+#pragma unroll
+        for (int i = 0; i < LW / 2; ++i) {
+          const double2 v = lr[i];
+          l[2 * i] = v.x;
+          l[2 * i + 1] = v.y;
+        }
         double acc = X[r][col];
 #pragma unroll
-        for (int i = 0; i < LW; ++i) acc = fma(-Ls[r - j0][i], xj[i], acc);
+        for (int i = 0; i < LW; ++i) acc = fma(-l[i], xj[i], acc);
         X[r][col] = acc;
       }
     }
     __syncthreads();
   }
   if (cok)
-    for (int r = rg; r < nb; r += 8) cp[(int64_t)r * g.ldc] = X[r][col];
+    for (int r = rg; r < nb; r += kTrGroups) cp[(int64_t)r * g.ldc] = X[r][col];
 }
 
 // ---- block back substitution helpers ----------------------------------------
@@ -817,13 +831,14 @@ int panel_trsm(double* C, int64_t ldc, int64_t ncols, int64_t nb, const double* 
   if (ncols <= 0) return GELIM_OK;
   if (nb <= 0 || nb > kTrNb || nb % LW) return GELIM_FAIL(GELIM_E_ARG, "panel_trsm: nb must be a multiple of 32 <= 256");
   PanelTrsmArgs a{C, ldc, (int)ncols, (int)nb, L, ldl};
-  const size_t lds = sizeof(double) * (size_t)kTrNb * (kTrCols + 1) * 2;
+  constexpr size_t lds = sizeof(double) * (size_t)kTrNb * ((kTrCols + 1) + (LW + 2));
   static bool attr = [] {
     return hipFuncSetAttribute((const void*)panel_trsm_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                               (int)(sizeof(double) * (size_t)kTrNb * (kTrCols + 1) * 2)) == hipSuccess;
+                               (int)lds) == hipSuccess;
   }();
   (void)attr;
-  hipLaunchKernelGGL(panel_trsm_kernel, dim3((unsigned)((ncols + kTrCols - 1) / kTrCols)), dim3(256), lds, s, a);
+  hipLaunchKernelGGL(panel_trsm_kernel, dim3((unsigned)((ncols + kTrCols - 1) / kTrCols)), dim3(kTrThreads), lds, s,
+                     a);
   HIP_TRY(hipGetLastError());
   return GELIM_OK;
 }

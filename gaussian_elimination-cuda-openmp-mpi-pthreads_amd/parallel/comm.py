@@ -130,6 +130,11 @@ def init_from_env(backend: str | None = None, device: str | None = None,
     if world <= 1:
         return Communicator(0, 1, dev, "none")
     backend = backend or ("nccl" if use_gpu else "gloo")
+    # failure detection: a rank that dies or hangs must not leave the others
+    # blocked forever.  RCCL's async error handling turns a collective that
+    # exceeds `timeout_s` (or a communicator error) into an abort + host
+    # exception on every surviving rank; gloo raises on the same timeout.
+    os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", "29511")
     if not dist.is_initialized():

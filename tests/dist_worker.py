@@ -9,12 +9,33 @@ from pathlib import Path
 sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
 
 
-def _init(rank, world, port, device):
+def _init(rank, world, port, device, timeout_s=120):
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK="0" if device == "cuda" else str(rank),
                       MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     from gelim.parallel import comm as C
 
-    return C.init_from_env(device=device if device == "cpu" else "cuda:0", timeout_s=120)
+    return C.init_from_env(device=device if device == "cpu" else "cuda:0", timeout_s=timeout_s)
+
+
+def dead_rank(rank, world, port, outdir):
+    """Failure detection: rank 1 dies right after joining; the survivors'
+    next collective (the distributed solve's first panel broadcast) must
+    raise within the communicator timeout instead of hanging."""
+    import time
+
+    from gelim.parallel import DistributedGauss
+
+    comm = _init(rank, world, port, "cpu", timeout_s=15)
+    if rank == 1:
+        os._exit(3)
+    t0 = time.perf_counter()
+    try:
+        dg = DistributedGauss(comm, 96, block=16)
+        dg.solve_(dg.generate_random(seed=1))
+        (Path(outdir) / f"ok{rank}.txt").write_text("finished")
+    except Exception as e:  # noqa: BLE001
+        (Path(outdir) / f"raised{rank}.txt").write_text(f"{time.perf_counter() - t0:.1f} {type(e).__name__}: {e}")
+    os._exit(0)
 
 
 def gauss(rank, world, port, outdir, n, block, seed, device, mode):

@@ -84,3 +84,14 @@ def test_column_layout():
     assert L.first_local_col_after(0, 0) == 16 and L.first_local_col_after(2, 0) == 16
     assert L.first_local_col_after(3, 0) == 32 and L.first_local_col_after(6, 0) == 36
     assert L.first_local_col_after(0, 1) == 0 and L.first_local_col_after(1, 1) == 16
+
+
+def test_dead_rank_raises_not_hangs(tmp_path):
+    """A rank that dies mid-job: the surviving ranks' collectives raise
+    (communicator timeout 15 s) instead of blocking forever."""
+    codes = _spawn(dist_worker.dead_rank, 3, _port(), str(tmp_path))
+    assert codes[1] == 3
+    for r in (0, 2):
+        f = tmp_path / f"raised{r}.txt"
+        assert f.exists(), (codes, list(tmp_path.iterdir()))
+        assert float(f.read_text().split()[0]) < 120

@@ -58,7 +58,7 @@ def parse():
     p.add_argument("--no-matmul", action="store_true")
     p.add_argument("--headline-only", action="store_true",
                    help="skip the distributed / 8192 / hip-pivot / external-matrix sections")
-    p.add_argument("--budget", type=float, default=900.0,
+    p.add_argument("--budget", type=float, default=400.0,
                    help="seconds the sections after the headline may take before the line is printed without "
                         "the missing ones (a hung collective never costs the headline)")
     p.add_argument("--measure-seq", action="store_true",

@@ -96,6 +96,14 @@ class Communicator:
     def recv(self, t: torch.Tensor, src: int):
         return dist.irecv(t, src=self.global_rank(src), group=self.group)
 
+    def sendrecv(self, send_t: torch.Tensor, dst: int, recv_t: torch.Tensor, src: int) -> list:
+        """Send to dst and receive from src as ONE batched p2p operation
+        (batch_isend_irecv: RCCL group semantics, so a ring of such calls
+        cannot deadlock on serialised send kernels).  Returns the requests."""
+        ops = [dist.P2POp(dist.isend, send_t, self.global_rank(dst), self.group),
+               dist.P2POp(dist.irecv, recv_t, self.global_rank(src), self.group)]
+        return dist.batch_isend_irecv(ops)
+
     def global_rank(self, r: int) -> int:
         if self.group is None:
             return r

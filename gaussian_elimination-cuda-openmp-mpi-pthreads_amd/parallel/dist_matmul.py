@@ -14,7 +14,7 @@ ring_matmul (1-D)
   A and C row-partitioned, B row-partitioned into P k-blocks.  P steps: each
   rank multiplies its A slice against the B block it currently holds
   (accumulating into C with the MFMA kernel) while that block is passed to
-  the next rank with isend/irecv on the communication stream — i.e. an
+  the next rank with one batched isend/irecv on the communication stream — i.e. an
   all-gather of B overlapped with compute, never materialising B whole.
   Per step each GPU sends/receives one K/P x N block over one xGMI link.
 
@@ -71,7 +71,7 @@ def ring_matmul(comm: Communicator, A_loc: torch.Tensor, B_loc: torch.Tensor, ke
         reqs = []
         nxt = bufs[t % 2] if t < P - 1 else None
         if t < P - 1:
-            reqs = [comm.send(cur, (r + 1) % P), comm.recv(nxt, (r - 1) % P)]
+            reqs = comm.sendrecv(cur, (r + 1) % P, nxt, (r - 1) % P)
         matmul_acc_(C, A_loc[:, src * kb:(src + 1) * kb], cur, accumulate=t > 0, kernel=kernel)
         for q in reqs:
             q.wait()

@@ -163,6 +163,9 @@ class EmulatedComm(Communicator):
     def recv(self, t: torch.Tensor, src: int):
         return _RecvReq(self._w.box(src, self.rank), t, self._w.timeout_s)
 
+    def sendrecv(self, send_t: torch.Tensor, dst: int, recv_t: torch.Tensor, src: int) -> list:
+        return [self.send(send_t, dst), self.recv(recv_t, src)]
+
     def global_rank(self, r: int) -> int:
         return r
 

@@ -600,9 +600,7 @@ struct PanelSwapArgs {
   int lbeg, lend, rbeg, rend;  // columns [lbeg, lend) and [rbeg, rend)
 };
 
-__global__ __launch_bounds__(64) void laswp_panel_kernel(PanelSwapArgs g) {
-  const int idx = blockIdx.x * 64 + threadIdx.x;
-  const int nl = g.lend - g.lbeg, nr = g.rend - g.rbeg;
+__device__ __forceinline__ void laswp_panel_block(const PanelSwapArgs& g, int idx, int nl, int nr) {
   const bool any = idx < nl + nr;
   // lanes past the ranges read a valid column and store nothing (no early
   // exit: the loop below stays uniform)
@@ -628,6 +626,108 @@ __global__ __launch_bounds__(64) void laswp_panel_kernel(PanelSwapArgs g) {
   }
 }
 
+__global__ __launch_bounds__(64) void laswp_panel_kernel(PanelSwapArgs g) {
+  const int nl = g.lend - g.lbeg, nr = g.rend - g.rbeg;
+  // grid-stride over 64-column blocks (a capped grid on the lookahead side
+  // stream); the block index is wave-uniform, so the loop is too
+  for (int blk = blockIdx.x; blk * 64 < nl + nr; blk += gridDim.x)
+    laswp_panel_block(g, blk * 64 + threadIdx.x, nl, nr);
+}
+
+// ---- an outer panel's row movement as ONE permutation -------------------------
+// laswp_panel replays the leaves' lists one after another per column (a chain
+// of dependent gathers: ~90 us whatever the width).  Composed once, the
+// panel's movement is a single permutation of <= 64 rows per leaf, applied
+// by a plain gather-then-scatter over (row, column) tiles.
+//
+// compose: one workgroup folds the nleaves pair lists (rows relative to
+// each leaf's diagonal c0 + 32 l) into the net list {count, (dst, src)...}
+// of rows relative to c0.  LDS holds, for every row position of the panel's
+// m rows, the original row now sitting there.
+struct ComposeArgs {
+  int m;              // rows from c0 to the end of the system
+  int nleaves;
+  const int* pairs;   // nleaves slots of `slot` ints
+  int slot;
+  int* net;           // [0] = count, then (dst, src) relative to c0
+};
+constexpr int kCmpThreads = 1024;
+
+__global__ __launch_bounds__(kCmpThreads) void compose_kernel(ComposeArgs g) {
+  extern __shared__ int content[];  // [m] + 1 counter
+  const int t = threadIdx.x;
+  for (int i = t; i < g.m; i += kCmpThreads) content[i] = i;
+  if (t == 0) content[g.m] = 0;
+  __syncthreads();
+  for (int l = 0; l < g.nleaves; ++l) {
+    const int* pr = g.pairs + (int64_t)l * g.slot;
+    const int cnt = min(pr[0], 2 * LW);
+    const int base = l * LW;
+    int v = 0, dst = -1;
+    if (t < cnt) {
+      const int d = base + pr[1 + 2 * t], sr = base + pr[2 + 2 * t];
+      if (d >= base && d < g.m && sr >= base && sr < g.m) {
+        v = content[sr];
+        dst = d;
+      }
+    }
+    __syncthreads();  // every source read before any destination is written
+    if (dst >= 0) content[dst] = v;
+    __syncthreads();
+  }
+  for (int i = t; i < g.m; i += kCmpThreads) {
+    const int r = content[i];
+    if (r != i) {
+      const int e = atomicAdd(&content[g.m], 1);
+      g.net[1 + 2 * e] = i;
+      g.net[2 + 2 * e] = r;
+    }
+  }
+  __syncthreads();
+  if (t == 0) g.net[0] = content[g.m];
+}
+
+// apply: 16 columns x all moved rows per workgroup, every source value in
+// registers (<= 512 rows: 32 per thread) before the barrier, then the
+// stores; a grid-stride loop over 16-column chunks of [lbeg, lend) and
+// [rbeg, rend).  Workgroups touch disjoint columns, so no cross-workgroup
+// ordering is needed.
+struct NetSwapArgs {
+  double* A;          // row c0, column 0 of the system
+  int64_t lda;
+  const int* net;
+  int lbeg, lend, rbeg, rend;
+};
+constexpr int kNsCols = 16, kNsThreads = 256, kNsGroups = kNsThreads / kNsCols;
+constexpr int kNsPer = 32, kNsMax = kNsGroups * kNsPer;  // 512 rows
+
+__global__ __launch_bounds__(kNsThreads) void laswp_net_kernel(NetSwapArgs g) {
+  __shared__ int2 lst[kNsMax];
+  const int t = threadIdx.x, cl = t % kNsCols, rg = t / kNsCols;
+  const int cnt = min(g.net[0], kNsMax);
+  if (cnt <= 0) return;
+  for (int e = t; e < cnt; e += kNsThreads) lst[e] = make_int2(g.net[1 + 2 * e], g.net[2 + 2 * e]);
+  __syncthreads();
+  const int nl = g.lend - g.lbeg, nr = g.rend - g.rbeg;
+  const int nch = (nl + nr + kNsCols - 1) / kNsCols;
+  for (int ch = blockIdx.x; ch < nch; ch += gridDim.x) {
+    const int idx = ch * kNsCols + cl;
+    const bool any = idx < nl + nr;
+    const int c = any ? (idx < nl ? g.lbeg + idx : g.rbeg + idx - nl) : (nl > 0 ? g.lbeg : g.rbeg);
+    double v[kNsPer];
+#pragma unroll
+    for (int k = 0; k < kNsPer; ++k) v[k] = g.A[(int64_t)lst[min(rg + k * kNsGroups, cnt - 1)].y * g.lda + c];
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every gather landed before any scatter
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kNsPer; ++k) {
+      const int e = rg + k * kNsGroups;
+      if (any && e < cnt) g.A[(int64_t)lst[e].x * g.lda + c] = v[k];
+    }
+    __syncthreads();  // (the gathers of the next chunk read other columns; kept for clarity of the LDS list)
+  }
+}
+
 // ---- U12 of a whole outer panel in one launch --------------------------------
 // U12 = L11^-1 A12 for the nb (<= 256, multiple of LW) rows of an outer panel,
 // L11 unit lower.  One workgroup per 32 columns keeps its nb x 32 block of
@@ -650,13 +750,9 @@ struct PanelTrsmArgs {
 constexpr int kTrThreads = 512;                // 16 row groups of 32 columns
 constexpr int kTrGroups = kTrThreads / kTrCols;
 
-__global__ __launch_bounds__(kTrThreads) void panel_trsm_kernel(PanelTrsmArgs g) {
-  extern __shared__ double trsm_lds[];
-  double (*X)[kTrCols + 1] = reinterpret_cast<double (*)[kTrCols + 1]>(trsm_lds);                  // [nb][33]
-  // L rows [j0, nb) x 32 columns, rows 16-byte aligned (34 doubles)
-  double (*Ls)[LW + 2] = reinterpret_cast<double (*)[LW + 2]>(trsm_lds + kTrNb * (kTrCols + 1));
-  const int t = threadIdx.x, col = t & 31, rg = t >> 5;
-  const int c0 = blockIdx.x * kTrCols;
+// one 32-column block [c0, c0 + 32) of the range
+__device__ __forceinline__ void panel_trsm_block(const PanelTrsmArgs& g, double (*X)[kTrCols + 1],
+                                                 double (*Ls)[LW + 2], int t, int col, int rg, int c0) {
   const bool cok = c0 + col < g.ncols;
   const int nb = g.nb;
   double* cp = g.C + c0 + (cok ? col : 0);
@@ -702,6 +798,18 @@ __global__ __launch_bounds__(kTrThreads) void panel_trsm_kernel(PanelTrsmArgs g)
   }
   if (cok)
     for (int r = rg; r < nb; r += kTrGroups) cp[(int64_t)r * g.ldc] = X[r][col];
+}
+
+__global__ __launch_bounds__(kTrThreads) void panel_trsm_kernel(PanelTrsmArgs g) {
+  extern __shared__ double trsm_lds[];
+  double (*X)[kTrCols + 1] = reinterpret_cast<double (*)[kTrCols + 1]>(trsm_lds);                  // [nb][33]
+  // L rows [j0, nb) x 32 columns, rows 16-byte aligned (34 doubles)
+  double (*Ls)[LW + 2] = reinterpret_cast<double (*)[LW + 2]>(trsm_lds + kTrNb * (kTrCols + 1));
+  const int t = threadIdx.x, col = t & 31, rg = t >> 5;
+  // grid-stride over 32-column blocks (a capped grid on the lookahead side
+  // stream); every loop below ends in a barrier, so X and Ls are free again
+  for (int c0 = blockIdx.x * kTrCols; c0 < g.ncols; c0 += gridDim.x * kTrCols)
+    panel_trsm_block(g, X, Ls, t, col, rg, c0);
 }
 
 // ---- block back substitution helpers ----------------------------------------
@@ -805,13 +913,51 @@ int laswp_trsm(double* A, int64_t lda, int64_t c0, int64_t lbeg, int64_t lend, i
 // pair lists `slot` ints apart) on columns [lbeg, lend) and [rbeg, rend) of
 // the n-row system at A (row 0, column 0).
 int laswp_panel(double* A, int64_t lda, int64_t n, int64_t c0, int nleaves, const int* pairs, int64_t slot,
-                int64_t lbeg, int64_t lend, int64_t rbeg, int64_t rend, hipStream_t s) {
+                int64_t lbeg, int64_t lend, int64_t rbeg, int64_t rend, hipStream_t s, int max_wg) {
   lend = std::max(lend, lbeg);
   rend = std::max(rend, rbeg);
   const int64_t cols = (lend - lbeg) + (rend - rbeg);
   if (cols <= 0 || nleaves <= 0) return GELIM_OK;
   PanelSwapArgs a{A, lda, (int)n, (int)c0, nleaves, pairs, (int)slot, (int)lbeg, (int)lend, (int)rbeg, (int)rend};
-  hipLaunchKernelGGL(laswp_panel_kernel, dim3((unsigned)((cols + 63) / 64)), dim3(64), 0, s, a);
+  int64_t grid = (cols + 63) / 64;
+  if (max_wg > 0) grid = std::min<int64_t>(grid, max_wg);  // <= max_wg CUs (lookahead side stream)
+  hipLaunchKernelGGL(laswp_panel_kernel, dim3((unsigned)grid), dim3(64), 0, s, a);
+  HIP_TRY(hipGetLastError());
+  return GELIM_OK;
+}
+
+// Net row movement of nleaves consecutive leaves (diagonals c0, c0 + LW, ...)
+// into net (1 + 2 * 64 * nleaves ints, rows relative to c0).
+int compose_pairs(int64_t n, int64_t c0, int nleaves, const int* pairs, int64_t slot, int* net, hipStream_t s) {
+  const int64_t m = n - c0;
+  if (nleaves <= 0 || m <= 0) return GELIM_OK;
+  if (m > max_rows()) return GELIM_FAIL(GELIM_E_ARG, "compose_pairs: too many rows");
+  const size_t lds = sizeof(int) * (size_t)(m + 1);
+  static const bool attr = [] {
+    return hipFuncSetAttribute((const void*)compose_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)(sizeof(int) * (size_t)(max_rows() + 1))) == hipSuccess;
+  }();
+  if (!attr) return GELIM_FAIL(GELIM_E_HIP, "compose_pairs: LDS attribute refused");
+  ComposeArgs a{(int)m, nleaves, pairs, (int)slot, net};
+  hipLaunchKernelGGL(compose_kernel, dim3(1), dim3(kCmpThreads), lds, s, a);
+  HIP_TRY(hipGetLastError());
+  return GELIM_OK;
+}
+
+int laswp_net_max() { return kNsMax; }
+
+// The composed movement on columns [lbeg, lend) and [rbeg, rend) of the rows
+// from c0 (A: row c0, column 0); at most laswp_net_max() moved rows.
+int laswp_net(double* A, int64_t lda, const int* net, int64_t lbeg, int64_t lend, int64_t rbeg, int64_t rend,
+              hipStream_t s, int max_wg) {
+  lend = std::max(lend, lbeg);
+  rend = std::max(rend, rbeg);
+  const int64_t cols = (lend - lbeg) + (rend - rbeg);
+  if (cols <= 0) return GELIM_OK;
+  NetSwapArgs a{A, lda, net, (int)lbeg, (int)lend, (int)rbeg, (int)rend};
+  int64_t grid = (cols + kNsCols - 1) / kNsCols;
+  if (max_wg > 0) grid = std::min<int64_t>(grid, max_wg);
+  hipLaunchKernelGGL(laswp_net_kernel, dim3((unsigned)grid), dim3(kNsThreads), 0, s, a);
   HIP_TRY(hipGetLastError());
   return GELIM_OK;
 }
@@ -827,7 +973,8 @@ bool trsm_fused() {
   return v;
 }
 
-int panel_trsm(double* C, int64_t ldc, int64_t ncols, int64_t nb, const double* L, int64_t ldl, hipStream_t s) {
+int panel_trsm(double* C, int64_t ldc, int64_t ncols, int64_t nb, const double* L, int64_t ldl, hipStream_t s,
+               int max_wg) {
   if (ncols <= 0) return GELIM_OK;
   if (nb <= 0 || nb > kTrNb || nb % LW) return GELIM_FAIL(GELIM_E_ARG, "panel_trsm: nb must be a multiple of 32 <= 256");
   PanelTrsmArgs a{C, ldc, (int)ncols, (int)nb, L, ldl};
@@ -837,8 +984,9 @@ int panel_trsm(double* C, int64_t ldc, int64_t ncols, int64_t nb, const double* 
                                (int)lds) == hipSuccess;
   }();
   (void)attr;
-  hipLaunchKernelGGL(panel_trsm_kernel, dim3((unsigned)((ncols + kTrCols - 1) / kTrCols)), dim3(kTrThreads), lds, s,
-                     a);
+  int64_t grid = (ncols + kTrCols - 1) / kTrCols;
+  if (max_wg > 0) grid = std::min<int64_t>(grid, max_wg);  // one workgroup per CU (137 KiB of LDS)
+  hipLaunchKernelGGL(panel_trsm_kernel, dim3((unsigned)grid), dim3(kTrThreads), lds, s, a);
   HIP_TRY(hipGetLastError());
   return GELIM_OK;
 }
@@ -898,15 +1046,17 @@ extern "C" int gelim_debug_leaf_stamps(double* dA, int64_t lda, int64_t m, void*
   return rc;
 }
 
+// max_wg > 0: a grid of at most max_wg workgroups (the lookahead side stream's cap)
 extern "C" int gelim_gpu_laswp_panel(double* dA, int64_t lda, int64_t n, int64_t c0, int nleaves,
                                      const int32_t* dpairs, int64_t slot, int64_t lbeg, int64_t lend, int64_t rbeg,
-                                     int64_t rend, void* stream) {
-  return gelim::big::laswp_panel(dA, lda, n, c0, nleaves, dpairs, slot, lbeg, lend, rbeg, rend, (hipStream_t)stream);
+                                     int64_t rend, int max_wg, void* stream) {
+  return gelim::big::laswp_panel(dA, lda, n, c0, nleaves, dpairs, slot, lbeg, lend, rbeg, rend, (hipStream_t)stream,
+                                 max_wg);
 }
 
 extern "C" int gelim_gpu_panel_trsm(double* dC, int64_t ldc, int64_t ncols, int64_t nb, const double* dL, int64_t ldl,
-                                    void* stream) {
-  return gelim::big::panel_trsm(dC, ldc, ncols, nb, dL, ldl, (hipStream_t)stream);
+                                    int max_wg, void* stream) {
+  return gelim::big::panel_trsm(dC, ldc, ncols, nb, dL, ldl, (hipStream_t)stream, max_wg);
 }
 
 extern "C" int64_t gelim_gpu_leaf_workspace_bytes(void) { return (int64_t)gelim::big::workspace_bytes(); }
@@ -915,3 +1065,16 @@ extern "C" int gelim_gpu_laswp_trsm(double* dA, int64_t lda, int64_t c0, int64_t
                                     int64_t trsm_end, int64_t nrows, const int32_t* dpairs, void* stream) {
   return gelim::big::laswp_trsm(dA, lda, c0, 0, lend, rbeg, rend, trsm_end, nrows, dpairs, (hipStream_t)stream, nullptr, 0);
 }
+
+// the composed form of the same movement (compose + gather/scatter); net:
+// 1 + 2 * 64 * nleaves ints of device scratch
+extern "C" int gelim_gpu_laswp_net(double* dA, int64_t lda, int64_t n, int64_t c0, int nleaves, const int32_t* dpairs,
+                                   int64_t slot, int64_t lbeg, int64_t lend, int64_t rbeg, int64_t rend, int32_t* dnet,
+                                   int max_wg, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if ((int64_t)nleaves * 2 * 32 > gelim::big::laswp_net_max())
+    return GELIM_FAIL(GELIM_E_ARG, "laswp_net: more moved rows than one pass holds");
+  GELIM_TRY(gelim::big::compose_pairs(n, c0, nleaves, dpairs, slot, dnet, s));
+  return gelim::big::laswp_net(dA + c0 * lda, lda, dnet, lbeg, lend, rbeg, rend, s, max_wg);
+}
+

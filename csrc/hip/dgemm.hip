@@ -65,8 +65,7 @@ struct Stage {
 };
 
 template <bool FULL>
-__device__ __forceinline__ void load_stage(Stage& st, const Args& g, int m0, int n0, int k0) {
-  const int t = threadIdx.x;
+__device__ __forceinline__ void load_stage(Stage& st, const Args& g, int m0, int n0, int k0, int t) {
 #pragma unroll
   for (int h = 0; h < kCA; ++h) {
     const int idx = t + kThreads * h;
@@ -99,8 +98,7 @@ __device__ __forceinline__ void load_stage(Stage& st, const Args& g, int m0, int
   }
 }
 
-__device__ __forceinline__ void store_stage(const Stage& st, double* As, double* Bs, double alpha) {
-  const int t = threadIdx.x;
+__device__ __forceinline__ void store_stage(const Stage& st, double* As, double* Bs, double alpha, int t) {
 #pragma unroll
   for (int h = 0; h < kCA; ++h) {
     const int idx = t + kThreads * h;
@@ -116,11 +114,14 @@ __device__ __forceinline__ void store_stage(const Stage& st, double* As, double*
   }
 }
 
+// One 128 x 128 tile by the 256 threads t = 0..255 (4 waves) over the LDS
+// double buffer at lds.  store = false: computed, not written (a persistent
+// workgroup's idle half, which still has to meet every barrier).
 template <bool FULL>
-__device__ __forceinline__ void tile_body(const Args& g, int m0, int n0, double* lds) {
+__device__ __forceinline__ void tile_body(const Args& g, int m0, int n0, double* lds, int t, bool store = true) {
   double* As[2] = {lds, lds + BK * SA};
   double* Bs[2] = {lds + 2 * BK * SA, lds + 2 * BK * SA + BK * SB};
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = t & 63, wave = t >> 6;
   const int wm = (wave >> 1) * WM, wn = (wave & 1) * WN;
   const int r16 = lane & 15, q = lane >> 4;
 
@@ -139,13 +140,13 @@ __device__ __forceinline__ void tile_body(const Args& g, int m0, int n0, double*
     }
 
   Stage st;
-  load_stage<FULL>(st, g, m0, n0, 0);
-  store_stage(st, As[0], Bs[0], g.alpha);
+  load_stage<FULL>(st, g, m0, n0, 0, t);
+  store_stage(st, As[0], Bs[0], g.alpha, t);
   __syncthreads();
   const int nk = (g.K + BK - 1) / BK;
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
-    if (kt + 1 < nk) load_stage<FULL>(st, g, m0, n0, (kt + 1) * BK);
+    if (kt + 1 < nk) load_stage<FULL>(st, g, m0, n0, (kt + 1) * BK, t);
     const double* a_s = As[cur] + wm + r16;
     const double* b_s = Bs[cur] + wn + r16;
 #pragma unroll
@@ -162,7 +163,7 @@ __device__ __forceinline__ void tile_body(const Args& g, int m0, int n0, double*
         for (int j = 0; j < NB; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[i], bf[j], acc[i][j], 0, 0, 0);
     }
-    if (kt + 1 < nk) store_stage(st, As[cur ^ 1], Bs[cur ^ 1], g.alpha);
+    if (kt + 1 < nk) store_stage(st, As[cur ^ 1], Bs[cur ^ 1], g.alpha, t);
     __syncthreads();
   }
 
@@ -174,7 +175,7 @@ __device__ __forceinline__ void tile_body(const Args& g, int m0, int n0, double*
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int row = m0 + wm + 16 * i + q + 4 * r;
-        if (FULL || (row < g.M && col < g.N)) g.C[(int64_t)row * g.ldc + col] = acc[i][j][r];
+        if (store && (FULL || (row < g.M && col < g.N))) g.C[(int64_t)row * g.ldc + col] = acc[i][j][r];
       }
     }
 }
@@ -188,17 +189,53 @@ __global__ __launch_bounds__(kThreads, 2) void dgemm_kernel(Args g) {
   const int tile = (xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q) + orig / 8;
   const int m0 = (tile / g.tiles_n) * BM, n0 = (tile % g.tiles_n) * BN;
   if (m0 + BM <= g.M && n0 + BN <= g.N && (g.K % BK) == 0)
-    tile_body<true>(g, m0, n0, lds);
+    tile_body<true>(g, m0, n0, lds, threadIdx.x);
   else
-    tile_body<false>(g, m0, n0, lds);
+    tile_body<false>(g, m0, n0, lds, threadIdx.x);
+}
+
+// Persistent form for a grid capped below the CU count (the lookahead side
+// stream of plan.hip enqueue_big, which must leave CUs free for the leaf
+// chain): 512 threads = two tile engines (2 waves per SIMD, as two of the
+// workgroups above), 2 x 72 KiB of LDS, so one workgroup per CU and a grid
+// of G workgroups occupies at most G CUs.  Tile pairs are dealt to XCDs in
+// contiguous runs (G a multiple of 8); an odd last tile leaves one half
+// computing a clamped tile it does not store.
+constexpr int kPThreads = 2 * kThreads;
+constexpr size_t kStageBytes = sizeof(double) * (2 * BK * SA + 2 * BK * SB);
+
+__global__ __launch_bounds__(kPThreads, 1) void dgemm_persist_kernel(Args g) {
+  extern __shared__ __attribute__((aligned(16))) double plds[];
+  const int half = __builtin_amdgcn_readfirstlane(threadIdx.x / kThreads), t = threadIdx.x % kThreads;
+  double* lds = plds + half * (kStageBytes / sizeof(double));
+  const int npairs = (g.ntiles + 1) / 2;
+  const int xcd = blockIdx.x % 8, local = blockIdx.x / 8, per = gridDim.x / 8;
+  const int q = npairs / 8, rem = npairs % 8;
+  const int beg = xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q;
+  const int end = beg + q + (xcd < rem ? 1 : 0);
+  for (int pr = beg + local; pr < end; pr += per) {
+    const int tile0 = 2 * pr + half;
+    const bool store = tile0 < g.ntiles;
+    const int tile = store ? tile0 : g.ntiles - 1;
+    const int m0 = (tile / g.tiles_n) * BM, n0 = (tile % g.tiles_n) * BN;
+    // an opaque copy of t per pair: nothing thread-dependent is hoisted out
+    // of the loop (hoisted address terms pushed the body past 256 VGPRs)
+    int tt = t;
+    asm volatile("" : "+v"(tt));
+    if (m0 + BM <= g.M && n0 + BN <= g.N && (g.K % BK) == 0)
+      tile_body<true>(g, m0, n0, lds, tt, store);
+    else
+      tile_body<false>(g, m0, n0, lds, tt, store);
+    __syncthreads();  // the next pair's first stage overwrites this one's LDS
+  }
 }
 
 }  // namespace
 
 // C (M x N, ldc) += alpha * A (M x K, lda) * B (K x N, ldb); alpha in {+1, -1}
 // in practice (any value works: A is scaled once on its way into LDS).
-int dgemm(double* C, int64_t ldc, const double* A, int64_t lda, const double* B, int64_t ldb, int64_t M,
-          int64_t N, int64_t K, double alpha, hipStream_t s) {
+int dgemm_capped(double* C, int64_t ldc, const double* A, int64_t lda, const double* B, int64_t ldb, int64_t M,
+                 int64_t N, int64_t K, double alpha, int max_wg, hipStream_t s) {
   if (M <= 0 || N <= 0 || K <= 0) return GELIM_OK;
   if (M > INT32_MAX || N > INT32_MAX || K > INT32_MAX) return GELIM_FAIL(GELIM_E_ARG, "dgemm: dimension > 2^31");
   // 16-byte operand chunks: 16-byte aligned A and B, even leading dimensions
@@ -209,9 +246,29 @@ int dgemm(double* C, int64_t ldc, const double* A, int64_t lda, const double* B,
                                        " lda=" + std::to_string(lda) + " ldb=" + std::to_string(ldb) + ")");
   const int tm = (int)((M + BM - 1) / BM), tn = (int)((N + BN - 1) / BN);
   Args g{C, ldc, A, lda, B, ldb, (int)M, (int)N, (int)K, tn, tm * tn, alpha};
-  hipLaunchKernelGGL(dgemm_kernel, dim3((unsigned)(tm * tn)), dim3(kThreads), 0, s, g);
+  // max_wg > 0: at most max_wg CUs (rounded down to a multiple of 8)
+  const int cap = max_wg > 0 ? std::max(8, max_wg / 8 * 8) : 0;
+  // few tiles: one 256-thread workgroup per tile already stays within the
+  // cap (<= tiles CUs) and halves the per-workgroup work
+  if (cap > 0 && tm * tn > cap) {
+    static const bool attr = [] {
+      return hipFuncSetAttribute((const void*)dgemm_persist_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                 (int)(2 * kStageBytes)) == hipSuccess;
+    }();
+    if (!attr) return GELIM_FAIL(GELIM_E_HIP, "dgemm: 144 KiB of LDS per workgroup refused");
+    const int grid = std::min(cap, (tm * tn + 1) / 2 + 7) / 8 * 8;  // whole XCD rounds
+    hipLaunchKernelGGL(dgemm_persist_kernel, dim3((unsigned)std::max(grid, 8)), dim3(kPThreads), 2 * kStageBytes, s,
+                       g);
+  } else {
+    hipLaunchKernelGGL(dgemm_kernel, dim3((unsigned)(tm * tn)), dim3(kThreads), 0, s, g);
+  }
   HIP_TRY(hipGetLastError());
   return GELIM_OK;
+}
+
+int dgemm(double* C, int64_t ldc, const double* A, int64_t lda, const double* B, int64_t ldb, int64_t M,
+          int64_t N, int64_t K, double alpha, hipStream_t s) {
+  return dgemm_capped(C, ldc, A, lda, B, ldb, M, N, K, alpha, 0, s);
 }
 
 }  // namespace gelim
@@ -219,4 +276,11 @@ int dgemm(double* C, int64_t ldc, const double* A, int64_t lda, const double* B,
 extern "C" int gelim_gpu_dgemm(double* dC, int64_t ldc, const double* dA, int64_t lda, const double* dB,
                                int64_t ldb, int64_t M, int64_t N, int64_t K, double alpha, void* stream) {
   return gelim::dgemm(dC, ldc, dA, lda, dB, ldb, M, N, K, alpha, (hipStream_t)stream);
+}
+
+// the persistent form on at most max_wg CUs (tests / benchmarks)
+extern "C" int gelim_gpu_dgemm_capped(double* dC, int64_t ldc, const double* dA, int64_t lda, const double* dB,
+                                      int64_t ldb, int64_t M, int64_t N, int64_t K, double alpha, int max_wg,
+                                      void* stream) {
+  return gelim::dgemm_capped(dC, ldc, dA, lda, dB, ldb, M, N, K, alpha, max_wg, (hipStream_t)stream);
 }

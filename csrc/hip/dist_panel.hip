@@ -36,8 +36,9 @@ int leaf_factor(double* A, int64_t lda, int64_t m, int64_t c0, int mode, int* ip
 int laswp_trsm(double* A, int64_t lda, int64_t c0, int64_t lbeg, int64_t lend, int64_t rbeg, int64_t rend,
                int64_t trsm_end, int64_t nrows, const int* pairs, hipStream_t s, const double* L, int64_t ldl);
 int laswp_panel(double* A, int64_t lda, int64_t n, int64_t c0, int nleaves, const int* pairs, int64_t slot,
-                int64_t lbeg, int64_t lend, int64_t rbeg, int64_t rend, hipStream_t s);
-int panel_trsm(double* C, int64_t ldc, int64_t ncols, int64_t nb, const double* L, int64_t ldl, hipStream_t s);
+                int64_t lbeg, int64_t lend, int64_t rbeg, int64_t rend, hipStream_t s, int max_wg = 0);
+int panel_trsm(double* C, int64_t ldc, int64_t ncols, int64_t nb, const double* L, int64_t ldl, hipStream_t s,
+               int max_wg = 0);
 bool trsm_fused();
 }  // namespace big
 }  // namespace gelim

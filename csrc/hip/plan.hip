@@ -38,6 +38,8 @@ int backsub_f32(const float* U, int64_t ldu, const float* y, int64_t incy, doubl
                 const int* perm = nullptr, int* err = nullptr);
 int dgemm(double* C, int64_t ldc, const double* A, int64_t lda, const double* B, int64_t ldb, int64_t M,
           int64_t N, int64_t K, double alpha, hipStream_t s);
+int dgemm_capped(double* C, int64_t ldc, const double* A, int64_t lda, const double* B, int64_t ldb, int64_t M,
+                 int64_t N, int64_t K, double alpha, int max_wg, hipStream_t s);
 namespace big {
 size_t workspace_bytes();
 int leaf_width();
@@ -48,8 +50,13 @@ int laswp_trsm(double* A, int64_t lda, int64_t c0, int64_t lbeg, int64_t lend, i
                int64_t trsm_end, int64_t nrows, const int* pairs, hipStream_t s, const double* L = nullptr,
                int64_t ldl = 0);
 int laswp_panel(double* A, int64_t lda, int64_t n, int64_t c0, int nleaves, const int* pairs, int64_t slot,
-                int64_t lbeg, int64_t lend, int64_t rbeg, int64_t rend, hipStream_t s);
-int panel_trsm(double* C, int64_t ldc, int64_t ncols, int64_t nb, const double* L, int64_t ldl, hipStream_t s);
+                int64_t lbeg, int64_t lend, int64_t rbeg, int64_t rend, hipStream_t s, int max_wg = 0);
+int panel_trsm(double* C, int64_t ldc, int64_t ncols, int64_t nb, const double* L, int64_t ldl, hipStream_t s,
+               int max_wg = 0);
+int compose_pairs(int64_t n, int64_t c0, int nleaves, const int* pairs, int64_t slot, int* net, hipStream_t s);
+int laswp_net_max();
+int laswp_net(double* A, int64_t lda, const int* net, int64_t lbeg, int64_t lend, int64_t rbeg, int64_t rend,
+              hipStream_t s, int max_wg);
 bool trsm_fused();
 int tail_gemv(const double* A, int64_t lda, int64_t n, int64_t K, const double* x, double* y, double* bnorm,
               hipStream_t s);
@@ -105,10 +112,14 @@ struct gelim_gauss_plan {
   void* big_ws = nullptr;                // leaf exchange granules + rows
   int* big_pairs = nullptr;              // per-leaf row movement
   double* big_y = nullptr;               // top right-hand side after the tail
-  // lookahead (GELIM_BIG_LOOKAHEAD=1; default serial, graph-captured): the
-  // trailing updates run on big_side, eagerly launched, optionally masked
-  // off the last GELIM_BIG_RESERVE CUs (default 0: unmasked)
+  // lookahead (default from n = 6144, GELIM_BIG_LOOKAHEAD=0/1 forces it;
+  // otherwise serial, graph-captured): the
+  // trailing updates run on big_side, eagerly launched, every side kernel on
+  // a grid of at most big_cap workgroups of one per CU (the CU count less
+  // GELIM_BIG_RESERVE, default 64), so the leaf chain always finds free CUs
   bool big_la = false;
+  int big_cap = 0;
+  int* big_net = nullptr;                // an outer panel's composed row movement (side stream)
   hipStream_t big_side = nullptr;
   std::vector<hipEvent_t> big_ev;        // fork, fact[T], next[T], join
   hipGraphExec_t exec = nullptr;
@@ -196,12 +207,12 @@ int enqueue(gelim_gauss_plan* p, const void* src, int64_t src_ld, void* dx, void
 // substitution with the panel's unit-lower L11, one leaf-row block at a
 // time), then their trailing update A[kend:, cb:ce) -= L21 U12 (K = kend - k).
 int panel_u12_update(gelim_gauss_plan* p, double* A, int64_t k, int64_t kend, int64_t cb, int64_t ce,
-                     hipStream_t s) {
+                     hipStream_t s, int cap = 0) {
   using namespace gelim;
   const int64_t n = p->n, lda = p->lda, LW = big::leaf_width();
   if (ce <= cb) return GELIM_OK;
   if (big::trsm_fused()) {
-    GELIM_TRY(big::panel_trsm(A + k * lda + cb, lda, ce - cb, kend - k, A + k * lda + k, lda, s));
+    GELIM_TRY(big::panel_trsm(A + k * lda + cb, lda, ce - cb, kend - k, A + k * lda + k, lda, s, cap));
   } else {
     for (int64_t r = k; r < kend; r += LW) {
       GELIM_TRY(big::laswp_trsm(A + r * lda, lda, r, 0, 0, cb, ce, ce, n - r, nullptr, s));
@@ -210,8 +221,8 @@ int panel_u12_update(gelim_gauss_plan* p, double* A, int64_t k, int64_t kend, in
                         kend - r - LW, ce - cb, LW, -1.0, s));
     }
   }
-  return dgemm(A + kend * lda + cb, lda, A + kend * lda + k, lda, A + k * lda + cb, lda, n - kend, ce - cb,
-               kend - k, -1.0, s);
+  return dgemm_capped(A + kend * lda + cb, lda, A + kend * lda + k, lda, A + k * lda + cb, lda, n - kend, ce - cb,
+                      kend - k, -1.0, cap, s);
 }
 
 // Wide-panel LU of columns [0, big_k) of the working system, then the tail
@@ -224,11 +235,11 @@ int panel_u12_update(gelim_gauss_plan* p, double* A, int64_t k, int64_t kend, in
 // on the other columns + the TRSM of its U rows, and a rank-32 GEMM of the
 // columns right of it inside the panel.
 //
-// Serial schedule (GELIM_BIG_LOOKAHEAD=0): after P_j, U12 and one K = 256
+// Serial schedule (n < 6144, or GELIM_BIG_LOOKAHEAD=0): after P_j, U12 and one K = 256
 // GEMM update every column right of it -- the leaf chain and the big GEMMs
 // alternate on one stream.
 //
-// Lookahead schedule (default), the leaf chain on the caller's stream
+// Lookahead schedule (n >= 6144, or GELIM_BIG_LOOKAHEAD=1), the leaf chain on the caller's stream
 // ("crit"), the big GEMMs beside it on big_side:
 //   crit, P_j:  every leaf also updates the NEXT panel's columns P_j+1
 //               (swap, TRSM, rank-32 GEMM -- right-looking at nb = 32), so
@@ -288,17 +299,25 @@ int enqueue_big(gelim_gauss_plan* p, double* A, double* x, double* bnorm, hipStr
     const int* pr0 = p->big_pairs + first_leaf * kBigPairSlot;
     HIP_TRY(hipEventRecord(ev_fact[j], s));
     HIP_TRY(hipStreamWaitEvent(side, ev_fact[j], 0));
+    // the panel's row movement composed into one permutation (<= 64 rows per
+    // leaf), applied by gather/scatter tiles; laswp_panel replays the lists
+    const bool net = p->big_net != nullptr && nl * 2 * LW <= big::laswp_net_max();
+    if (net) GELIM_TRY(big::compose_pairs(n, k, nl, pr0, kBigPairSlot, p->big_net, side));
+    auto swaps = [&](int64_t lb, int64_t le, int64_t rb, int64_t re) {
+      return net ? big::laswp_net(A + k * lda, lda, p->big_net, lb, le, rb, re, side, p->big_cap)
+                 : big::laswp_panel(A, lda, n, k, nl, pr0, kBigPairSlot, lb, le, rb, re, side, p->big_cap);
+    };
     // side, first part: P_j+2 = [kb(j+2), kb(j+3))
     const int64_t nb0 = kb(j + 2), nb1 = kb(j + 3);
     if (nb1 > nb0) {
-      GELIM_TRY(big::laswp_panel(A, lda, n, k, nl, pr0, kBigPairSlot, 0, 0, nb0, nb1, side));
-      GELIM_TRY(panel_u12_update(p, A, k, kend, nb0, nb1, side));
+      GELIM_TRY(swaps(0, 0, nb0, nb1));
+      GELIM_TRY(panel_u12_update(p, A, k, kend, nb0, nb1, side, p->big_cap));
     }
     HIP_TRY(hipEventRecord(ev_next[j], side));
     // side, the rest: the L part left of P_j, every column from P_j+3 on
     const int64_t rb = std::max(nb1, cend);
-    GELIM_TRY(big::laswp_panel(A, lda, n, k, nl, pr0, kBigPairSlot, 0, k, rb, n + 1, side));
-    GELIM_TRY(panel_u12_update(p, A, k, kend, rb, n + 1, side));
+    GELIM_TRY(swaps(0, k, rb, n + 1));
+    GELIM_TRY(panel_u12_update(p, A, k, kend, rb, n + 1, side, p->big_cap));
   }
   if (la) {
     HIP_TRY(hipEventRecord(*ev_join, side));
@@ -494,29 +513,28 @@ extern "C" gelim_gauss_plan* gelim_gauss_plan_create(int64_t n, int algo, int pi
     const int64_t nleaves = big_k / lw;
     if (hipMalloc((void**)&p->big_pairs, sizeof(int) * kBigPairSlot * nleaves) != hipSuccess) return fail("pairs");
     if (hipStreamCreateWithFlags(&p->cap, hipStreamNonBlocking) != hipSuccess) return fail("stream");
-    // lookahead (opt-in): trailing updates on a second stream, launched
-    // eagerly (a replayed graph would not keep a stream's CU mask).
-    // Measured at n = 8192 (profiles/big_lookahead_8192.txt): serial 42.0 ms;
-    // lookahead unmasked 42.3 ms -- the leaves run 22 % slower beside the
-    // GEMMs and the crit stream waits for the side's next-panel update every
-    // panel; masked off 32 / 64 CUs 147 / 66 ms -- the masked queue's
-    // kernels never ran beside the leaves (0 us of GEMM under a leaf)
+    // lookahead: trailing updates on a second stream, launched eagerly.  Every side kernel runs on a capped grid of one workgroup per
+    // CU (dgemm_capped, panel_trsm, laswp_panel with max_wg), so at most
+    // big_cap CUs ever hold side work and the leaf chain -- whose waves need
+    // a whole SIMD's registers and all of a leaf's workgroups resident --
+    // always finds free CUs.  Earlier attempts (profiles/big_lookahead_8192.txt):
+    // uncapped grids 42.3 ms (leaves dispatched only as GEMM workgroups
+    // drained), a CU-masked side queue 147 ms (it never ran beside the leaves).
+    // default: lookahead from n = 6144 (8192: 36.3 vs 39.8 ms serial; 4096
+    // even, where the graph-replayed serial schedule saves the launches)
     const char* el = std::getenv("GELIM_BIG_LOOKAHEAD");
-    p->big_la = el && std::atoi(el) != 0;
+    p->big_la = el ? std::atoi(el) != 0 : n >= 6144;
     if (p->big_la) {
       int dev = 0, ncu = 0;
       (void)hipGetDevice(&dev);
       (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-      int reserve = 0;
+      int reserve = 64;  // 8192: 35.4 ms (32: 36.3, 96: 35.5)
       if (const char* er = std::getenv("GELIM_BIG_RESERVE")) reserve = std::max(0, std::atoi(er));
-      if (ncu > 0 && reserve > 0 && reserve < ncu) {
-        std::vector<uint32_t> mask((size_t)(ncu + 31) / 32, 0u);
-        for (int c = 0; c < ncu - reserve; ++c) mask[(size_t)c / 32] |= 1u << (c % 32);
-        if (hipExtStreamCreateWithCUMask(&p->big_side, (uint32_t)mask.size(), mask.data()) != hipSuccess)
-          return fail("CU-masked stream");
-      } else if (hipStreamCreateWithFlags(&p->big_side, hipStreamNonBlocking) != hipSuccess) {
-        return fail("side stream");
-      }
+      p->big_cap = ncu > reserve + 8 ? ncu - reserve : std::max(8, ncu / 2);
+      if (hipStreamCreateWithFlags(&p->big_side, hipStreamNonBlocking) != hipSuccess) return fail("side stream");
+      if (std::getenv("GELIM_BIG_NET") == nullptr || std::atoi(std::getenv("GELIM_BIG_NET")) != 0)
+        if (hipMalloc((void**)&p->big_net, sizeof(int) * (1 + 2 * (size_t)gelim::big::laswp_net_max())) != hipSuccess)
+          return fail("net movement");
       const int64_t T = (big_k + big_nb() - 1) / big_nb();
       p->big_ev.assign((size_t)(2 * T + 2), nullptr);
       for (auto& e : p->big_ev)
@@ -631,6 +649,7 @@ extern "C" void gelim_gauss_plan_destroy(gelim_gauss_plan* p) {
   (void)hipFree(p->tmp);
   (void)hipFree(p->big_ws);
   (void)hipFree(p->big_pairs);
+  (void)hipFree(p->big_net);
   (void)hipFree(p->big_y);
   gelim_gauss_plan_destroy(p->tail);
   delete p;

@@ -165,6 +165,10 @@ int gelim_gpu_swap_trsm(double* dC, int64_t ldc, int64_t ncols,
  * lda / ldb / K even, ldb > N when N is odd. */
 int gelim_gpu_dgemm(double* dC, int64_t ldc, const double* dA, int64_t lda, const double* dB,
                     int64_t ldb, int64_t M, int64_t N, int64_t K, double alpha, void* stream);
+/* the same as a persistent kernel on at most max_wg CUs (one 512-thread
+ * workgroup per CU, two tiles each) -- the lookahead side stream's form */
+int gelim_gpu_dgemm_capped(double* dC, int64_t ldc, const double* dA, int64_t lda, const double* dB,
+                           int64_t ldb, int64_t M, int64_t N, int64_t K, double alpha, int max_wg, void* stream);
 /* Wide-panel LU pieces (biglu.hip), exposed for tests: factor the m x 32
  * leaf at dA (its diagonal is row/column c0 of the system: dipiv[c0 + j]
  * gets the absolute LAPACK pivot row of column c0 + j, dpairs the net row
@@ -176,15 +180,22 @@ int gelim_gpu_leaf_factor(double* dA, int64_t lda, int64_t m, int64_t c0, int pi
                           int32_t* dpairs, int32_t* dinfo, void* stream);
 int gelim_gpu_laswp_trsm(double* dA, int64_t lda, int64_t c0, int64_t lend, int64_t rbeg, int64_t rend,
                          int64_t trsm_end, int64_t nrows, const int32_t* dpairs, void* stream);
+/* U12 = L11^-1 C: nb (<= 256, multiple of 32) rows of C over ncols columns,
+ * L11 the unit-lower nb x nb block at dL; max_wg > 0 caps the grid */
+int gelim_gpu_panel_trsm(double* dC, int64_t ldc, int64_t ncols, int64_t nb, const double* dL, int64_t ldl,
+                         int max_wg, void* stream);
 /* a whole outer panel's interchanges (nleaves leaf pair lists, `slot` ints
  * apart, diagonals c0, c0 + 32, ...) on columns [lbeg, lend) and
- * [rbeg, rend) of the n-row system at dA (row 0, column 0) */
-/* U12 = L11^-1 C: nb (<= 256, multiple of 32) rows of C over ncols columns,
- * L11 the unit-lower nb x nb block at dL */
-int gelim_gpu_panel_trsm(double* dC, int64_t ldc, int64_t ncols, int64_t nb, const double* dL, int64_t ldl,
-                         void* stream);
+ * [rbeg, rend) of the n-row system at dA (row 0, column 0); max_wg > 0
+ * caps the grid */
 int gelim_gpu_laswp_panel(double* dA, int64_t lda, int64_t n, int64_t c0, int nleaves, const int32_t* dpairs,
-                          int64_t slot, int64_t lbeg, int64_t lend, int64_t rbeg, int64_t rend, void* stream);
+                          int64_t slot, int64_t lbeg, int64_t lend, int64_t rbeg, int64_t rend, int max_wg,
+                          void* stream);
+/* the same movement composed into one permutation first (<= 512 moved rows,
+ * dnet: 1 + 128 * nleaves ints of device scratch), then gathered/scattered */
+int gelim_gpu_laswp_net(double* dA, int64_t lda, int64_t n, int64_t c0, int nleaves, const int32_t* dpairs,
+                        int64_t slot, int64_t lbeg, int64_t lend, int64_t rbeg, int64_t rend, int32_t* dnet,
+                        int max_wg, void* stream);
 int gelim_gpu_gemm_update(double* dC, int64_t ldc, const double* dL,
                           int64_t ldl, const double* dU, int64_t ldu,
                           int64_t M, int64_t N, int64_t K, void* stream);

@@ -68,6 +68,7 @@ _PROTOS = {
     "gelim_gpu_swap_trsm": (_int, [_vp, _i64, _i64, _vp, _i64, _i64, _vp, _i64, _vp]),
     "gelim_gpu_gemm_update": (_int, [_vp, _i64, _vp, _i64, _vp, _i64, _i64, _i64, _i64, _vp]),
     "gelim_gpu_dgemm": (_int, [_vp, _i64, _vp, _i64, _vp, _i64, _i64, _i64, _i64, _dbl, _vp]),
+    "gelim_gpu_dgemm_capped": (_int, [_vp, _i64, _vp, _i64, _vp, _i64, _i64, _i64, _i64, _dbl, _int, _vp]),
     "gelim_gpu_leaf_factor": (_int, [_vp, _i64, _i64, _i64, _int, _vp, _vp, _vp, _vp]),
     "gelim_gpu_leaf_factor_ws": (_int, [_vp, _i64, _i64, _i64, _int, _vp, _vp, _vp, _vp, _int, _vp]),
     "gelim_gpu_leaf_workspace_bytes": (_i64, []),
@@ -76,8 +77,9 @@ _PROTOS = {
     "gelim_dist_pair_slot": (_i64, []),
     "gelim_dist_panel_factor": (_int, [_vp, _i64, _i64, _i64, _i64, _i64, _int, _vp, _vp, _vp, _vp, _int, _vp]),
     "gelim_dist_panel_apply": (_int, [_vp, _i64, _i64, _i64, _i64, _i64, _vp, _i64, _i64, _vp, _vp]),
-    "gelim_gpu_panel_trsm": (_int, [_vp, _i64, _i64, _i64, _vp, _i64, _vp]),
-    "gelim_gpu_laswp_panel": (_int, [_vp, _i64, _i64, _i64, _int, _vp, _i64, _i64, _i64, _i64, _i64, _vp]),
+    "gelim_gpu_panel_trsm": (_int, [_vp, _i64, _i64, _i64, _vp, _i64, _int, _vp]),
+    "gelim_gpu_laswp_panel": (_int, [_vp, _i64, _i64, _i64, _int, _vp, _i64, _i64, _i64, _i64, _i64, _int, _vp]),
+    "gelim_gpu_laswp_net": (_int, [_vp, _i64, _i64, _i64, _int, _vp, _i64, _i64, _i64, _i64, _i64, _vp, _int, _vp]),
     "gelim_gpu_backsub": (_int, [_vp, _i64, _vp, _i64, _vp, _vp, _i64, _int, _vp]),
     "gelim_gauss_plan_create": (_vp, [_i64, _int, _int, _int, _int]),
     "gelim_gauss_plan_resolve": (_int, [_vp, _vp, _vp, _vp]),

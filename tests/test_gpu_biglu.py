@@ -8,21 +8,27 @@ from conftest import GOLDEN_ERROR
 pytestmark = pytest.mark.gpu
 
 
-def _dgemm(gelim, C, A, B, alpha):
+def _dgemm(gelim, C, A, B, alpha, cap=None):
     from gelim import _native
     from gelim.utils.tensors import ptr, row_major_ld, stream_handle
 
     M, N = C.shape
     K = A.shape[1]
-    rc = _native.lib().gelim_gpu_dgemm(ptr(C), row_major_ld(C), ptr(A), row_major_ld(A), ptr(B), row_major_ld(B),
-                                       M, N, K, alpha, stream_handle(C.device))
+    args = (ptr(C), row_major_ld(C), ptr(A), row_major_ld(A), ptr(B), row_major_ld(B), M, N, K, alpha)
+    if cap is None:
+        rc = _native.lib().gelim_gpu_dgemm(*args, stream_handle(C.device))
+    else:
+        rc = _native.lib().gelim_gpu_dgemm_capped(*args, cap, stream_handle(C.device))
     _native.check(rc, "dgemm")
 
 
 @pytest.mark.parametrize("M,N,K", [(128, 128, 16), (256, 384, 256), (300, 517, 32), (129, 1, 2),
                                    (1000, 2049, 64), (64, 64, 30)])
 @pytest.mark.parametrize("alpha", [-1.0, 1.0])
-def test_dgemm_matches_torch(gelim, cuda, M, N, K, alpha):
+@pytest.mark.parametrize("cap", [None, 8, 224])
+def test_dgemm_matches_torch(gelim, cuda, M, N, K, alpha, cap):
+    """Plain launch, and the persistent capped form (512-thread workgroups,
+    two tiles each, odd tile counts leaving an idle half) on 8 / 224 CUs."""
     torch.manual_seed(M * 7 + N + K)
     ldn = N + 1 + (N + 1) % 2  # even, > N (the dgemm contract)
     Cf = torch.randn(M, ldn, dtype=torch.float64, device=cuda)
@@ -31,7 +37,7 @@ def test_dgemm_matches_torch(gelim, cuda, M, N, K, alpha):
     C, A, B = Cf[:, :N], Af[:, :K], Bf[:, :N]
     ref = C + alpha * (A @ B)
     C0 = Cf.clone()
-    _dgemm(gelim, C, A, B, alpha)
+    _dgemm(gelim, C, A, B, alpha, cap)
     torch.cuda.synchronize()
     assert torch.allclose(C, ref, rtol=1e-12, atol=1e-11 * K)
     assert torch.equal(Cf[:, N:], C0[:, N:])  # padding untouched
@@ -220,11 +226,11 @@ def test_memplus_blocked(gelim, cuda):
     assert err <= max(20 * err_ref, 1e-12), (err, err_ref)
 
 
-@pytest.mark.parametrize("la,reserve", [("0", "32"), ("1", "32"), ("1", "0"), ("1", "200")])
+@pytest.mark.parametrize("la,reserve", [("0", "32"), ("1", "32"), ("1", "0"), ("1", "200"), ("1", "255")])
 @pytest.mark.parametrize("n", [700, 1500, 2600])
 def test_big_schedules_agree(gelim, cuda, monkeypatch, la, reserve, n):
-    """Serial (graph-captured) and lookahead (crit + CU-masked side stream)
-    schedules of the wide-panel engine, several outer panels each
+    """Serial (graph-captured) and lookahead (crit + side stream on capped
+    grids: 256 - reserve workgroups, 8 at least) schedules of the wide-panel engine, several outer panels each
     (GELIM_BIG_TAIL=256): same pivots, so the same solution to rounding."""
     monkeypatch.setenv("GELIM_BIG_TAIL", "256")
     monkeypatch.setenv("GELIM_BIG_LOOKAHEAD", la)
@@ -270,16 +276,27 @@ def test_laswp_panel_matches_sequential(gelim, cuda):
         old = ref.clone()
         for d, s in pl:
             ref[base + d, cols] = old[base + s, cols]
-    Ag = A.to(cuda)
-    rc = _native.lib().gelim_gpu_laswp_panel(ptr(Ag), A.shape[1], n, c0, nl, ptr(pairs.to(cuda)), slot, lb, le, rb,
-                                             re, stream_handle(cuda))
-    _native.check(rc, "laswp_panel")
-    torch.cuda.synchronize()
-    assert torch.equal(Ag.cpu(), ref)
+    net = torch.zeros(1 + 2 * 64 * nl, dtype=torch.int32, device=cuda)
+    for cap in (0, 2):  # one workgroup per 64 columns / a 2-workgroup grid-stride loop
+        Ag = A.to(cuda)
+        rc = _native.lib().gelim_gpu_laswp_panel(ptr(Ag), A.shape[1], n, c0, nl, ptr(pairs.to(cuda)), slot, lb, le,
+                                                 rb, re, cap, stream_handle(cuda))
+        _native.check(rc, "laswp_panel")
+        torch.cuda.synchronize()
+        assert torch.equal(Ag.cpu(), ref)
+        # the composed permutation (compose + gather/scatter) moves the same rows
+        Ag = A.to(cuda)
+        rc = _native.lib().gelim_gpu_laswp_net(ptr(Ag), A.shape[1], n, c0, nl, ptr(pairs.to(cuda)), slot, lb, le, rb,
+                                               re, ptr(net), cap, stream_handle(cuda))
+        _native.check(rc, "laswp_net")
+        torch.cuda.synchronize()
+        assert torch.equal(Ag.cpu(), ref)
+        assert 0 < int(net[0]) <= 64 * nl
 
 
 @pytest.mark.parametrize("nb,ncols", [(256, 1000), (32, 70), (160, 33), (256, 8193)])
-def test_panel_trsm_matches_torch(gelim, cuda, nb, ncols):
+@pytest.mark.parametrize("cap", [0, 3])
+def test_panel_trsm_matches_torch(gelim, cuda, nb, ncols, cap):
     """The one-launch U12 = L11^-1 A12 of an outer panel (nb rows, unit lower
     L11) against torch's triangular solve."""
     from gelim import _native
@@ -292,7 +309,7 @@ def test_panel_trsm_matches_torch(gelim, cuda, nb, ncols):
     L11 = torch.tril(L[:, :nb], -1) + torch.eye(nb, dtype=torch.float64)
     ref = torch.linalg.solve_triangular(L11, C[:, :ncols], upper=False, unitriangular=True)
     Cg, Lg = C.to(cuda), L.to(cuda)
-    rc = _native.lib().gelim_gpu_panel_trsm(ptr(Cg), ld, ncols, nb, ptr(Lg), nb + 4, stream_handle(cuda))
+    rc = _native.lib().gelim_gpu_panel_trsm(ptr(Cg), ld, ncols, nb, ptr(Lg), nb + 4, cap, stream_handle(cuda))
     _native.check(rc, "panel_trsm")
     torch.cuda.synchronize()
     assert torch.allclose(Cg.cpu()[:, :ncols], ref, rtol=1e-11, atol=1e-11)

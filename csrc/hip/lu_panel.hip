@@ -124,19 +124,53 @@ struct Panel {
       uint64_t best = 0;
       unsigned brow = 0xffffffffu;
       double bval = 0.0;
+      if constexpr (MODE == 1) {
+        // PARTIAL: compare magnitudes as fp64 (one v_cmp per row instead of
+        // the 64-bit key arithmetic): max(|a|, 0) ranks NaN like zero, a
+        // retired row gets a negative magnitude (hi word only) and never
+        // beats the -0.5 start; the integer key bits(m)+1 (0: none) is built
+        // once per lane -- the same order as pivot_ukey_t
+        double bm = -0.5;
 #pragma unroll
-      for (int i = 0; i < R; ++i) {
-        const int lr = t + i * NT;
-        // ZERO rule: the "diagonal" is physical row J (a row chosen earlier is
-        // never the diagonal here — documented difference from a physical-swap
-        // run; PARTIAL pivoting, the accuracy-relevant rule, is exact)
-        const uint64_t key = dev::pivot_ukey_t<MODE>(a[i][J], lr == J, live[i]);
-        const bool better = key > best;  // increasing rows: '>' keeps the lowest row on ties
-        best = better ? key : best;
-        brow = better ? (unsigned)lr : brow;
-        bval = better ? a[i][J] : bval;
+        for (int i = 0; i < R; ++i) {
+          // one v_max_f64 with the |.| modifier (fmax() would add a
+          // canonicalising max per row)
+          double mg;
+          asm("v_max_f64 %0, |%1|, 0" : "=v"(mg) : "v"(a[i][J]));
+          const uint64_t mb = (uint64_t)__double_as_longlong(mg);
+          const double m = __longlong_as_double(
+              (long long)((live[i] ? (mb >> 32) : 0xbff00000ull) << 32 | (mb & 0xffffffffull)));
+          const bool better = m > bm;  // increasing rows: '>' keeps the lowest row on ties
+          bm = better ? m : bm;
+          brow = better ? (unsigned)(t + i * NT) : brow;
+          bval = better ? a[i][J] : bval;
+        }
+        best = bm >= 0.0 ? (uint64_t)__double_as_longlong(bm) + 1 : 0;
+      } else {
+#pragma unroll
+        for (int i = 0; i < R; ++i) {
+          const int lr = t + i * NT;
+          // ZERO rule: the "diagonal" is physical row J (a row chosen earlier is
+          // never the diagonal here — documented difference from a physical-swap
+          // run; PARTIAL pivoting, the accuracy-relevant rule, is exact)
+          const uint64_t key = dev::pivot_ukey_t<MODE>(a[i][J], lr == J, live[i]);
+          const bool better = key > best;  // increasing rows: '>' keeps the lowest row on ties
+          best = better ? key : best;
+          brow = better ? (unsigned)lr : brow;
+          bval = better ? a[i][J] : bval;
+        }
       }
-      const double lrd = (bval != 0.0) ? 1.0 / bval : 0.0;
+      // reciprocal of this lane's candidate, computed by every lane BEFORE the
+      // ladder (the value barrier stops LLVM from sinking it into the
+      // winner's publish branch, onto the critical path): v_rcp_f64 + two
+      // Newton steps, within an ulp of the IEEE quotient
+      double lrd = 0.0;
+      {
+        const double r0 = __builtin_amdgcn_rcp(bval);
+        const double r1 = fma(r0, fma(-bval, r0, 1.0), r0);
+        lrd = (bval != 0.0) ? fma(r1, fma(-bval, r1, 1.0), r1) : 0.0;
+        lrd = opaque(lrd);
+      }
       // 2. wave arg-max: DPP max of the high word + one ballot; exact path
       //    only for high-word ties (or all-zero / denormal columns)
       if constexpr (MODE == 1) {
@@ -201,31 +235,53 @@ struct Panel {
         cv[0] = sh.cand_row[par][qq][c0];
       }
     }
+    // fast path: a max ladder over the waves' key HIGH words (one DPP max per
+    // level) + one ballot; the exact (key, lowest row) ladder only when two
+    // waves share the high word (or no wave has a candidate)
+    uint64_t gkey;
+    unsigned p;
+    {
+      const unsigned khi = (unsigned)(k >> 32);
+      unsigned hm = khi;
 #pragma unroll
-    for (int sft = 1; sft < kWaves; sft <<= 1) {
-      unsigned khi = (unsigned)(k >> 32), klo = (unsigned)k, k2hi, k2lo, r2;
-      if (sft == 1) {
-        k2hi = dev::dpp_u32<dev::kDppRowShr1, 0xf, 0xf>(0u, khi);
-        k2lo = dev::dpp_u32<dev::kDppRowShr1, 0xf, 0xf>(0u, klo);
-        r2 = dev::dpp_u32<dev::kDppRowShr1, 0xf, 0xf>(0xffffffffu, r);
-      } else if (sft == 2) {
-        k2hi = dev::dpp_u32<dev::kDppRowShr2, 0xf, 0xf>(0u, khi);
-        k2lo = dev::dpp_u32<dev::kDppRowShr2, 0xf, 0xf>(0u, klo);
-        r2 = dev::dpp_u32<dev::kDppRowShr2, 0xf, 0xf>(0xffffffffu, r);
-      } else {
-        k2hi = dev::dpp_u32<dev::kDppRowShr4, 0xf, 0xf>(0u, khi);
-        k2lo = dev::dpp_u32<dev::kDppRowShr4, 0xf, 0xf>(0u, klo);
-        r2 = dev::dpp_u32<dev::kDppRowShr4, 0xf, 0xf>(0xffffffffu, r);
+      for (int sft = 1; sft < kWaves; sft <<= 1) {
+        if (sft == 1) hm = max(hm, dev::dpp_u32<dev::kDppRowShr1, 0xf, 0xf>(0u, hm));
+        else if (sft == 2) hm = max(hm, dev::dpp_u32<dev::kDppRowShr2, 0xf, 0xf>(0u, hm));
+        else hm = max(hm, dev::dpp_u32<dev::kDppRowShr4, 0xf, 0xf>(0u, hm));
       }
-      const uint64_t k2 = ((uint64_t)k2hi << 32) | k2lo;
-      const bool better = k2 > k || (k2 == k && r2 < r);
-      k = better ? k2 : k;
-      r = better ? r2 : r;
+      const unsigned hmax = (unsigned)__builtin_amdgcn_readlane((int)hm, kWaves - 1);
+      const uint64_t holders = __ballot(khi == hmax) & ((1ull << kWaves) - 1ull);
+      if (hmax != 0 && __popcll(holders) == 1) {
+        const int wl = __ffsll((long long)holders) - 1;
+        gkey = ((uint64_t)hmax << 32) | (unsigned)__builtin_amdgcn_readlane((int)(unsigned)k, wl);
+        p = (unsigned)__builtin_amdgcn_readlane((int)r, wl);
+      } else {
+#pragma unroll
+        for (int sft = 1; sft < kWaves; sft <<= 1) {
+          unsigned khi2 = (unsigned)(k >> 32), klo = (unsigned)k, k2hi, k2lo, r2;
+          if (sft == 1) {
+            k2hi = dev::dpp_u32<dev::kDppRowShr1, 0xf, 0xf>(0u, khi2);
+            k2lo = dev::dpp_u32<dev::kDppRowShr1, 0xf, 0xf>(0u, klo);
+            r2 = dev::dpp_u32<dev::kDppRowShr1, 0xf, 0xf>(0xffffffffu, r);
+          } else if (sft == 2) {
+            k2hi = dev::dpp_u32<dev::kDppRowShr2, 0xf, 0xf>(0u, khi2);
+            k2lo = dev::dpp_u32<dev::kDppRowShr2, 0xf, 0xf>(0u, klo);
+            r2 = dev::dpp_u32<dev::kDppRowShr2, 0xf, 0xf>(0xffffffffu, r);
+          } else {
+            k2hi = dev::dpp_u32<dev::kDppRowShr4, 0xf, 0xf>(0u, khi2);
+            k2lo = dev::dpp_u32<dev::kDppRowShr4, 0xf, 0xf>(0u, klo);
+            r2 = dev::dpp_u32<dev::kDppRowShr4, 0xf, 0xf>(0xffffffffu, r);
+          }
+          const uint64_t k2 = ((uint64_t)k2hi << 32) | k2lo;
+          const bool better = k2 > k || (k2 == k && r2 < r);
+          k = better ? k2 : k;
+          r = better ? r2 : r;
+        }
+        gkey = ((uint64_t)(unsigned)__builtin_amdgcn_readlane((int)(unsigned)(k >> 32), kWaves - 1) << 32) |
+               (unsigned)__builtin_amdgcn_readlane((int)(unsigned)k, kWaves - 1);
+        p = (unsigned)__builtin_amdgcn_readlane((int)r, kWaves - 1);
+      }
     }
-    const uint64_t gkey =
-        ((uint64_t)(unsigned)__builtin_amdgcn_readlane((int)(unsigned)(k >> 32), kWaves - 1) << 32) |
-        (unsigned)__builtin_amdgcn_readlane((int)(unsigned)k, kWaves - 1);
-    const unsigned p = (unsigned)__builtin_amdgcn_readlane((int)r, kWaves - 1);
     const int pw = (int)((p & (NT - 1)) >> 6);  // wave that published the pivot row
     auto bcast = [&](int c) -> double {         // u[c] of the pivot row (uniform)
       const int src = pw * LPR + c / DPL;
@@ -236,8 +292,21 @@ struct Panel {
     };
     const double rd = bcast(J);
     double uc[W];
+    // the critical operand (column J+1, whose update feeds the next pivot
+    // search) by v_readlane; the rest of the pivot row as uniform-address
+    // LDS reads (broadcast, 2 doubles per ds_read_b128 instead of 4 VALU
+    // readlanes), consumed after column J+1 is done
+    if constexpr (J + 1 < W) uc[J + 1] = bcast(J + 1);
+    {
+      const double* prow = sh.cand_row[par][pw];
+      constexpr int c0 = (J + 2) & ~1;
 #pragma unroll
-    for (int c = J + 1; c < W; ++c) uc[c] = bcast(c);
+      for (int c = c0; c < W; c += 2) {
+        const double2 v = *reinterpret_cast<const double2*>(prow + c);
+        if (c >= J + 2) uc[c] = v.x;
+        if (c + 1 >= J + 2) uc[c + 1] = v.y;
+      }
+    }
     if (t == 0) {
       sh.sel[J] = (int)p;
       if (gkey <= 1 && info && *info == 0) *info = row0 + J + 1;  // zero pivot

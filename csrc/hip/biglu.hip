@@ -135,10 +135,6 @@ struct Table {
   int trow, tpos, cnt;
 };
 
-__device__ __forceinline__ int table_row_at(const Table& tb, int pos, int lane) {
-  const uint64_t m = __ballot(lane < tb.cnt && tb.tpos == pos);
-  return m ? __builtin_amdgcn_readlane(tb.trow, __ffsll((long long)m) - 1) : pos;
-}
 
 // step J: pivot row pr moves to position J, the row at J moves to pr's spot q
 __device__ __forceinline__ int table_swap(Table& tb, int J, int pr, int lane) {
@@ -195,8 +191,8 @@ template <int MODE, int NKK, int NR>
 struct Leaf {
   // one column J of the leaf (compile time); false: hand-off aborted
   template <int J>
-  static __device__ __forceinline__ bool col(double (&a)[R][LW], bool (&live)[R], double (&lp)[R], LeafLds& sh,
-                                             Table& tb, const LeafArgs& g, int lane, int base) {
+  static __device__ __forceinline__ bool col(double (&a)[R][LW], bool (&live)[R], int (&pos)[R], double (&lp)[R],
+                                             LeafLds& sh, Table& tb, const LeafArgs& g, int lane, int base) {
     constexpr int par = J & 1;
     lane = opq(lane);
     const unsigned seq = (unsigned)(J + 1);
@@ -204,13 +200,15 @@ struct Leaf {
     lstamp(g, J, 0, __builtin_amdgcn_s_memtime());
     // 1. this lane's candidate: best live row (rows grow with the slot, so a
     //    strict '>' keeps the lowest row on ties)
-    const int diag = MODE == 0 ? table_row_at(tb, J, lane) : -1;
+    //    ZERO rule: the diagonal is the row at POSITION J and "the first
+    //    non-zero row below" is the lowest POSITION, so the key is
+    //    class<<32 | ~position (each lane tracks its rows' positions)
     uint64_t bk = 0;
     int bi = 0;
 #pragma unroll
     for (int i = 0; i < R; ++i) {
-      const int r = base + lane + 64 * i;
-      const uint64_t k = dev::pivot_ukey_t<MODE>(a[i][J], r == diag, live[i]);
+      uint64_t k = dev::pivot_ukey_t<MODE>(a[i][J], pos[i] == J, live[i]);
+      if constexpr (MODE == 0) k = k == 0 ? 0 : (k << 32) | (0xffffffffu - (unsigned)pos[i]);
       const bool c = k > bk;
       bk = c ? k : bk;
       bi = c ? i : bi;
@@ -363,6 +361,11 @@ struct Leaf {
     if (mine) sh.prow[par][cc] = pval;
     // interchange replay; participant 0 records the LAPACK pivot
     const int qpos = table_swap(tb, J, (int)pr, lane);
+    if constexpr (MODE == 0) {  // positions J and qpos exchange their rows
+#pragma unroll
+      for (int i = 0; i < R; ++i)
+        pos[i] = (base + lane + 64 * i == (int)pr) ? J : (pos[i] == J ? qpos : pos[i]);
+    }
     if (blockIdx.x == 0 && lane == 0) g.ipiv[g.col0 + J] = g.col0 + qpos;
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the pivot row is in LDS (wave-local)
     lstamp(g, J, 5, __builtin_amdgcn_s_memtime());
@@ -393,13 +396,14 @@ struct Leaf {
   }
 
   template <int... J>
-  static __device__ __forceinline__ bool factor(double (&a)[R][LW], bool (&live)[R], LeafLds& sh, Table& tb,
+  static __device__ __forceinline__ bool factor(double (&a)[R][LW], bool (&live)[R], int (&pos)[R], LeafLds& sh,
+                                                Table& tb,
                                                 const LeafArgs& g, int lane, int base,
                                                 std::integer_sequence<int, J...>) {
     double lp[R];  // multipliers of the pending (previous) pivot
 #pragma unroll
     for (int i = 0; i < R; ++i) lp[i] = 0.0;
-    return (col<J>(a, live, lp, sh, tb, g, lane, base) && ...);
+    return (col<J>(a, live, pos, lp, sh, tb, g, lane, base) && ...);
   }
 };
 
@@ -412,10 +416,12 @@ __global__ __launch_bounds__(64, 1) void leaf_kernel(LeafArgs g) {
   const int base = blockIdx.x * kRowsPerWave;
   double a[R][LW];
   bool live[R];
+  int pos[R];  // ZERO rule: current position of each row (unused for PARTIAL)
 #pragma unroll
   for (int i = 0; i < R; ++i) {
     const int r = base + lane + 64 * i;
     live[i] = r < g.m;
+    pos[i] = r;
     const double2* src = reinterpret_cast<const double2*>(g.A + (int64_t)min(r, g.m - 1) * g.lda);
 #pragma unroll
     for (int c = 0; c < LW; c += 2) {
@@ -427,7 +433,8 @@ __global__ __launch_bounds__(64, 1) void leaf_kernel(LeafArgs g) {
 #pragma unroll
   for (int i = 0; i < R; ++i) sh.dest[lane + 64 * i] = -1;
   Table tb{0, 0, 0};
-  if (!Leaf<MODE, NKK, NR>::factor(a, live, sh, tb, g, lane, base, std::make_integer_sequence<int, LW>{})) return;
+  if (!Leaf<MODE, NKK, NR>::factor(a, live, pos, sh, tb, g, lane, base, std::make_integer_sequence<int, LW>{}))
+    return;
 
   // net row movement (participant 0 publishes it); every participant maps
   // its own moved rows to their final positions and writes its rows there

@@ -106,7 +106,7 @@ struct Panel {
   // a lane-parallel DPP merge of the per-wave candidates.
   template <int J>
   static __device__ __forceinline__ void step(double (&a)[R][W], bool (&live)[R], int (&retj)[R],
-                                              PanelLds<W>& sh, int t, int lane, int wave,
+                                              int (&pos)[R], PanelLds<W>& sh, int t, int lane, int wave,
                                               bool active, int w, int row0,
                                               int* __restrict__ info, StepStamps& ss,
                                               double* __restrict__ Lout, int ldL,
@@ -147,16 +147,19 @@ struct Panel {
         }
         best = bm >= 0.0 ? (uint64_t)__double_as_longlong(bm) + 1 : 0;
       } else {
+        // ZERO rule (Pthreads/Version-1/gauss_internal_input.c:75-121): the
+        // row at POSITION J after the earlier interchanges is "the diagonal";
+        // rows never move here, so each lane tracks its rows' positions and
+        // the key is class<<32 | ~position (class 3 non-zero diagonal, 2 other
+        // non-zero, 1 zero): the max key is the reference's choice, and keys
+        // are unique, so no row tie-break is ever needed
 #pragma unroll
         for (int i = 0; i < R; ++i) {
-          const int lr = t + i * NT;
-          // ZERO rule: the "diagonal" is physical row J (a row chosen earlier is
-          // never the diagonal here — documented difference from a physical-swap
-          // run; PARTIAL pivoting, the accuracy-relevant rule, is exact)
-          const uint64_t key = dev::pivot_ukey_t<MODE>(a[i][J], lr == J, live[i]);
-          const bool better = key > best;  // increasing rows: '>' keeps the lowest row on ties
+          const uint64_t cls = dev::pivot_ukey_t<MODE>(a[i][J], pos[i] == J, live[i]);
+          const uint64_t key = cls == 0 ? 0 : (cls << 32) | (0xffffffffu - (unsigned)pos[i]);
+          const bool better = key > best;
           best = better ? key : best;
-          brow = better ? (unsigned)lr : brow;
+          brow = better ? (unsigned)(t + i * NT) : brow;
           bval = better ? a[i][J] : bval;
         }
       }
@@ -309,13 +312,21 @@ struct Panel {
     }
     if (t == 0) {
       sh.sel[J] = (int)p;
-      if (gkey <= 1 && info && *info == 0) *info = row0 + J + 1;  // zero pivot
+      const bool zpiv = MODE == 1 ? gkey <= 1 : (gkey >> 32) <= 1;
+      if (zpiv && info && *info == 0) *info = row0 + J + 1;  // zero pivot
     }
 #pragma unroll
     for (int i = 0; i < R; ++i) {
       const bool won = t + i * NT == (int)p;
       retj[i] = won ? J : retj[i];  // the step this row was chosen at (dest, below)
       live[i] = live[i] && !won;
+    }
+    if constexpr (MODE == 0) {
+      // interchange of positions J and pos(p) (p's position is in its key)
+      const int posp = gkey != 0 ? (int)(0xffffffffu - (unsigned)gkey) : J;
+#pragma unroll
+      for (int i = 0; i < R; ++i)
+        pos[i] = (t + i * NT == (int)p) ? J : (pos[i] == J ? posp : pos[i]);
     }
     stamp<J>(ss, 4);
 
@@ -357,12 +368,12 @@ struct Panel {
 
   template <int... J>
   static __device__ __forceinline__ void steps(double (&a)[R][W], bool (&live)[R], int (&retj)[R],
-                                               PanelLds<W>& sh, int t, int lane, int wave,
+                                               int (&pos)[R], PanelLds<W>& sh, int t, int lane, int wave,
                                                bool active, int w, int row0, int* info,
                                                StepStamps& ss, double* Lout, int ldL,
                                                __amdgpu_buffer_rsrc_t lrs,
                                                std::integer_sequence<int, J...>) {
-    (step<J>(a, live, retj, sh, t, lane, wave, active, w, row0, info, ss, Lout, ldL, lrs), ...);
+    (step<J>(a, live, retj, pos, sh, t, lane, wave, active, w, row0, info, ss, Lout, ldL, lrs), ...);
   }
 
   // LDS staging tile: NT rows x W doubles in 16-byte chunks, XOR-swizzled by
@@ -564,10 +575,12 @@ __device__ __forceinline__ void panel_body(double* __restrict__ P, int64_t ldp, 
   }
   bool live[R];
   int retj[R];
+  int pos[R];  // ZERO rule: current position of each row (unused for PARTIAL)
 #pragma unroll
   for (int i = 0; i < R; ++i) {
     live[i] = t + i * NT < m;
     retj[i] = 0;
+    pos[i] = t + i * NT;
   }
   const __amdgpu_buffer_rsrc_t lrs = dev::buffer_rsrc(Lout, (uint64_t)W * (uint64_t)ldL * 8);
   const bool active = wave * dev::kWave < m;  // the wave holds panel rows
@@ -578,7 +591,7 @@ __device__ __forceinline__ void panel_body(double* __restrict__ P, int64_t ldp, 
   }
 
   StepStamps ss{};
-  K::steps(a, live, retj, sh, t, lane, wave, active, w, row0, info, ss, Lout, ldL, lrs,
+  K::steps(a, live, retj, pos, sh, t, lane, wave, active, w, row0, info, ss, Lout, ldL, lrs,
            std::make_integer_sequence<int, W>{});
   unsigned long long t2 = 0;
   if constexpr (STAMP) t2 = stamp_now();

@@ -318,8 +318,8 @@ template <int R, int MODE>
 struct Engine {
   // One column J (compile time) of the panel whose first column is k0.
   template <int J>
-  static __device__ __forceinline__ void col(double (&a)[R][kW], bool (&live)[R], Shared& sh, int t,
-                                             int lane, int wave, int w, int k0, int* info,
+  static __device__ __forceinline__ void col(double (&a)[R][kW], bool (&live)[R], int (&pos)[R], Shared& sh,
+                                             int t, int lane, int wave, int w, int k0, int* info,
                                              unsigned long long* cs) {
     if (J >= w) return;  // uniform
     // diagnostics: shader-clock stamps of column 4 (cs != null only when stamping)
@@ -365,14 +365,16 @@ struct Engine {
       bs = (bv != 0.0) ? sl[0] : R;
       h = (hi32(bv) & 0x7fffffffu) + (bs < R ? 1u : 0u);
     } else {
-      // ZERO rule: physical row k0+J is "the diagonal" when live and
-      // non-zero, else the lowest live non-zero row: key = class<<30 | ~row
+      // ZERO rule (Pthreads/Version-1/gauss_internal_input.c:75-121): the row
+      // at POSITION k0+J (after every earlier interchange) is "the diagonal"
+      // when non-zero, else the live non-zero row at the lowest position:
+      // key = class<<30 | ~position.  Rows never move here, so each lane
+      // tracks the current position of its rows (pos[], updated per pivot)
 #pragma unroll
       for (int i = 0; i < R; ++i) {
-        const int r = t + i * NT;
         const double v = a[i][J];
         const bool nz = live[i] & (v == v) & (v != 0.0);
-        const unsigned key = nz ? ((((r == k0 + J) ? 2u : 1u) << 30) | (0x3fffffffu - (unsigned)r)) : 0u;
+        const unsigned key = nz ? ((((pos[i] == k0 + J) ? 2u : 1u) << 30) | (0x3fffffffu - (unsigned)pos[i])) : 0u;
         const bool c = key > h;
         h = c ? key : h;
         bv = c ? v : bv;
@@ -448,7 +450,8 @@ struct Engine {
       if (t == 0 && info[0] == 0) info[0] = k0 + J + 1;
       unsigned lr = 0xffffffffu;
 #pragma unroll
-      for (int i = R - 1; i >= 0; --i) lr = live[i] ? (unsigned)(t + i * NT) : lr;
+      for (int i = R - 1; i >= 0; --i)  // ZERO: the row at the diagonal position (no interchange)
+        lr = (live[i] && (MODE == 1 || pos[i] == k0 + J)) ? (unsigned)(t + i * NT) : lr;
       lr = dev::wave_min_u32(lr);
       if (lane == 0) sh.fb[wave] = lr;
       __syncthreads();
@@ -484,6 +487,16 @@ struct Engine {
     if (t == 0) sh.sel[J] = (int)p;
 #pragma unroll
     for (int i = 0; i < R; ++i) live[i] = live[i] & (t + i * NT != (int)p);
+    if constexpr (MODE == 0) {
+      // interchange of positions k0+J and pos(p): p moves up to k0+J, the row
+      // that sat there moves down to p's old position (read from its key)
+      const int posp = gh != 0 ? (int)(0x3fffffffu - (gh & 0x3fffffffu)) : k0 + J;
+#pragma unroll
+      for (int i = 0; i < R; ++i) {
+        const bool isp = t + i * NT == (int)p;
+        pos[i] = isp ? k0 + J : (pos[i] == k0 + J ? posp : pos[i]);
+      }
+    }
     double l[R];
 #pragma unroll
     for (int i = 0; i < R; ++i) {
@@ -504,10 +517,10 @@ struct Engine {
   }
 
   template <int... J>
-  static __device__ __forceinline__ void factor(double (&a)[R][kW], bool (&live)[R], Shared& sh, int t,
-                                                int lane, int wave, int w, int k0, int* info,
+  static __device__ __forceinline__ void factor(double (&a)[R][kW], bool (&live)[R], int (&pos)[R], Shared& sh,
+                                                int t, int lane, int wave, int w, int k0, int* info,
                                                 unsigned long long* cs, std::integer_sequence<int, J...>) {
-    (col<J>(a, live, sh, t, lane, wave, w, k0, info, cs), ...);
+    (col<J>(a, live, pos, sh, t, lane, wave, w, k0, info, cs), ...);
   }
 };
 
@@ -519,12 +532,14 @@ __device__ __forceinline__ void engine(const Args& g, Shared& sh) {
   constexpr int kPanelBytes = R * 8 * NT * 16;
   double a[R][kW];
   bool live[R];
+  int pos[R];  // ZERO rule: current position of each row (unused for PARTIAL)
   // panel 0 straight from the input (8-byte loads: input rows need not be
   // 16-byte aligned); rows >= n read row n-1 and are never live
 #pragma unroll
   for (int i = 0; i < R; ++i) {
     const int r = t + i * NT;
     live[i] = r < n;
+    pos[i] = r;
     const double* rp = g.src + (int64_t)min(r, n - 1) * g.lds;
 #pragma unroll
     for (int c = 0; c < kW; ++c) a[i][c] = rp[min(c, n - 1)];
@@ -541,7 +556,7 @@ __device__ __forceinline__ void engine(const Args& g, Shared& sh) {
     unsigned pre = 1;
     if (more && t == 0) pre = __hip_atomic_load(&g.flags[np + j + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     unsigned long long* cs = (g.stamps != nullptr && j == 10) ? g.stamps + 8 * np + 2 * (np + 1) * np : nullptr;
-    Engine<R, MODE>::factor(a, live, sh, t, lane, wave, w, k0, g.info, cs, std::make_integer_sequence<int, kW>{});
+    Engine<R, MODE>::factor(a, live, pos, sh, t, lane, wave, w, k0, g.info, cs, std::make_integer_sequence<int, kW>{});
     if (more && t == 0) {
       int ok = 1;
       if (pre == 0) {  // not published yet: bounded poll

@@ -111,3 +111,29 @@ def test_device_random_matches_host(gelim, cuda):
     assert torch.allclose(d.cpu()[:, 130], h[:, 130], rtol=1e-12)
     s = gelim.synthetic_system(50, device=cuda)
     assert torch.equal(s.cpu(), gelim.synthetic_system(50))
+
+
+@pytest.mark.parametrize("m,w", [(40, 8), (1000, 16), (2048, 16)])
+def test_panel_zero_rule_positions(gelim, cuda, m, w):
+    """ZERO rule in the register panel: after step 0 moves row 0 to position 5,
+    step 1's zero diagonal must be replaced by the first non-zero row in
+    POSITION order (row 3), not the lowest physical row (row 0) -- the same
+    interchanges as the CPU panel (physical swaps, the reference's loop)."""
+    torch.manual_seed(m)
+    P = torch.rand(m, w, dtype=torch.float64) + 0.5
+    P[:, 0] = 0.0
+    P[5, 0] = 1.0
+    P[:, 1] = 0.0
+    P[3, 1] = 2.0
+    P[0, 1] = 7.0
+    Pc, Pg = P.clone(), P.to(cuda)
+    piv_c = torch.zeros(w, dtype=torch.int32)
+    piv_g = torch.zeros(w, dtype=torch.int32, device=cuda)
+    info_c = torch.zeros(4, dtype=torch.int32)
+    info_g = torch.zeros(4, dtype=torch.int32, device=cuda)
+    gelim.ops.lu.panel_factor(Pc, piv_c, info_c, pivot="zero")
+    gelim.ops.lu.panel_factor(Pg, piv_g, info_g, pivot="zero")
+    torch.cuda.synchronize()
+    assert piv_c.tolist()[:2] == [5, 3]
+    assert torch.equal(piv_g.cpu(), piv_c)
+    assert torch.allclose(Pg.cpu(), Pc, rtol=1e-11, atol=1e-11)

@@ -258,3 +258,48 @@ def test_refinement_steps_are_quadratic(gelim, cuda):
     assert t_step < t_factor / 10, (t_step, t_factor)
     x, steps = s.solve_refined(aug, max_steps=8)
     assert steps >= 1 and gelim.ops.gauss.error_metric(x) < 1e-9
+
+
+def zero_rule_position_system(n: int, device, tiny: float = 1e-14):
+    """[A | b] on which the internal programs' zero rule (swap only on a zero
+    diagonal, first non-zero row BELOW in position order) must track row
+    positions: step 0 swaps rows 0 and 5 (column 0 = e5), so at step 1 the
+    diagonal (row 1) is zero and the candidates are row 3 (position 3, value
+    1) and row 0 (now at position 5, value `tiny`).  The reference takes row 3;
+    a rule keyed on the physical row takes row 0 and its 1e-14 pivot ruins the
+    solution.  The trailing block is diagonally dominant in the reference's
+    final row order, so no further interchange happens."""
+    g = torch.Generator().manual_seed(n)
+    A = torch.rand(n, n, generator=g, dtype=torch.float64) * 2 - 1
+    A[:, 0] = 0.0
+    A[5, 0] = 1.0
+    A[:, 1] = 0.0
+    A[3, 1] = 1.0
+    A[0, 1] = tiny
+    row_at = list(range(n))  # final position -> row
+    row_at[0], row_at[5] = 5, 0
+    row_at[1], row_at[3] = 3, 1
+    for j in range(2, n):
+        A[row_at[j], j] += n
+    x = torch.arange(1, n + 1, dtype=torch.float64)
+    return torch.cat([A, (A @ x)[:, None]], dim=1).to(device)
+
+
+def test_zero_rule_position_system_cpu_reference(gelim):
+    """The exact reference loop (CPU seq, physical swaps) solves the pattern."""
+    aug = zero_rule_position_system(300, "cpu")
+    x = gelim.GaussSolver(300, backend="seq", pivot="zero").solve(aug)
+    assert gelim.ops.gauss.error_metric(x) < 1e-10
+
+
+@pytest.mark.parametrize("n", [600, 1500, 2048, 3000])
+def test_zero_rule_tracks_positions(gelim, cuda, n):
+    """pivot='zero' on every GPU engine (resident LU n <= 1024, fused steps +
+    resident tail to 2048, wide-panel leaves above) picks the reference's row
+    when an earlier interchange put a lower physical row at a later position."""
+    aug = zero_rule_position_system(n, cuda)
+    ref = gelim.GaussSolver(n, backend="seq", pivot="zero").solve(aug.cpu())
+    for backend in ("hip", "hip-pivot"):
+        x = gelim.GaussSolver(n, backend=backend, pivot="zero", device=cuda).solve(aug)
+        assert gelim.ops.gauss.error_metric(x) < 1e-9, backend
+        assert torch.allclose(x.cpu(), ref, rtol=1e-8, atol=0), backend

@@ -9,7 +9,7 @@
 //             one barrier per K-step, XCD-aware tile order.  4 wave64s per
 //             workgroup in a 2x2 arrangement; 64x64x16 tiles (one 32x32 MFMA
 //             block per wave, four workgroups per CU) or, when there are at
-//             least 2 such tiles per CU, 128x128x32 tiles (2x2 blocks per
+//             least 2 128x128 tiles per CU, 128x64x16 tiles (2x1 blocks per
 //             wave).  LDS holds A transposed ([k][m]) and B as is ([k][n]), so
 //             both fragment reads are unit-stride across lanes; rows padded
 //             by 4 floats (PMC: ~14 % LDS bank-conflict cycles remain on the
@@ -19,6 +19,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdlib>
+#include <cstring>
 
 #include "device_common.h"
 #include "gelim/internal.h"
@@ -61,8 +62,10 @@ __global__ void naive_elem_kernel(Mat p) {
 //    1024 workgroups, four co-resident per CU, so one workgroup's LDS store +
 //    barrier hides under the others' MFMAs: 128x128 179 us, 128x64 170 us,
 //    64x64 166 us at 2048^2);
-//  * 128 x 128 x 32 (each wave 64 x 64 = 2 x 2 MFMA blocks: half the LDS
-//    fragment reads per MFMA) for larger problems, two workgroups per CU.
+//  * 128 x 64 x 16 (each wave 64 x 32 = 2 x 1 MFMA blocks) for larger
+//    problems (>= 2 128x128 tiles per CU): 125 TF at 8192^2, 124 at 16384^2
+//    vs 120-121 for 128 x 128 x 32 (GELIM_SGEMM_SHAPE picks any compiled
+//    shape for A/B runs).
 constexpr int kMmThreads = 256;
 constexpr int APAD = 4, BPAD = 4;
 
@@ -257,7 +260,20 @@ int matmul_f32(const float* A, int64_t lda, const float* B, int64_t ldb, float* 
           hipLaunchKernelGGL((mfma_gemm_kernel<true, BM, BN, BK>), dim3(ntiles), dim3(kMmThreads), 0, s, p,
                              tiles_n, ntiles);
       };
-      if (big) launch(Shape<128, 128, 32>{});
+      // GELIM_SGEMM_SHAPE=BMxBNxBK: A/B runs of other tile shapes
+      const char* sv = std::getenv("GELIM_SGEMM_SHAPE");
+      const int shape = sv ? std::atoi(sv) * 1000000 + std::atoi(std::strchr(sv, 'x') ? std::strchr(sv, 'x') + 1 : sv) * 1000 +
+                                 std::atoi(std::strrchr(sv, 'x') ? std::strrchr(sv, 'x') + 1 : sv)
+                           : 0;
+      // measured (profiles/gemm_microbench.txt, round 2): 128x64x16 is the
+      // fastest shape once there are >= 2 128x128 tiles per CU (8192^2: 125
+      // vs 120 TF for 128x128x32), 64x64x16 below (2048^2)
+      if (shape == 64064032) launch(Shape<64, 64, 32>{});
+      else if (shape == 128128032) launch(Shape<128, 128, 32>{});
+      else if (shape == 128064032) launch(Shape<128, 64, 32>{});
+      else if (shape == 64128016) launch(Shape<64, 128, 16>{});
+      else if (shape == 64064016) launch(Shape<64, 64, 16>{});
+      else if (big || shape == 128064016) launch(Shape<128, 64, 16>{});
       else launch(Shape<64, 64, 16>{});
       break;
     }

@@ -112,7 +112,7 @@ struct gelim_gauss_plan {
   void* big_ws = nullptr;                // leaf exchange granules + rows
   int* big_pairs = nullptr;              // per-leaf row movement
   double* big_y = nullptr;               // top right-hand side after the tail
-  // lookahead (default from n = 6144, GELIM_BIG_LOOKAHEAD=0/1 forces it;
+  // lookahead (default from n = 3072, GELIM_BIG_LOOKAHEAD=0/1 forces it;
   // otherwise serial, graph-captured): the
   // trailing updates run on big_side, eagerly launched, every side kernel on
   // a grid of at most big_cap workgroups of one per CU (the CU count less
@@ -190,14 +190,19 @@ __global__ void hybrid_perm_kernel(int* __restrict__ perm, int n, int split, int
   }
 }
 
-// outer panel width of the wide-panel engine: 256 (GELIM_BIG_NB = 256 | 512)
-int64_t big_nb() {
-  static const int64_t nb = [] {
+// outer panel width of the wide-panel engine: 128 under the lookahead
+// schedule up to n = 10240, 256 above it and under the serial schedule
+// (GELIM_BIG_NB = 128 | 256 | 512 overrides).  Measured with lookahead
+// (profiles/big_nb_lookahead.txt): 8192 128 / 256 / 512 -> 34.2 / 34.8 /
+// 41.1 ms; memplus (n = 17758) 169 / 151 ms for 128 / 256; serial 8192:
+// 43.1 / 41.9 / 42.2 ms.
+int64_t big_nb(bool la, int64_t n) {
+  static const int64_t env = [] {
     const char* e = std::getenv("GELIM_BIG_NB");
-    const int64_t v = e ? std::atoll(e) : 256;
-    return (v == 512 || v == 128) ? v : int64_t(256);
+    const int64_t v = e ? std::atoll(e) : 0;
+    return (v == 512 || v == 256 || v == 128) ? v : int64_t(0);
   }();
-  return nb;
+  return env ? env : ((la && n <= 10240) ? int64_t(128) : int64_t(256));
 }
 constexpr int64_t kBigPairSlot = 1 + 4 * 32 + 3;
 
@@ -211,7 +216,7 @@ int panel_u12_update(gelim_gauss_plan* p, double* A, int64_t k, int64_t kend, in
   using namespace gelim;
   const int64_t n = p->n, lda = p->lda, LW = big::leaf_width();
   if (ce <= cb) return GELIM_OK;
-  if (big::trsm_fused()) {
+  if (big::trsm_fused() && kend - k <= 256) {  // the one-launch TRSM holds <= 256 rows in LDS
     GELIM_TRY(big::panel_trsm(A + k * lda + cb, lda, ce - cb, kend - k, A + k * lda + k, lda, s, cap));
   } else {
     for (int64_t r = k; r < kend; r += LW) {
@@ -230,16 +235,16 @@ int panel_u12_update(gelim_gauss_plan* p, double* A, int64_t k, int64_t kend, in
 //   x[K..n) = tail solve of A[K:, K:] (already carrying every update),
 //   y = A[0:K, n] - A[0:K, K:n] x[K..n),  x[0..K) = U11^-1 y.
 //
-// Outer panels P_j = [k_j, k_j+1) of big_nb() columns, each factored as
+// Outer panels P_j = [k_j, k_j+1) of big_nb(la, n) columns, each factored as
 // 32-column leaves: per leaf the leaf itself (biglu.hip), its row movement
 // on the other columns + the TRSM of its U rows, and a rank-32 GEMM of the
 // columns right of it inside the panel.
 //
-// Serial schedule (n < 6144, or GELIM_BIG_LOOKAHEAD=0): after P_j, U12 and one K = 256
+// Serial schedule (n < 3072, or GELIM_BIG_LOOKAHEAD=0): after P_j, U12 and one K = 256
 // GEMM update every column right of it -- the leaf chain and the big GEMMs
 // alternate on one stream.
 //
-// Lookahead schedule (n >= 6144, or GELIM_BIG_LOOKAHEAD=1), the leaf chain on the caller's stream
+// Lookahead schedule (n >= 3072, or GELIM_BIG_LOOKAHEAD=1), the leaf chain on the caller's stream
 // ("crit"), the big GEMMs beside it on big_side:
 //   crit, P_j:  every leaf also updates the NEXT panel's columns P_j+1
 //               (swap, TRSM, rank-32 GEMM -- right-looking at nb = 32), so
@@ -253,7 +258,7 @@ int panel_u12_update(gelim_gauss_plan* p, double* A, int64_t k, int64_t kend, in
 int enqueue_big(gelim_gauss_plan* p, double* A, double* x, double* bnorm, hipStream_t s) {
   using namespace gelim;
   const int64_t n = p->n, lda = p->lda, K = p->big_k, LW = big::leaf_width();
-  const int64_t nbw = big_nb();
+  const int64_t nbw = big_nb(p->big_la, n);
   const int64_t T = (K + nbw - 1) / nbw;
   auto kb = [&](int64_t j) { return std::min(j * nbw, K); };  // P_j = [kb(j), kb(j+1))
   const bool la = p->big_la;
@@ -520,10 +525,11 @@ extern "C" gelim_gauss_plan* gelim_gauss_plan_create(int64_t n, int algo, int pi
     // always finds free CUs.  Earlier attempts (profiles/big_lookahead_8192.txt):
     // uncapped grids 42.3 ms (leaves dispatched only as GEMM workgroups
     // drained), a CU-masked side queue 147 ms (it never ran beside the leaves).
-    // default: lookahead from n = 6144 (8192: 36.3 vs 39.8 ms serial; 4096
-    // even, where the graph-replayed serial schedule saves the launches)
+    // default: lookahead from n = 3072 (with the 128-column outer panels,
+    // profiles/big_nb_lookahead.txt: 3072 8.45 vs 8.57 ms serial, 4096 12.9
+    // vs 13.5, 5120 17.7 vs 19.1, 8192 34.2 vs 39.9)
     const char* el = std::getenv("GELIM_BIG_LOOKAHEAD");
-    p->big_la = el ? std::atoi(el) != 0 : n >= 6144;
+    p->big_la = el ? std::atoi(el) != 0 : n >= 3072;
     if (p->big_la) {
       int dev = 0, ncu = 0;
       (void)hipGetDevice(&dev);
@@ -535,7 +541,7 @@ extern "C" gelim_gauss_plan* gelim_gauss_plan_create(int64_t n, int algo, int pi
       if (std::getenv("GELIM_BIG_NET") == nullptr || std::atoi(std::getenv("GELIM_BIG_NET")) != 0)
         if (hipMalloc((void**)&p->big_net, sizeof(int) * (1 + 2 * (size_t)gelim::big::laswp_net_max())) != hipSuccess)
           return fail("net movement");
-      const int64_t T = (big_k + big_nb() - 1) / big_nb();
+      const int64_t T = (big_k + big_nb(true, n) - 1) / big_nb(true, n);
       p->big_ev.assign((size_t)(2 * T + 2), nullptr);
       for (auto& e : p->big_ev)
         if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return fail("event");

@@ -118,6 +118,8 @@ struct LeafArgs {
 // 0 start, 1 arg-max done, 2 published + pending update applied, 3 key
 // sweep ready, 4 pivot row loaded, 5 pivot row in LDS, 6 multipliers and
 // next column done, 7 key sweeps + 256 * row loads
+// (call sites test g.stamps first, so production runs issue no s_memtime: an
+// SMEM op in flight would also hold every lgkmcnt(0) wait for the LDS)
 __device__ __forceinline__ void lstamp(const LeafArgs& g, int J, int k, unsigned long long v) {
   if (g.stamps != nullptr && threadIdx.x == 0) g.stamps[((int64_t)blockIdx.x * LW + J) * 8 + k] = v;
 }
@@ -197,7 +199,7 @@ struct Leaf {
     lane = opq(lane);
     const unsigned seq = (unsigned)(J + 1);
     const int slot = (g.set * 2 + par) * kMaxW;
-    lstamp(g, J, 0, __builtin_amdgcn_s_memtime());
+    if (g.stamps != nullptr) lstamp(g, J, 0, __builtin_amdgcn_s_memtime());
     // 1. this lane's candidate: best live row (rows grow with the slot, so a
     //    strict '>' keeps the lowest row on ties)
     //    ZERO rule: the diagonal is the row at POSITION J and "the first
@@ -216,7 +218,7 @@ struct Leaf {
     const unsigned brow = (unsigned)(base + lane + 64 * bi);
     // 2. this wave's candidate
     const int wl = wave_argmax_lane(bk, brow);
-    lstamp(g, J, 1, __builtin_amdgcn_s_memtime());
+    if (g.stamps != nullptr) lstamp(g, J, 1, __builtin_amdgcn_s_memtime());
     // 3. publish: the winning lane stores its row as LW data-tagged granules
     //    {value, row, seq}, then its key granule; no drain and no flag -- a
     //    reader trusts a granule exactly when its seq matches (16-byte sc1
@@ -269,7 +271,7 @@ struct Leaf {
         for (int i = 0; i < R; ++i) a[i][c] = fma(-lp[i], uc, a[i][c]);
       }
     }
-    lstamp(g, J, 2, __builtin_amdgcn_s_memtime());
+    if (g.stamps != nullptr) lstamp(g, J, 2, __builtin_amdgcn_s_memtime());
     // 4. sweep: lane p (+ 64 k) reads participant p's key and, when the
     //    candidate rows fit (NR > 0), every participant's row too -- granule
     //    p*LW + c sits in load p/2 of lane 32 (p&1) + c -- so the winner's
@@ -308,7 +310,7 @@ struct Leaf {
         if (__hip_atomic_load(g.info + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return false;
       }
     }
-    lstamp(g, J, 3, __builtin_amdgcn_s_memtime());
+    if (g.stamps != nullptr) lstamp(g, J, 3, __builtin_amdgcn_s_memtime());
     // 5. global winner (largest key, lowest row); lanes past P hold clamped
     //    duplicates, which never change the arg-max
     uint64_t key = u64of(kv[0].x, kv[0].y);
@@ -347,7 +349,7 @@ struct Leaf {
       if ((++rl & 63) == 63 && __hip_atomic_load(g.info + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0)
         return false;
     }
-    lstamp(g, J, 4, __builtin_amdgcn_s_memtime());
+    if (g.stamps != nullptr) lstamp(g, J, 4, __builtin_amdgcn_s_memtime());
     // the winner published its row before applying the pending update of
     // pivot J-1 to columns J+1..: apply it here, with the row's own
     // multiplier (its column J-1) -- the very FMA its owner performs
@@ -368,7 +370,7 @@ struct Leaf {
     }
     if (blockIdx.x == 0 && lane == 0) g.ipiv[g.col0 + J] = g.col0 + qpos;
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the pivot row is in LDS (wave-local)
-    lstamp(g, J, 5, __builtin_amdgcn_s_memtime());
+    if (g.stamps != nullptr) lstamp(g, J, 5, __builtin_amdgcn_s_memtime());
     lstamp(g, J, 7, (unsigned long long)sweeps + 256ull * rl);
 
     // 7. multipliers; this pivot's update of column J+1 only (the next
@@ -390,7 +392,7 @@ struct Leaf {
     }
     if (g.stamps != nullptr) {
       asm volatile("" ::"v"(a[R - 1][LW - 1]));
-      lstamp(g, J, 6, __builtin_amdgcn_s_memtime());
+      if (g.stamps != nullptr) lstamp(g, J, 6, __builtin_amdgcn_s_memtime());
     }
     return true;
   }

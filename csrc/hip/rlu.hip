@@ -381,7 +381,9 @@ struct Engine {
         bs = c ? i : bs;
       }
     }
-    const double rv = recip(bv);  // speculative, hidden under the arg-max
+    // speculative, hidden under the arg-max: the value barrier keeps LLVM from
+    // sinking the reciprocal into the winner's publish branch after the ladder
+    const double rv = opq(recip(bv));
     mark(1);
 
     // 2. wave arg-max: DPP max of the 32-bit key and one ballot; the exact

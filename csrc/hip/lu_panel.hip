@@ -1010,12 +1010,13 @@ __global__ __launch_bounds__(NT) void step_kernel(StepArgs g) {
 }
 
 // ---- narrow kernel ------------------------------------------------------------
-// Step j applied to the NEXT panel's column strip, spread over ceil(m/256)
-// workgroups (one 256-row slice each) instead of serialising it on the panel
+// Step j applied to the NEXT panel's column strip, spread over ceil(m/64)
+// workgroups (one 64-row slice each: 2048: 3.96 ms vs 3.99 with 128 and 4.03
+// with 256-row slices) instead of serialising it on the panel
 // workgroup.  A is only read; the updated strip (rows relative to the step-j
 // panel top, U12 rows first) goes to a side buffer that the next panel loads
 // directly, so the row interchanges need no cross-workgroup ordering.
-constexpr int kNarrowRows = 256;
+constexpr int kNarrowRows = 64;
 
 struct NarrowArgs {
   const double* C;  // strip: A + kp*lda + k (rows relative to kp)
@@ -1060,7 +1061,7 @@ __global__ __launch_bounds__(256) void narrow_kernel(NarrowArgs g) {
                                 cc < rr && rr < wp);
     x[rr][cc] = dev::load_sel(g.C + (int64_t)min(rr, wp - 1) * g.ldc + min(cc, ncols - 1),
                               rr < wp && cc < ncols);
-    srcmap[t] = r0 + t;
+    if (t < kNarrowRows) srcmap[t] = r0 + t;
   }
 #pragma unroll
   for (int s = 0; s < 4; ++s) {

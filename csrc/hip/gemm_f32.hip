@@ -170,15 +170,21 @@ __global__ __launch_bounds__(kMmThreads, 2) void mfma_gemm_kernel(Mat p, int til
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-  typename TL::Frag f;
-  load_tiles<CHECK, BM, BN, BK>(f, p, m0, n0, 0);
-  store_tiles<BM, BN, BK>(f, As[0], Bs[0]);
+  // LDS double buffer + TWO register fragments in flight: tile kt+1 is stored
+  // to LDS during step kt from registers loaded two steps earlier, so a
+  // global load has two K-steps of MFMA work (not one) to land under
+  const int nk = (K + BK - 1) / BK;
+  typename TL::Frag fa, fb;
+  load_tiles<CHECK, BM, BN, BK>(fa, p, m0, n0, 0);
+  store_tiles<BM, BN, BK>(fa, As[0], Bs[0]);
+  if (nk > 1) load_tiles<CHECK, BM, BN, BK>(fa, p, m0, n0, BK);
+  if (nk > 2) load_tiles<CHECK, BM, BN, BK>(fb, p, m0, n0, 2 * BK);
   __syncthreads();
 
-  const int nk = (K + BK - 1) / BK;
-  for (int kt = 0; kt < nk; ++kt) {
+  // one K-step: MFMAs on LDS buffer kt&1; fnext (tile kt+1) goes to the other
+  // buffer and its registers are reloaded with tile kt+3
+  auto kstep = [&](int kt, typename TL::Frag& fnext) {
     const int cur = kt & 1;
-    if (kt + 1 < nk) load_tiles<CHECK, BM, BN, BK>(f, p, m0, n0, (kt + 1) * BK);
 #pragma unroll
     for (int k = 0; k < BK; k += 2) {
       const int kk = k + kh;
@@ -193,8 +199,13 @@ __global__ __launch_bounds__(kMmThreads, 2) void mfma_gemm_kernel(Mat p, int til
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(ai[i], bj, acc[i][j], 0, 0, 0);
       }
     }
-    if (kt + 1 < nk) store_tiles<BM, BN, BK>(f, As[cur ^ 1], Bs[cur ^ 1]);
+    if (kt + 1 < nk) store_tiles<BM, BN, BK>(fnext, As[cur ^ 1], Bs[cur ^ 1]);
+    if (kt + 3 < nk) load_tiles<CHECK, BM, BN, BK>(fnext, p, m0, n0, (kt + 3) * BK);
     __syncthreads();
+  };
+  for (int kt = 0; kt < nk; kt += 2) {
+    kstep(kt, fa);
+    if (kt + 1 < nk) kstep(kt + 1, fb);
   }
 
   // epilogue: C/D map of 32x32 f32 MFMA: col = l&31, row = (r&3) + 8(r>>2) + 4(l>>5)

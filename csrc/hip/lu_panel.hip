@@ -106,7 +106,8 @@ struct Panel {
   // a lane-parallel DPP merge of the per-wave candidates.
   template <int J>
   static __device__ __forceinline__ void step(double (&a)[R][W], bool (&live)[R], int (&retj)[R],
-                                              int (&pos)[R], PanelLds<W>& sh, int t, int lane, int wave,
+                                              int (&pos)[R], int (&rec)[4], PanelLds<W>& sh, int t, int lane,
+                                              int wave,
                                               bool active, int w, int row0,
                                               int* __restrict__ info, StepStamps& ss,
                                               double* __restrict__ Lout, int ldL,
@@ -364,16 +365,36 @@ struct Panel {
       for (int i = 0; i < R; ++i)
         dev::store_buf(lrs, (uint32_t)t * 8u, (uint32_t)(J * ldL + i * NT) * 8u, a[i][J]);
     }
+    // 6. wave 0: step J of the LAPACK interchange replay (compact ids: rows
+    //    < w keep their index, the row chosen at step j >= w is w + j; lane x
+    //    holds pos_of[x] (rec[0]), row_at[x] (rec[1]), sel[x] (rec[2]) and
+    //    the LAPACK ipiv (rec[3])) -- done column by column here instead of
+    //    as a 16-step serial chain after the loop
+    if (wave == 0) {
+      rec[2] = (lane == J) ? (int)p : rec[2];  // sel[J] (read below when p is new)
+      const int idp = (int)p < w ? (int)p : w + J;
+      const int cur = __builtin_amdgcn_readlane(rec[0], idp);
+      const int other = __builtin_amdgcn_readlane(rec[1], J);
+      rec[1] = (lane == J) ? idp : rec[1];  // row_at[J] = idp; row_at[cur] = other
+      rec[1] = (lane == cur) ? other : rec[1];
+      rec[0] = (lane == idp) ? J : rec[0];  // pos_of[idp] = J; pos_of[other] = cur
+      rec[0] = (lane == other) ? cur : rec[0];
+      if (Lout == nullptr) {  // standalone panel: LAPACK ipiv
+        const int pj = cur < w ? cur : __builtin_amdgcn_readlane(rec[2], cur < w ? 0 : cur - w);
+        rec[3] = (lane == J) ? pj : rec[3];
+      }
+    }
   }
 
   template <int... J>
   static __device__ __forceinline__ void steps(double (&a)[R][W], bool (&live)[R], int (&retj)[R],
-                                               int (&pos)[R], PanelLds<W>& sh, int t, int lane, int wave,
+                                               int (&pos)[R], int (&rec)[4], PanelLds<W>& sh, int t, int lane,
+                                               int wave,
                                                bool active, int w, int row0, int* info,
                                                StepStamps& ss, double* Lout, int ldL,
                                                __amdgpu_buffer_rsrc_t lrs,
                                                std::integer_sequence<int, J...>) {
-    (step<J>(a, live, retj, pos, sh, t, lane, wave, active, w, row0, info, ss, Lout, ldL, lrs), ...);
+    (step<J>(a, live, retj, pos, rec, sh, t, lane, wave, active, w, row0, info, ss, Lout, ldL, lrs), ...);
   }
 
   // LDS staging tile: NT rows x W doubles in 16-byte chunks, XOR-swizzled by
@@ -591,7 +612,8 @@ __device__ __forceinline__ void panel_body(double* __restrict__ P, int64_t ldp, 
   }
 
   StepStamps ss{};
-  K::steps(a, live, retj, pos, sh, t, lane, wave, active, w, row0, info, ss, Lout, ldL, lrs,
+  int rec[4] = {lane, lane, 0, 0};  // wave 0: interchange replay state (see step 6)
+  K::steps(a, live, retj, pos, rec, sh, t, lane, wave, active, w, row0, info, ss, Lout, ldL, lrs,
            std::make_integer_sequence<int, W>{});
   unsigned long long t2 = 0;
   if constexpr (STAMP) t2 = stamp_now();
@@ -604,32 +626,9 @@ __device__ __forceinline__ void panel_body(double* __restrict__ P, int64_t ldp, 
   // and row_at[x]; every index is wave-uniform, so reads are v_readlane and
   // writes are lane selects) — no serial LDS round trips.
   if (wave == 0) {
-    const int selv = (lane < w) ? sh.sel[lane] : 0;  // lane j: row chosen at step j
-    // fully unrolled with the chosen rows in SGPRs: per step two v_readlane
-    // (pos of the chosen row, row at position j) and four lane selects; the
-    // LAPACK ipiv (one more dependent readlane) only for the standalone panel
-    int ssel[W];
-#pragma unroll
-    for (int j = 0; j < W; ++j) ssel[j] = __builtin_amdgcn_readlane(selv, j);
-    const bool need_piv = Lout == nullptr;
-    int pos = lane, rat = lane, pivv = 0;
-#pragma unroll
-    for (int j = 0; j < W; ++j) {
-      if (j < w) {
-        const int p = ssel[j];
-        const int idp = p < w ? p : w + j;
-        const int cur = __builtin_amdgcn_readlane(pos, idp);
-        const int other = __builtin_amdgcn_readlane(rat, j);
-        rat = (lane == j) ? idp : rat;  // row_at[j] = idp; row_at[cur] = other
-        rat = (lane == cur) ? other : rat;
-        pos = (lane == idp) ? j : pos;  // pos_of[idp] = j; pos_of[other] = cur
-        pos = (lane == other) ? cur : pos;
-        if (need_piv) {
-          const int pj = cur < w ? cur : __builtin_amdgcn_readlane(selv, cur < w ? 0 : cur - w);
-          pivv = (lane == j) ? pj : pivv;
-        }
-      }
-    }
+    // the replay ran column by column (step 6): rec = pos_of, row_at, sel, ipiv
+    const int selv = rec[2];
+    const int pos = rec[0], rat = rec[1], pivv = rec[3];
     if (lane < w) sh.piv[lane] = pivv;
     if (lane < 2 * w) {
       sh.pos_of[lane] = pos;

@@ -52,7 +52,8 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=5)
-    p.add_argument("--n", type=int, default=2048)
+    p.add_argument("--size", "--n", dest="n", type=int, default=2048,
+                   help="matrix order of the headline system (--n is an alias)")
     p.add_argument("--backend", default="hip", choices=["hip", "hip-pivot"])
     p.add_argument("--graph", type=int, default=0, help="replay the solve from a hipGraph (1) or launch eagerly (0)")
     p.add_argument("--no-matmul", action="store_true")
@@ -98,23 +99,78 @@ def _section(out: dict, key: str, fn) -> None:
         out[key] = {"error": repr(e)[:300]}
 
 
+def launch_ranks(n: int, argv: list[str]) -> int:
+    """`python bench.py --gpus N` without a torchrun environment: act as a
+    pure launcher (no torch / gelim import, no GPU call in this process) and
+    run torchrun with N ranks as a CHILD process, relaying rank 0's JSON line
+    on stdout (everything else goes to stderr).  Returns non-zero if any rank
+    failed or no JSON line arrived.  The counterpart of the reference's
+    `mpirun -np P` (OpenMP_and_MPI/README.txt:23,46), which refuses P < 2
+    ranks (gauss_mpi/gauss_internal_input.c:289-297)."""
+    import socket
+    import subprocess
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    # torchrun's own parser prefix-matches options even after the script
+    # path ("--n" would be read as an abbreviation of "--nnodes")
+    argv = ["--size" + a[3:] if a == "--n" or a.startswith("--n=") else a for a in argv]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", str(Path(__file__).resolve()), *argv]
+    env = dict(os.environ, GELIM_BENCH_LAUNCHER="self (bench.py -> torchrun child)")
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    print(f"bench.py: launching {n} ranks: {' '.join(cmd)}", file=sys.stderr, flush=True)
+    proc = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, text=True, bufsize=1)
+    line = None
+    assert proc.stdout is not None
+    for raw in proc.stdout:  # streamed, so long runs keep showing progress
+        if raw.startswith("{") and '"metric"' in raw:
+            line = raw.strip()
+            print(line, flush=True)
+        else:
+            print(raw, end="", file=sys.stderr, flush=True)
+    rc = proc.wait()
+    if rc != 0:
+        print(f"bench.py: torchrun exited with {rc}", file=sys.stderr)
+        return rc
+    if line is None:
+        print("bench.py: no JSON line from rank 0", file=sys.stderr)
+        return 1
+    return 0
+
+
 def main() -> None:
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
     import torch
+    import torch.distributed as dist
 
     import gelim
     from gelim.parallel import comm as C
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world != args.gpus:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks")
     comm = C.init_from_env(timeout_s=300)
     dev = comm.device
     rank, N = comm.rank, comm.world_size
+    joined = dist.get_world_size() if dist.is_initialized() else 1
+    if joined != args.gpus:
+        raise SystemExit(f"bench.py: {joined} ranks joined the process group, expected {args.gpus}")
     n = args.n
+    on_gpu = dev.type == "cuda"
+    backend = args.backend if on_gpu else "omp"  # CPU ranks (gloo): the OpenMP reference loop
+
+    def dsync():
+        if on_gpu:
+            torch.cuda.synchronize(dev)
 
     # a watchdog prints whatever has been measured if a section hangs (a
-    # stuck collective), so the headline line is never lost
+    # stuck collective), so the headline line is never lost -- and exits
+    # non-zero so the hang still reads as a failure
     import threading
 
     result: dict = {}
@@ -129,23 +185,26 @@ def main() -> None:
         result["watchdog"] = f"sections after the headline did not finish within {args.budget:.0f} s"
         emit()
         sys.stdout.flush()
-        os._exit(0)
+        os._exit(3)
 
     # -- headline: one independent 2048^2 system per GPU ----------------------
     src = gelim.random_system(n, seed=1234 + rank, device=dev)
-    solver = gelim.GaussSolver(n, backend=args.backend, pivot="partial", device=dev, use_graph=bool(args.graph))
+    if on_gpu:
+        solver = gelim.GaussSolver(n, backend=backend, pivot="partial", device=dev, use_graph=bool(args.graph))
+    else:
+        solver = gelim.GaussSolver(n, backend=backend, pivot="partial")
     x = None
     for _ in range(args.warmup):
         x = solver.solve(src)
-    torch.cuda.synchronize(dev)
+    dsync()
     comm.barrier()
-    torch.cuda.synchronize(dev)
+    dsync()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         x = solver.solve(src)
-    torch.cuda.synchronize(dev)
+    dsync()
     comm.barrier()
-    torch.cuda.synchronize(dev)
+    dsync()
     elapsed = time.perf_counter() - t0
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     comm.all_reduce(t, "max")
@@ -157,7 +216,7 @@ def main() -> None:
     del src, x
 
     result.update({
-        "metric": "wall-clock sec per 2048x2048 Gauss-elim solve (fp64, partial pivoting, "
+        "metric": f"wall-clock sec per {n}x{n} Gauss-elim solve (fp64, partial pivoting, "
                   "elimination + back-substitution) [BASELINE: wall-clock sec + speedup-vs-sequential, "
                   "2048x2048 Gauss-elim & matmul]",
         "value": step_s,
@@ -173,8 +232,13 @@ def main() -> None:
         "dtype": "fp64 (Gauss, reference precision); fp32 (matmul)",
         "data": "synthetic random U[-1,1) systems generated on device, b = A(1..n); reference .dat matrices "
                 "for external_matrices",
-        "config": {"model": f"gauss_elim_{n}x{n}_partial_pivot_{args.backend}", "global_batch": N,
+        "config": {"model": f"gauss_elim_{n}x{n}_partial_pivot_{backend}", "global_batch": N,
                    "seq_len": n, "parallelism": f"dp{N} (one independent system per GPU per step)"},
+        "backend": comm.backend,
+        "world_size": joined,
+        "device": str(dev) if on_gpu else "cpu",
+        "launcher": os.environ.get("GELIM_BENCH_LAUNCHER",
+                                   "external torchrun" if "WORLD_SIZE" in os.environ else "single process"),
         "throughput_solves_per_s": N / step_s,
         "gflops_per_gpu": (2.0 / 3.0) * n ** 3 / step_s * 1e-9,
         "max_error": err.item(),
@@ -184,9 +248,11 @@ def main() -> None:
     timer.daemon = True
     timer.start()
 
-    if not args.no_matmul:
+    if not on_gpu:
+        result["sections"] = "GPU-only sections skipped (CPU ranks)"
+    if not args.no_matmul and on_gpu:
         _section(result, "matmul_2048", lambda: bench_matmul(gelim, torch, dev))
-    if not args.headline_only:
+    if not args.headline_only and on_gpu:
         # strong scaling over ALL ranks: the BASELINE.json multi-GPU configs
         _section(result, "dist_gauss_8192", lambda: bench_dist_gauss(comm, gelim, torch, 8192))
         _section(result, "dist_matmul_16384", lambda: bench_dist_matmul(comm, gelim, torch, 16384))

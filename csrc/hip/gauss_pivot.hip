@@ -205,6 +205,10 @@ int pivot_lower_resolve(const T* A, int64_t lda, int64_t n, const int* ipiv, con
                         T* y, hipStream_t s) {
   const size_t lds = (size_t)n * (sizeof(double) + sizeof(int));
   if (lds > 160 * 1024) return GELIM_FAIL(GELIM_E_ARG, "resolve: n too large for the one-workgroup solve");
+  // more than 64 KiB of dynamic LDS (n > ~5460) must be requested explicitly
+  static const bool attr = hipFuncSetAttribute((const void*)lower_resolve_kernel<T>,
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
+  if (!attr && lds > 64 * 1024) return GELIM_FAIL(GELIM_E_HIP, "resolve: LDS attribute refused");
   hipLaunchKernelGGL(lower_resolve_kernel<T>, dim3(1), dim3(1024), lds, s, A, lda, (int)n, ipiv, diag, c, y);
   HIP_TRY(hipGetLastError());
   return GELIM_OK;

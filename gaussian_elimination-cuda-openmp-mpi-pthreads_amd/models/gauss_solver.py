@@ -27,6 +27,7 @@ from ..utils.tensors import ptr, row_major_ld, stream_handle
 
 GPU_BACKENDS = {"hip": _native.GPU_BLOCKED, "hip-blocked": _native.GPU_BLOCKED, "hip-pivot": _native.GPU_PIVOT}
 CPU_BACKENDS = tuple(cpu_ops.CPU_BACKENDS)
+RESOLVE_LDS_BYTES = 160 * 1024  # lower_resolve_kernel (csrc/hip/gauss_pivot.hip)
 BACKENDS = tuple(GPU_BACKENDS) + CPU_BACKENDS
 
 
@@ -141,7 +142,9 @@ class GaussSolver:
         aug64 = aug[:, :n + 1].to(dev, torch.float64).contiguous()
         work = aug[:, :n + 1].to(dev, self.dtype).contiguous()
         tol = 4 * torch.finfo(torch.float64).eps if tol is None else tol
-        stored = self.gpu and self.backend == "hip-pivot"
+        # the stored-factor re-solve is one workgroup with y and the row map
+        # in LDS (12 bytes per row of 160 KiB); larger systems re-solve
+        stored = self.gpu and self.backend == "hip-pivot" and n * 12 <= RESOLVE_LDS_BYTES
 
         def residual(xv: torch.Tensor) -> torch.Tensor:
             if self.gpu:

@@ -35,6 +35,24 @@ class _Done:
         return True
 
 
+class _Staged:
+    """Handle of a point-to-point op staged through host memory: wait()
+    completes the host transfer, then copies a received buffer to the
+    device tensor."""
+
+    def __init__(self, work, host: torch.Tensor, dst: torch.Tensor | None = None):
+        self.work, self.host, self.dst = work, host, dst
+
+    def wait(self) -> bool:
+        self.work.wait()
+        if self.dst is not None:
+            self.dst.copy_(self.host)
+        return True
+
+    def is_completed(self) -> bool:
+        return self.work.is_completed()
+
+
 @dataclass
 class Communicator:
     rank: int = 0
@@ -47,6 +65,14 @@ class Communicator:
     @property
     def distributed(self) -> bool:
         return self.world_size > 1
+
+    @property
+    def staged(self) -> bool:
+        """gloo ranks holding device tensors (several ranks sharing one GPU,
+        which RCCL refuses): broadcast and all_reduce use gloo's own device
+        path (asynchronous, stream-ordered); all_gather and point-to-point
+        ops, which it lacks for device tensors, go through host memory."""
+        return self.backend == "gloo" and self.device.type == "cuda"
 
     def broadcast(self, t: torch.Tensor, src: int) -> torch.Tensor:
         if self.distributed:
@@ -69,14 +95,22 @@ class Communicator:
 
     def all_gather(self, out: torch.Tensor, t: torch.Tensor) -> torch.Tensor:
         """out: (world_size * t.numel()) contiguous tensor."""
-        if self.distributed:
+        if self.distributed and self.staged:
+            ho = torch.empty(out.numel(), dtype=out.dtype)
+            dist.all_gather_into_tensor(ho, t.detach().reshape(-1).cpu(), group=self.group)
+            out.view(-1).copy_(ho)
+        elif self.distributed:
             dist.all_gather_into_tensor(out, t.contiguous(), group=self.group)
         else:
             out.view(-1).copy_(t.reshape(-1))
         return out
 
     def all_gather_async(self, out: torch.Tensor, t: torch.Tensor):
-        """Non-blocking all_gather_into_tensor (see broadcast_async)."""
+        """Non-blocking all_gather_into_tensor (see broadcast_async); staged
+        ranks complete it before returning."""
+        if self.distributed and self.staged:
+            self.all_gather(out, t)
+            return _Done()
         if self.distributed:
             return dist.all_gather_into_tensor(out.view(-1), t.contiguous().view(-1), group=self.group,
                                                async_op=True)
@@ -91,15 +125,28 @@ class Communicator:
                 dist.barrier(group=self.group)
 
     def send(self, t: torch.Tensor, dst: int):
+        if self.staged:
+            h = t.detach().cpu()
+            return _Staged(dist.isend(h, dst=self.global_rank(dst), group=self.group), h)
         return dist.isend(t, dst=self.global_rank(dst), group=self.group)
 
     def recv(self, t: torch.Tensor, src: int):
+        if self.staged:
+            h = torch.empty(t.shape, dtype=t.dtype)
+            return _Staged(dist.irecv(h, src=self.global_rank(src), group=self.group), h, t)
         return dist.irecv(t, src=self.global_rank(src), group=self.group)
 
     def sendrecv(self, send_t: torch.Tensor, dst: int, recv_t: torch.Tensor, src: int) -> list:
         """Send to dst and receive from src as ONE batched p2p operation
         (batch_isend_irecv: RCCL group semantics, so a ring of such calls
         cannot deadlock on serialised send kernels).  Returns the requests."""
+        if self.staged:
+            hs = send_t.detach().cpu()
+            hr = torch.empty(recv_t.shape, dtype=recv_t.dtype)
+            ops = [dist.P2POp(dist.isend, hs, self.global_rank(dst), self.group),
+                   dist.P2POp(dist.irecv, hr, self.global_rank(src), self.group)]
+            works = dist.batch_isend_irecv(ops)
+            return [_Staged(works[0], hs), _Staged(works[1], hr, recv_t)]
         ops = [dist.P2POp(dist.isend, send_t, self.global_rank(dst), self.group),
                dist.P2POp(dist.irecv, recv_t, self.global_rank(src), self.group)]
         return dist.batch_isend_irecv(ops)
@@ -127,7 +174,10 @@ def env_world() -> tuple[int, int, int]:
 def init_from_env(backend: str | None = None, device: str | None = None,
                   timeout_s: float = 600.0) -> Communicator:
     """Join the job described by RANK/WORLD_SIZE/LOCAL_RANK/MASTER_* (torchrun).
-    backend None -> "nccl" (RCCL) when a GPU is visible, else "gloo"."""
+    backend None -> GELIM_DIST_BACKEND if set, else "nccl" (RCCL) when a GPU
+    is visible, else "gloo".  gloo with a GPU device is the transport of
+    several ranks sharing ONE GPU (tests): device tensors, host-staged where
+    gloo has no device path (Communicator.staged)."""
     rank, world, local = env_world()
     use_gpu = device != "cpu" and (device is not None or torch.cuda.is_available())
     if use_gpu:
@@ -137,7 +187,7 @@ def init_from_env(backend: str | None = None, device: str | None = None,
         dev = torch.device("cpu")
     if world <= 1:
         return Communicator(0, 1, dev, "none")
-    backend = backend or ("nccl" if use_gpu else "gloo")
+    backend = backend or os.environ.get("GELIM_DIST_BACKEND") or ("nccl" if use_gpu else "gloo")
     # failure detection: a rank that dies or hangs must not leave the others
     # blocked forever.  RCCL's async error handling turns a collective that
     # exceeds `timeout_s` (or a communicator error) into an abort + host

@@ -326,6 +326,8 @@ class DistributedGauss:
         leaf = 0
         B = self._bufs
         if g0 < L.nblocks:
+            if not la:
+                maybe_inject_fault(g0, r, fault_at_block)
             o = L.owner(g0)
             if r == o:
                 leaf = self._panel_factor(loc, g0, B[g0 & 1], leaf)
@@ -355,6 +357,15 @@ class DistributedGauss:
                 if r == o1:
                     leaf = self._panel_factor(loc, g + 1, B[(g + 1) & 1], leaf)
                 h = comm.broadcast_async(B[(g + 1) & 1][:self._bsize(g + 1)], src=o1)
+
+    def abort_code(self) -> int:
+        """Hand-off error word of the GPU leaves (info[1], max over ranks):
+        non-zero when a bounded spin timed out (code 5) or a row map left
+        the system; every later leaf of that rank then returned early, so
+        the factors are incomplete."""
+        v = self._info[1:2].clone().to(torch.int64)
+        self.comm.all_reduce(v, "max")
+        return int(v.item())
 
     def info(self) -> int:
         """First zero-pivot column + 1 over all ranks (0 = non-singular): each
@@ -407,6 +418,10 @@ class DistributedGauss:
                fault_at_block: int | None = None) -> torch.Tensor:
         """Factor + back-substitute (destroys loc); raises on a zero pivot."""
         self.factor_(loc, ckpt, resume, fault_at_block)
+        code = self.abort_code()
+        if code != 0:
+            raise _native.GelimError(_native.E_HIP, f"GPU hand-off timed out or left the system (code {code}): "
+                                                    "workgroups of a leaf were not co-resident; factors incomplete")
         if self.info() != 0:
             raise _native.SingularMatrixError(_native.E_SINGULAR, "The matrix is singular")
         return self.backsolve(loc)[:self.n]

@@ -10,11 +10,16 @@ sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
 
 
 def _init(rank, world, port, device, timeout_s=120):
+    """device "cpu": gloo CPU ranks; "cuda": every rank on cuda:0 over gloo
+    (RCCL refuses two ranks on one GPU) -- device tensors, gloo's
+    asynchronous device broadcast / all_reduce, host-staged all_gather."""
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK="0" if device == "cuda" else str(rank),
                       MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     from gelim.parallel import comm as C
 
-    return C.init_from_env(device=device if device == "cpu" else "cuda:0", timeout_s=timeout_s)
+    if device == "cpu":
+        return C.init_from_env(device="cpu", timeout_s=timeout_s)
+    return C.init_from_env(backend="gloo", device="cuda:0", timeout_s=timeout_s)
 
 
 def dead_rank(rank, world, port, outdir):
@@ -38,7 +43,7 @@ def dead_rank(rank, world, port, outdir):
     os._exit(0)
 
 
-def gauss(rank, world, port, outdir, n, block, seed, device, mode):
+def gauss(rank, world, port, outdir, n, block, seed, device, mode, lookahead=None):
     import torch
 
     import gelim
@@ -47,7 +52,8 @@ def gauss(rank, world, port, outdir, n, block, seed, device, mode):
 
     try:
         comm = _init(rank, world, port, device)
-        dg = DistributedGauss(comm, n, block=block)
+        dg = DistributedGauss(comm, n, block=block, lookahead=lookahead)
+        (Path(outdir) / f"meta{rank}.txt").write_text(f"{comm.backend} {comm.world_size} {dg.wide} {dg.lookahead}")
         if mode == "random":
             loc = dg.generate_random(seed=seed)
         else:

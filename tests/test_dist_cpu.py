@@ -95,3 +95,21 @@ def test_dead_rank_raises_not_hangs(tmp_path):
         f = tmp_path / f"raised{r}.txt"
         assert f.exists(), (codes, list(tmp_path.iterdir()))
         assert float(f.read_text().split()[0]) < 120
+
+
+def test_dist_handoff_abort_raises(gelim, monkeypatch):
+    """A leaf hand-off timeout (info[1] != 0) must fail the solve, never
+    back-substitute a half-factored system."""
+    from gelim.parallel import DistributedGauss
+    from gelim.parallel.comm import Communicator
+
+    dg = DistributedGauss(Communicator(0, 1, torch.device("cpu"), "none"), 64, block=16)
+    orig = dg.factor_
+
+    def aborted(loc, *a, **k):
+        orig(loc, *a, **k)
+        dg._info[1] = 5
+
+    monkeypatch.setattr(dg, "factor_", aborted)
+    with pytest.raises(gelim.GelimError, match="code 5"):
+        dg.solve_(dg.generate_random(seed=3))

@@ -12,32 +12,14 @@
 // rlu.hip keep an m x 16 panel on ONE CU, which caps m at 2048 (256 KiB of
 // VGPRs).  Past that the panel had to shrink to 8/4/2 columns and the
 // trailing update became a bandwidth-bound rank-2..8 update.  Here a leaf of
-// m x 32 is spread over P = ceil(m / 1024) workgroups (4 rows x 32 columns
-// per lane, one wave per SIMD), every column's pivot is an exact global
-// arg-max (ties to the lowest row, like the reference's strict '>'), and the
-// trailing update of each 256-column outer panel is one fp64 MFMA GEMM with
-// K = 256 (dgemm.hip) instead of 128 bandwidth-bound rank-2 sweeps.
-//
-// Leaf protocol, per column J (MI355X_MICROARCH.md "Valid forms", row 1):
-//  1. every workgroup finds its best live row (DPP arg-max per wave, one LDS
-//     merge behind one barrier);
-//  2. wave 0 publishes that row (16-byte sc1 stores), drains (vmcnt 0), then
-//     stores ONE 16-byte sc1 granule {key, row, seq = J+1};
-//  3. every wave polls the P granules of this column with sc1 loads (lane p
-//     reads workgroup p), picks the global winner and loads its row with sc1
-//     loads into a wave-private LDS line (no second barrier);
-//  4. multipliers and the rank-1 update of the remaining leaf columns in
-//     registers.
-// Granules and rows are double-buffered by column parity: a workgroup
-// overwrites parity J&1 only at column J+2, after every workgroup has
-// published column J+1, i.e. after every workgroup has read column J.
-// Rows never move inside the leaf (logical pivoting); every wave replays the
-// LAPACK interchange sequence in its lanes (<= 64 displaced rows), which
-// gives ipiv, the net (dst, src) row movement for the other columns, and --
-// for the zero-pivot rule -- the row currently sitting on the diagonal.  At
-// the end every lane writes its rows straight to their final LAPACK
-// positions (each final position receives exactly one row).
-// Every spin is bounded (200 ms) and reports through info[1].
+// m x 32 is spread over P participant workgroups of NWV waves each (4 rows x
+// 32 columns per lane, one wave per SIMD: 256 NWV rows per workgroup), every
+// column's pivot is an exact global arg-max (ties to the lowest row, like the
+// reference's strict '>'), and the trailing update of each outer panel is
+// one fp64 MFMA GEMM with K = nb (dgemm.hip) instead of rank-2 sweeps.  The
+// leaf kernel itself is in leaf.h (instantiated by leaf_w*.hip); this file
+// holds the row-movement, TRSM and back-substitution kernels around it and
+// the host entry points.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -47,427 +29,13 @@
 
 #include "device_common.h"
 #include "gelim/internal.h"
+#include "leaf.h"
 
 namespace gelim {
 namespace big {
 namespace {
 
-constexpr int LW = 32;             // leaf width
-constexpr int R = 4;               // rows per lane
-constexpr int kRowsPerWave = 64 * R;
-constexpr int kMaxW = 128;         // participating waves (m <= 32768)
-constexpr int kAuxSc1 = 16;        // buffer-op aux: sc1
-constexpr unsigned long long kSpinTicks = 20000000ull;  // 200 ms at 100 MHz
-
-typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-
-__device__ __forceinline__ unsigned long long rtc() {
-  unsigned long long t;
-  asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
-  return t;
-}
-
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, uint32_t bytes) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
-}
-
-__device__ __forceinline__ unsigned lo32(double x) { return (unsigned)__double_as_longlong(x); }
-__device__ __forceinline__ unsigned hi32(double x) { return (unsigned)((uint64_t)__double_as_longlong(x) >> 32); }
-__device__ __forceinline__ double mkd(unsigned lo, unsigned hi) {
-  return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
-}
-__device__ __forceinline__ uint64_t u64of(unsigned lo, unsigned hi) { return ((uint64_t)hi << 32) | lo; }
-
-// 1/p: v_rcp_f64 + two Newton steps (within an ulp of the IEEE quotient)
-__device__ __forceinline__ double recip(double p) {
-  double r = __builtin_amdgcn_rcp(p);
-  r = fma(r, fma(-p, r, 1.0), r);
-  return fma(r, fma(-p, r, 1.0), r);
-}
-
-template <typename T>
-__device__ __forceinline__ T opq(T x) {
-  asm volatile("" : "+v"(x));
-  return x;
-}
-
-// Exchange workspace: per (set, parity, participant) one key granule and
-// the candidate row as LW data-tagged granules.
-struct Xchg {
-  u32x4* key;   // [2 sets][2 parities][kMaxW] {key lo, key hi, row, seq}
-  u32x4* row;   // [2 sets][2 parities][kMaxW][LW] {value lo, value hi, row, seq}
-};
-constexpr size_t kKeyBytes = (size_t)2 * 2 * kMaxW * 16;
-constexpr size_t kRowBytes = (size_t)2 * 2 * kMaxW * LW * 16;
-
-struct LeafArgs {
-  double* A;         // leaf top-left: row c0, column c0 of the system
-  int64_t lda;
-  int m;             // rows n - c0 (>= LW)
-  int col0;          // c0 (absolute column / row of the leaf's diagonal)
-  int P;             // participating waves (one per workgroup)
-  int set;           // granule set used by this launch (leaf counter & 1)
-  int* ipiv;         // ipiv[c0 + J] = absolute row swapped with row c0 + J
-  int* pairs;        // [0] = count, then (dst, src) rows relative to c0
-  int* info;         // [0] 1 + first zero-pivot column (kept if set), [1] hand-off error
-  Xchg x;
-  unsigned long long* stamps;  // diagnostics (null in production): [P][LW][8] shader clocks
-};
-
-// Diagnostic phase stamp of column J (lane 0 of every participant):
-// 0 start, 1 arg-max done, 2 published + pending update applied, 3 key
-// sweep ready, 4 pivot row loaded, 5 pivot row in LDS, 6 multipliers and
-// next column done, 7 key sweeps + 256 * row loads
-// (call sites test g.stamps first, so production runs issue no s_memtime: an
-// SMEM op in flight would also hold every lgkmcnt(0) wait for the LDS)
-__device__ __forceinline__ void lstamp(const LeafArgs& g, int J, int k, unsigned long long v) {
-  if (g.stamps != nullptr && threadIdx.x == 0) g.stamps[((int64_t)blockIdx.x * LW + J) * 8 + k] = v;
-}
-
-struct alignas(16) LeafLds {
-  double cand[LW];             // this wave's candidate row on its way out
-  double prow[2][LW];          // the pivot rows of the last two columns (parity)
-  int dest[kRowsPerWave];      // final row of a moved local row (-1: unmoved)
-};
-
-// ---- the LAPACK interchange replay, in the lanes of the wave -----------------
-// Lane e < cnt holds one displaced row: trow (row index, relative to c0) now
-// at position tpos.  Rows not in the table sit at their own index.
-struct Table {
-  int trow, tpos, cnt;
-};
-
-
-// step J: pivot row pr moves to position J, the row at J moves to pr's spot q
-__device__ __forceinline__ int table_swap(Table& tb, int J, int pr, int lane) {
-  const uint64_t m1 = __ballot(lane < tb.cnt && tb.trow == pr);
-  const int q = m1 ? __builtin_amdgcn_readlane(tb.tpos, __ffsll((long long)m1) - 1) : pr;
-  if (q == J) return q;
-  const uint64_t m2 = __ballot(lane < tb.cnt && tb.tpos == J);
-  const int rj = m2 ? __builtin_amdgcn_readlane(tb.trow, __ffsll((long long)m2) - 1) : J;
-  int cnt = tb.cnt;
-  const int e1 = m1 ? __ffsll((long long)m1) - 1 : cnt++;
-  const int e2 = m2 ? __ffsll((long long)m2) - 1 : cnt++;
-  if (lane == e1) {
-    tb.trow = pr;
-    tb.tpos = J;
-  }
-  if (lane == e2) {
-    tb.trow = rj;
-    tb.tpos = q;
-  }
-  tb.cnt = cnt;
-  return q;
-}
-
-// Wave arg-max of (key, row): largest key, lowest row; returns the winning
-// lane (-1 when every key is 0).  DPP max of the high word + one ballot; the
-// exact 64-bit / lowest-row resolution only on high-word ties.
-__device__ __forceinline__ int wave_argmax_lane(uint64_t k, unsigned row) {
-  const unsigned h = (unsigned)(k >> 32);
-  const unsigned hm = dev::wave_max_u32(h);
-  const bool c1 = h == hm && k != 0;
-  const uint64_t hold = __ballot(c1);
-  if (hold == 0) return -1;
-  if (__popcll(hold) == 1) return __ffsll((long long)hold) - 1;
-  const unsigned lm = dev::wave_max_u32(c1 ? (unsigned)k : 0u);
-  const bool c2 = c1 && (unsigned)k == lm;
-  const unsigned mr = dev::wave_min_u32(c2 ? row : 0xffffffffu);
-  return __ffsll((long long)__ballot(c2 && row == mr)) - 1;
-}
-
-// First live column of a candidate row at column J: J - 1 (the row's own
-// multiplier of the pending update) and everything right of it.
-template <int J>
-constexpr int kLive = J > 0 ? J - 1 : 0;
-
-// Granule index g = participant * LW + column of a row sweep at column J,
-// with dead columns redirected to the participant's first live one: the
-// lanes then share that line and the sweep moves only the live bytes.
-template <int J>
-__device__ __forceinline__ int live_granule(int g) {
-  return (g % LW) < kLive<J> ? g - (g % LW) + kLive<J> : g;
-}
-
-template <int MODE, int NKK, int NR>
-struct Leaf {
-  // one column J of the leaf (compile time); false: hand-off aborted
-  template <int J>
-  static __device__ __forceinline__ bool col(double (&a)[R][LW], bool (&live)[R], int (&pos)[R], double (&lp)[R],
-                                             LeafLds& sh, Table& tb, const LeafArgs& g, int lane, int base) {
-    constexpr int par = J & 1;
-    lane = opq(lane);
-    const unsigned seq = (unsigned)(J + 1);
-    const int slot = (g.set * 2 + par) * kMaxW;
-    if (g.stamps != nullptr) lstamp(g, J, 0, __builtin_amdgcn_s_memtime());
-    // 1. this lane's candidate: best live row (rows grow with the slot, so a
-    //    strict '>' keeps the lowest row on ties)
-    //    ZERO rule: the diagonal is the row at POSITION J and "the first
-    //    non-zero row below" is the lowest POSITION, so the key is
-    //    class<<32 | ~position (each lane tracks its rows' positions)
-    uint64_t bk = 0;
-    int bi = 0;
-#pragma unroll
-    for (int i = 0; i < R; ++i) {
-      uint64_t k = dev::pivot_ukey_t<MODE>(a[i][J], pos[i] == J, live[i]);
-      if constexpr (MODE == 0) k = k == 0 ? 0 : (k << 32) | (0xffffffffu - (unsigned)pos[i]);
-      const bool c = k > bk;
-      bk = c ? k : bk;
-      bi = c ? i : bi;
-    }
-    const unsigned brow = (unsigned)(base + lane + 64 * bi);
-    // 2. this wave's candidate
-    const int wl = wave_argmax_lane(bk, brow);
-    if (g.stamps != nullptr) lstamp(g, J, 1, __builtin_amdgcn_s_memtime());
-    // 3. publish: the winning lane stores its row as LW data-tagged granules
-    //    {value, row, seq}, then its key granule; no drain and no flag -- a
-    //    reader trusts a granule exactly when its seq matches (16-byte sc1
-    //    store / load, untorn on gfx950)
-    {
-      const __amdgpu_buffer_rsrc_t rk = rsrc(g.x.key + slot + blockIdx.x, 16);
-      if (wl >= 0) {
-        // the winner's row goes through LDS (the winning lane writes it,
-        // lane c reads element c) so the LW granules leave in ONE 32-lane
-        // store instead of LW single-lane ones (each of which stalls the
-        // wave for a write-through round trip).  The slot is wave-uniform
-        // (readlane): every slot branch is a uniform one over compile-time
-        // indices, so the register panel is never dynamically indexed.
-        const int wbi = __builtin_amdgcn_readlane(bi, wl);
-        const unsigned wrow = (unsigned)__builtin_amdgcn_readlane((int)brow, wl);
-#pragma unroll
-        for (int i = 0; i < R; ++i)
-          if (wbi == i && lane == wl) {
-#pragma unroll
-            for (int c = 0; c < LW; c += 2) {
-              const double x = a[i][c], y = a[i][c + 1];
-              asm volatile("" ::"v"(x), "v"(y));
-              *reinterpret_cast<double2*>(&sh.cand[c]) = make_double2(x, y);
-            }
-          }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // wave-local LDS hand-off
-        // only columns J-1.. of the candidate row matter from column J on
-        // (J-1: the row's own multiplier of the pending update): the dead
-        // granules are neither stored nor read
-        if (lane < LW && lane >= kLive<J>) {
-          const double x = sh.cand[lane];
-          const __amdgpu_buffer_rsrc_t rr = rsrc(g.x.row + (int64_t)(slot + blockIdx.x) * LW, LW * 16);
-          __builtin_amdgcn_raw_buffer_store_b128(u32x4{lo32(x), hi32(x), wrow, seq}, rr, lane * 16, 0, kAuxSc1);
-        }
-        if (lane == wl)
-          __builtin_amdgcn_raw_buffer_store_b128(u32x4{(unsigned)bk, (unsigned)(bk >> 32), brow, seq}, rk, 0, 0,
-                                                 kAuxSc1);
-      } else if (lane == 0) {  // no live row here: an empty candidate
-        __builtin_amdgcn_raw_buffer_store_b128(u32x4{0u, 0u, 0xffffffffu, seq}, rk, 0, 0, kAuxSc1);
-      }
-    }
-    // 3b. while the exchange is in flight: the previous pivot's rank-1
-    //     update of columns J+1.. (column J got it already, it is the one
-    //     the candidate above was computed on)
-    if constexpr (J > 0) {
-#pragma unroll
-      for (int c = J + 1; c < LW; ++c) {
-        const double uc = sh.prow[(J - 1) & 1][c];
-#pragma unroll
-        for (int i = 0; i < R; ++i) a[i][c] = fma(-lp[i], uc, a[i][c]);
-      }
-    }
-    if (g.stamps != nullptr) lstamp(g, J, 2, __builtin_amdgcn_s_memtime());
-    // 4. sweep: lane p (+ 64 k) reads participant p's key and, when the
-    //    candidate rows fit (NR > 0), every participant's row too -- granule
-    //    p*LW + c sits in load p/2 of lane 32 (p&1) + c -- so the winner's
-    //    row normally arrives with the last key sweep (one round trip per
-    //    column instead of two).  All loads unconditional and in flight at
-    //    once (clamped: a predicated load is a branch with its own vmcnt(0)).
-    const __amdgpu_buffer_rsrc_t rks = rsrc(g.x.key + slot, kMaxW * 16);
-    const __amdgpu_buffer_rsrc_t rrw = rsrc(g.x.row + (int64_t)slot * LW, kMaxW * LW * 16);
-    u32x4 kv[NKK];
-    u32x4 rw[NR > 0 ? NR : 1];
-    unsigned long long t0 = 0;
-    int sweeps = 0;
-    for (int it = 0;; ++it) {
-#pragma unroll
-      for (int k = 0; k < NKK; ++k)
-        kv[k] = __builtin_amdgcn_raw_buffer_load_b128(rks, min(k * 64 + lane, g.P - 1) * 16, 0, kAuxSc1);
-      if constexpr (NR > 0) {
-#pragma unroll
-        for (int k = 0; k < NR; ++k)
-          rw[k] = __builtin_amdgcn_raw_buffer_load_b128(rrw, min(live_granule<J>(k * 64 + lane), g.P * LW - 1) * 16, 0,
-                                                        kAuxSc1);
-      }
-      bool ready = true;
-#pragma unroll
-      for (int k = 0; k < NKK; ++k) ready = ready && kv[k].w == seq;
-      if (__ballot(!ready) == 0) {
-        sweeps = it + 1;
-        break;
-      }
-      if ((it & 63) == 63) {  // abort / timeout checks every 64 sweeps (each is a round trip)
-        if (t0 == 0) t0 = rtc();
-        else if (rtc() - t0 > kSpinTicks) {
-          __hip_atomic_store(g.info + 1, 5, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          return false;
-        }
-        if (__hip_atomic_load(g.info + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return false;
-      }
-    }
-    if (g.stamps != nullptr) lstamp(g, J, 3, __builtin_amdgcn_s_memtime());
-    // 5. global winner (largest key, lowest row); lanes past P hold clamped
-    //    duplicates, which never change the arg-max
-    uint64_t key = u64of(kv[0].x, kv[0].y);
-    unsigned krow = kv[0].z;
-    int kp = lane;
-#pragma unroll
-    for (int k = 1; k < NKK; ++k) {
-      const uint64_t kk = u64of(kv[k].x, kv[k].y);
-      const bool c = kk > key || (kk == key && kk != 0 && kv[k].z < krow);
-      key = c ? kk : key;
-      krow = c ? kv[k].z : krow;
-      kp = c ? min(k * 64 + lane, g.P - 1) : kp;
-    }
-    kp = min(kp, g.P - 1);
-    const int wlw = wave_argmax_lane(key, krow);
-    const int pw = __builtin_amdgcn_readlane(kp, wlw);
-    const unsigned pr = (unsigned)__builtin_amdgcn_readlane((int)krow, wlw);
-    // 6. the winner's row in the lanes of half h = pw & 1 (lane 32 h + c
-    //    holds column c): from the sweep when it carried the rows, re-read
-    //    until every granule is current (the row was stored before the key,
-    //    but nothing orders them)
-    const int h = pw & 1;
-    const bool mine = (lane >> 5) == h;
-    const __amdgpu_buffer_rsrc_t rrs = rsrc(g.x.row + (int64_t)(slot + pw) * LW, LW * 16);
-    u32x4 rv;
-    if constexpr (NR > 0) {
-      rv = rw[0];
-#pragma unroll
-      for (int k = 1; k < NR; ++k) rv = (k == (pw >> 1)) ? rw[k] : rv;
-    } else {
-      rv = __builtin_amdgcn_raw_buffer_load_b128(rrs, max(lane & (LW - 1), kLive<J>) * 16, 0, kAuxSc1);
-    }
-    int rl = 0;
-    while (__ballot(mine && (lane & (LW - 1)) >= kLive<J> && rv.w != seq) != 0) {
-      rv = __builtin_amdgcn_raw_buffer_load_b128(rrs, max(lane & (LW - 1), kLive<J>) * 16, 0, kAuxSc1);
-      if ((++rl & 63) == 63 && __hip_atomic_load(g.info + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0)
-        return false;
-    }
-    if (g.stamps != nullptr) lstamp(g, J, 4, __builtin_amdgcn_s_memtime());
-    // the winner published its row before applying the pending update of
-    // pivot J-1 to columns J+1..: apply it here, with the row's own
-    // multiplier (its column J-1) -- the very FMA its owner performs
-    const int cc = lane & (LW - 1);
-    double pval = mkd(rv.x, rv.y);
-    if constexpr (J > 0) {
-      const double lw = mkd((unsigned)__builtin_amdgcn_readlane((int)rv.x, 32 * h + J - 1),
-                            (unsigned)__builtin_amdgcn_readlane((int)rv.y, 32 * h + J - 1));
-      if (mine && cc > J) pval = fma(-lw, sh.prow[(J - 1) & 1][cc], pval);
-    }
-    if (mine) sh.prow[par][cc] = pval;
-    // interchange replay; participant 0 records the LAPACK pivot
-    const int qpos = table_swap(tb, J, (int)pr, lane);
-    if constexpr (MODE == 0) {  // positions J and qpos exchange their rows
-#pragma unroll
-      for (int i = 0; i < R; ++i)
-        pos[i] = (base + lane + 64 * i == (int)pr) ? J : (pos[i] == J ? qpos : pos[i]);
-    }
-    if (blockIdx.x == 0 && lane == 0) g.ipiv[g.col0 + J] = g.col0 + qpos;
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the pivot row is in LDS (wave-local)
-    if (g.stamps != nullptr) lstamp(g, J, 5, __builtin_amdgcn_s_memtime());
-    lstamp(g, J, 7, (unsigned long long)sweeps + 256ull * rl);
-
-    // 7. multipliers; this pivot's update of column J+1 only (the next
-    //    candidate), the rest of it is pending until the next exchange
-    const double pv = sh.prow[par][J];
-    const bool zero = !(pv != 0.0);
-    const double rinv = zero ? 0.0 : recip(pv);
-    if (zero && blockIdx.x == 0 && lane == 0 && g.info[0] == 0) atomicCAS(g.info, 0, g.col0 + J + 1);
-#pragma unroll
-    for (int i = 0; i < R; ++i) {
-      live[i] = live[i] && (base + lane + 64 * i != (int)pr);
-      lp[i] = live[i] ? a[i][J] * rinv : 0.0;
-      a[i][J] = live[i] ? lp[i] : a[i][J];
-    }
-    if constexpr (J + 1 < LW) {
-      const double uc = sh.prow[par][J + 1];
-#pragma unroll
-      for (int i = 0; i < R; ++i) a[i][J + 1] = fma(-lp[i], uc, a[i][J + 1]);
-    }
-    if (g.stamps != nullptr) {
-      asm volatile("" ::"v"(a[R - 1][LW - 1]));
-      if (g.stamps != nullptr) lstamp(g, J, 6, __builtin_amdgcn_s_memtime());
-    }
-    return true;
-  }
-
-  template <int... J>
-  static __device__ __forceinline__ bool factor(double (&a)[R][LW], bool (&live)[R], int (&pos)[R], LeafLds& sh,
-                                                Table& tb,
-                                                const LeafArgs& g, int lane, int base,
-                                                std::integer_sequence<int, J...>) {
-    double lp[R];  // multipliers of the pending (previous) pivot
-#pragma unroll
-    for (int i = 0; i < R; ++i) lp[i] = 0.0;
-    return (col<J>(a, live, pos, lp, sh, tb, g, lane, base) && ...);
-  }
-};
-
-// One wave per workgroup; participant w = blockIdx.x owns rows
-// [256 w, 256 w + 256) of the leaf, lane l the rows 256 w + l + 64 i.
-template <int MODE, int NKK, int NR>
-__global__ __launch_bounds__(64, 1) void leaf_kernel(LeafArgs g) {
-  __shared__ LeafLds sh;
-  const int lane = threadIdx.x;
-  const int base = blockIdx.x * kRowsPerWave;
-  double a[R][LW];
-  bool live[R];
-  int pos[R];  // ZERO rule: current position of each row (unused for PARTIAL)
-#pragma unroll
-  for (int i = 0; i < R; ++i) {
-    const int r = base + lane + 64 * i;
-    live[i] = r < g.m;
-    pos[i] = r;
-    const double2* src = reinterpret_cast<const double2*>(g.A + (int64_t)min(r, g.m - 1) * g.lda);
-#pragma unroll
-    for (int c = 0; c < LW; c += 2) {
-      const double2 x = src[c / 2];
-      a[i][c] = x.x;
-      a[i][c + 1] = x.y;
-    }
-  }
-#pragma unroll
-  for (int i = 0; i < R; ++i) sh.dest[lane + 64 * i] = -1;
-  Table tb{0, 0, 0};
-  if (!Leaf<MODE, NKK, NR>::factor(a, live, pos, sh, tb, g, lane, base, std::make_integer_sequence<int, LW>{}))
-    return;
-
-  // net row movement (participant 0 publishes it); every participant maps
-  // its own moved rows to their final positions and writes its rows there
-  if (blockIdx.x == 0) {
-    if (lane < tb.cnt) {
-      g.pairs[1 + 2 * lane] = tb.tpos;
-      g.pairs[2 + 2 * lane] = tb.trow;
-    }
-    if (lane == 0) g.pairs[0] = tb.cnt;
-  }
-  if (lane < tb.cnt && tb.trow >= base && tb.trow < base + kRowsPerWave) sh.dest[tb.trow - base] = tb.tpos;
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#pragma unroll
-  for (int i = 0; i < R; ++i) {
-    const int r = base + lane + 64 * i;
-    if (r < g.m) {
-      const int d = sh.dest[lane + 64 * i];
-      double2* dst = reinterpret_cast<double2*>(g.A + (int64_t)(d < 0 ? r : d) * g.lda);
-#pragma unroll
-      for (int c = 0; c < LW; c += 2) dst[c / 2] = make_double2(a[i][c], a[i][c + 1]);
-    }
-  }
-  // clear this participant's granules of the other set for the next leaf
-  // launch (its predecessor used that set and has finished; within one solve
-  // the number of participants never grows, and the driver zeroes the whole
-  // exchange area before every solve)
-  const int o = (g.set ^ 1) * 2 * kMaxW;
-  if (lane < 2) g.x.key[o + lane * kMaxW + blockIdx.x] = u32x4{0u, 0u, 0u, 0u};
-  for (int e = lane; e < 2 * LW; e += 64)
-    g.x.row[(int64_t)(o + (e / LW) * kMaxW + blockIdx.x) * LW + (e % LW)] = u32x4{0u, 0u, 0u, 0u};
-}
+using leafk::LW;
 
 // ---- row interchanges for the other columns + TRSM of a leaf's U rows -----
 // One thread per column of [lbeg, lend) (interchanges only: the L part left
@@ -852,45 +420,70 @@ __global__ void fold_info_kernel(int* __restrict__ info, const int* __restrict__
 
 }  // namespace
 
-size_t workspace_bytes() { return kKeyBytes + kRowBytes; }
+size_t workspace_bytes() { return leafk::kKeyBytes + leafk::kRowBytes; }
 int leaf_width() { return LW; }
-int64_t max_rows() { return (int64_t)kMaxW * kRowsPerWave; }
 
-// Factor the m x LW leaf at A (row/column c0 of the system) in place.
+// Waves per leaf participant: GELIM_LEAF_WAVES = 1 | 4 (default 1), raised
+// to 4 when m needs more than kMaxP single-wave participants (m > 65536).
+// Measured (profiles/leaf_waves_ab.txt): merging 4 waves per participant in
+// LDS first does not shorten the column (4.7 vs 4.5 us at m = 8192, 5.4 vs
+// 4.5 at 32768; 8192 solve 37.4 vs 34.9 ms) -- the exchange costs the same
+// with 8 or 32 parties -- so it is kept only for the rows past 65536.
+int leaf_waves(int64_t m) {
+  static const int env = [] {
+    const char* e = std::getenv("GELIM_LEAF_WAVES");
+    const int v = e ? std::atoi(e) : 0;
+    return (v == 1 || v == 4) ? v : 1;
+  }();
+  return (env == 1 && m > (int64_t)leafk::kMaxP * leafk::kRowsPerWave) ? 4 : env;
+}
+int64_t max_rows() { return (int64_t)leafk::kMaxP * 4 * leafk::kRowsPerWave; }
+int leaf_participants(int64_t m) {
+  const int64_t rows = (int64_t)leaf_waves(m) * leafk::kRowsPerWave;
+  return (int)((m + rows - 1) / rows);
+}
+// CUs a leaf of m rows needs at once (its waves take a whole SIMD's registers:
+// four single-wave participants or one 4-wave participant per CU)
+int leaf_cus(int64_t m) {
+  const int P = leaf_participants(m);
+  return leaf_waves(m) == 4 ? P : (P + 3) / 4;
+}
+// the composed row movement keeps one int per row of the panel in LDS
+int64_t compose_max_rows() { return 160 * 1024 / (int64_t)sizeof(int) - 1; }
+
+// Factor the m x LW leaf at A (row/column c0 of the system) in place; leaf =
+// the leaf counter of this solve (granule set and tag).
 int leaf_factor(double* A, int64_t lda, int64_t m, int64_t c0, int mode, int* ipiv, int* pairs, int* info,
-                void* ws, int set, hipStream_t s, unsigned long long* stamps) {
+                void* ws, int leaf, hipStream_t s, unsigned long long* stamps) {
   if (m < LW || m > max_rows()) return GELIM_FAIL(GELIM_E_ARG, "leaf: m out of range");
   if ((reinterpret_cast<uintptr_t>(A) & 15) || (lda & 1)) return GELIM_FAIL(GELIM_E_ARG, "leaf: alignment");
-  LeafArgs a{};
+  if (leaf < 0 || leaf >= (1 << 25)) return GELIM_FAIL(GELIM_E_ARG, "leaf: counter out of range");
+  const int nwv = leaf_waves(m);
+  leafk::LeafArgs a{};
   a.A = A;
   a.lda = lda;
   a.m = (int)m;
   a.col0 = (int)c0;
-  a.P = (int)((m + kRowsPerWave - 1) / kRowsPerWave);
-  a.set = set & 1;
+  a.P = leaf_participants(m);
+  a.leaf = leaf;
   a.ipiv = ipiv;
   a.pairs = pairs;
   a.info = info;
-  a.x.key = static_cast<u32x4*>(ws);
-  a.x.row = reinterpret_cast<u32x4*>(static_cast<char*>(ws) + kKeyBytes);
+  a.x.key = static_cast<leafk::u32x4*>(ws);
+  a.x.row = reinterpret_cast<leafk::u32x4*>(static_cast<char*>(ws) + leafk::kKeyBytes);
   a.stamps = stamps;
-  // NR: row loads per lane when the sweep carries every candidate row
-  // (P <= 32: at most 16 KiB per sweep), 0 = key sweep then row load
-  // (GELIM_LEAF_2HOP=1).  Measured within noise of each other: the 8192
-  // solve 42.0 vs 43.0 ms, the lone m = 8192 leaf 137.7 vs 130.7 us
-  // (profiles/leaf_fused_vs_2hop.txt)
-#define GELIM_LEAF(NKK, NR)                                                                      \
-  if (mode == GELIM_PIVOT_PARTIAL)                                                               \
-    hipLaunchKernelGGL((leaf_kernel<1, NKK, NR>), dim3((unsigned)a.P), dim3(64), 0, s, a);       \
-  else                                                                                           \
-    hipLaunchKernelGGL((leaf_kernel<0, NKK, NR>), dim3((unsigned)a.P), dim3(64), 0, s, a)
-  const bool fused = std::getenv("GELIM_LEAF_2HOP") == nullptr;
-  if (fused && a.P <= 8) GELIM_LEAF(1, 4);
-  else if (fused && a.P <= 16) GELIM_LEAF(1, 8);
-  else if (fused && a.P <= 32) GELIM_LEAF(1, 16);
-  else if (a.P <= 64) GELIM_LEAF(1, 0);
-  else GELIM_LEAF(2, 0);
-#undef GELIM_LEAF
+  // fused sweep (the key sweep carries every candidate row, P <= 32) vs key
+  // sweep then row load (GELIM_LEAF_2HOP=1); within noise of each other for
+  // single-wave participants (profiles/leaf_fused_vs_2hop.txt)
+  static const bool fused = std::getenv("GELIM_LEAF_2HOP") == nullptr;
+  const bool zero = mode != GELIM_PIVOT_PARTIAL;
+  if (nwv == 1) {
+    if (zero) leafk::launch_leaf_nwv<1, 0>(a, fused, s);
+    else leafk::launch_leaf_nwv<1, 1>(a, fused, s);
+  } else {
+    if (zero) leafk::launch_leaf_nwv<4, 0>(a, fused, s);
+    else leafk::launch_leaf_nwv<4, 1>(a, fused, s);
+  }
   HIP_TRY(hipGetLastError());
   return GELIM_OK;
 }
@@ -940,11 +533,11 @@ int laswp_panel(double* A, int64_t lda, int64_t n, int64_t c0, int nleaves, cons
 int compose_pairs(int64_t n, int64_t c0, int nleaves, const int* pairs, int64_t slot, int* net, hipStream_t s) {
   const int64_t m = n - c0;
   if (nleaves <= 0 || m <= 0) return GELIM_OK;
-  if (m > max_rows()) return GELIM_FAIL(GELIM_E_ARG, "compose_pairs: too many rows");
+  if (m > compose_max_rows()) return GELIM_FAIL(GELIM_E_ARG, "compose_pairs: too many rows for the LDS row map");
   const size_t lds = sizeof(int) * (size_t)(m + 1);
   static const bool attr = [] {
     return hipFuncSetAttribute((const void*)compose_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                               (int)(sizeof(int) * (size_t)(max_rows() + 1))) == hipSuccess;
+                               (int)(sizeof(int) * (size_t)(compose_max_rows() + 1))) == hipSuccess;
   }();
   if (!attr) return GELIM_FAIL(GELIM_E_HIP, "compose_pairs: LDS attribute refused");
   ComposeArgs a{(int)m, nleaves, pairs, (int)slot, net};
@@ -1069,6 +662,8 @@ extern "C" int gelim_gpu_panel_trsm(double* dC, int64_t ldc, int64_t ncols, int6
 }
 
 extern "C" int64_t gelim_gpu_leaf_workspace_bytes(void) { return (int64_t)gelim::big::workspace_bytes(); }
+extern "C" int gelim_gpu_leaf_participants(int64_t m) { return gelim::big::leaf_participants(m); }
+extern "C" int64_t gelim_gpu_leaf_max_rows(void) { return gelim::big::max_rows(); }
 
 extern "C" int gelim_gpu_laswp_trsm(double* dA, int64_t lda, int64_t c0, int64_t lend, int64_t rbeg, int64_t rend,
                                     int64_t trsm_end, int64_t nrows, const int32_t* dpairs, void* stream) {

@@ -29,6 +29,8 @@
 namespace gelim {
 int dgemm(double* C, int64_t ldc, const double* A, int64_t lda, const double* B, int64_t ldb, int64_t M,
           int64_t N, int64_t K, double alpha, hipStream_t s);
+int dgemm_capped(double* C, int64_t ldc, const double* A, int64_t lda, const double* B, int64_t ldb, int64_t M,
+                 int64_t N, int64_t K, double alpha, int max_wg, hipStream_t s);
 namespace big {
 int leaf_width();
 int leaf_factor(double* A, int64_t lda, int64_t m, int64_t c0, int mode, int* ipiv, int* pairs, int* info,
@@ -40,6 +42,7 @@ int laswp_panel(double* A, int64_t lda, int64_t n, int64_t c0, int nleaves, cons
 int panel_trsm(double* C, int64_t ldc, int64_t ncols, int64_t nb, const double* L, int64_t ldl, hipStream_t s,
                int max_wg = 0);
 bool trsm_fused();
+int leaf_cus(int64_t m);
 }  // namespace big
 }  // namespace gelim
 
@@ -81,9 +84,11 @@ extern "C" int gelim_dist_panel_factor(double* A, int64_t lda, int64_t n, int64_
 // Apply a factored panel (its rows [k, n) as a row-major (n - k) x wg block L
 // with leading dimension ldl, and its leaf pair lists) to local columns
 // [cb, ce) of the slab C: the leaves' row movement, U12 = L11^-1 A12 on rows
-// [k, k + wg), A22 -= L21 U12 on rows [k + wg, n).
+// [k, k + wg), A22 -= L21 U12 on rows [k + wg, n).  max_wg > 0: every launch
+// on at most max_wg CUs (the lookahead side stream, which must leave the
+// leaves of the concurrent panel factorisation free CUs; plan.hip's cap).
 extern "C" int gelim_dist_panel_apply(double* C, int64_t ldc, int64_t n, int64_t k, int64_t cb, int64_t ce,
-                                      const double* L, int64_t ldl, int64_t wg, const int32_t* pairs,
+                                      const double* L, int64_t ldl, int64_t wg, const int32_t* pairs, int max_wg,
                                       void* stream) {
   using namespace gelim;
   hipStream_t s = (hipStream_t)stream;
@@ -91,9 +96,9 @@ extern "C" int gelim_dist_panel_apply(double* C, int64_t ldc, int64_t n, int64_t
   if (wg <= 0 || wg % kLW || n % kLW || k + wg > n || (cb & 1) || (ldc & 1) || (ldl & 1))
     return GELIM_FAIL(GELIM_E_ARG, "dist_panel_apply: widths must be multiples of 32 (even offsets)");
   const int nl = (int)(wg / kLW);
-  GELIM_TRY(big::laswp_panel(C, ldc, n, k, nl, pairs, kSlot, 0, 0, cb, ce, s));
+  GELIM_TRY(big::laswp_panel(C, ldc, n, k, nl, pairs, kSlot, 0, 0, cb, ce, s, max_wg));
   if (big::trsm_fused() && wg <= 256) {
-    GELIM_TRY(big::panel_trsm(C + k * ldc + cb, ldc, ce - cb, wg, L, ldl, s));
+    GELIM_TRY(big::panel_trsm(C + k * ldc + cb, ldc, ce - cb, wg, L, ldl, s, max_wg));
   } else {
     for (int64_t j = 0; j < nl; ++j) {
       const int64_t r = k + j * kLW;
@@ -105,7 +110,17 @@ extern "C" int gelim_dist_panel_apply(double* C, int64_t ldc, int64_t n, int64_t
     }
   }
   if (k + wg < n)
-    GELIM_TRY(dgemm(C + (k + wg) * ldc + cb, ldc, L + wg * ldl, ldl, C + k * ldc + cb, ldc, n - k - wg, ce - cb, wg,
-                    -1.0, s));
+    GELIM_TRY(dgemm_capped(C + (k + wg) * ldc + cb, ldc, L + wg * ldl, ldl, C + k * ldc + cb, ldc, n - k - wg, ce - cb,
+                           wg, -1.0, max_wg, s));
   return GELIM_OK;
+}
+
+// CUs the side stream may use beside the leaves of an m-row panel: the CU
+// count less max(64, the CUs the largest leaf needs + 8) (plan.hip's rule)
+extern "C" int gelim_dist_side_cap(int64_t m) {
+  int dev = 0, ncu = 0;
+  (void)hipGetDevice(&dev);
+  (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+  const int reserve = std::max(64, gelim::big::leaf_cus(m) + 8);
+  return ncu > reserve + 8 ? ncu - reserve : std::max(8, ncu / 2);
 }

@@ -1,0 +1,13 @@
+// Leaf instantiations: 4 wave(s) per participant, partial pivoting
+// (csrc/hip/leaf.h; split per variant so they compile in parallel).
+#include "leaf.h"
+
+#include "gelim/internal.h"
+
+namespace gelim {
+namespace big {
+namespace leafk {
+GELIM_LEAF_NWV_DEFINE(4, 1)
+}  // namespace leafk
+}  // namespace big
+}  // namespace gelim

@@ -44,6 +44,8 @@ namespace big {
 size_t workspace_bytes();
 int leaf_width();
 int64_t max_rows();
+int64_t compose_max_rows();
+int leaf_cus(int64_t m);
 int leaf_factor(double* A, int64_t lda, int64_t m, int64_t c0, int mode, int* ipiv, int* pairs, int* info,
                 void* ws, int set, hipStream_t s, unsigned long long* stamps = nullptr);
 int laswp_trsm(double* A, int64_t lda, int64_t c0, int64_t lbeg, int64_t lend, int64_t rbeg, int64_t rend,
@@ -306,7 +308,7 @@ int enqueue_big(gelim_gauss_plan* p, double* A, double* x, double* bnorm, hipStr
     HIP_TRY(hipStreamWaitEvent(side, ev_fact[j], 0));
     // the panel's row movement composed into one permutation (<= 64 rows per
     // leaf), applied by gather/scatter tiles; laswp_panel replays the lists
-    const bool net = p->big_net != nullptr && nl * 2 * LW <= big::laswp_net_max();
+    const bool net = p->big_net != nullptr && nl * 2 * LW <= big::laswp_net_max() && n - k <= big::compose_max_rows();
     if (net) GELIM_TRY(big::compose_pairs(n, k, nl, pr0, kBigPairSlot, p->big_net, side));
     auto swaps = [&](int64_t lb, int64_t le, int64_t rb, int64_t re) {
       return net ? big::laswp_net(A + k * lda, lda, p->big_net, lb, le, rb, re, side, p->big_cap)
@@ -536,6 +538,10 @@ extern "C" gelim_gauss_plan* gelim_gauss_plan_create(int64_t n, int algo, int pi
       (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
       int reserve = 64;  // 8192: 35.4 ms (32: 36.3, 96: 35.5)
       if (const char* er = std::getenv("GELIM_BIG_RESERVE")) reserve = std::max(0, std::atoi(er));
+      // never fewer free CUs than the first (largest) leaf needs at once: a
+      // side GEMM holds its CUs for its whole grid-stride loop, and a leaf
+      // whose participants cannot all be resident would spin into its timeout
+      reserve = std::max(reserve, gelim::big::leaf_cus(n) + 8);
       p->big_cap = ncu > reserve + 8 ? ncu - reserve : std::max(8, ncu / 2);
       if (hipStreamCreateWithFlags(&p->big_side, hipStreamNonBlocking) != hipSuccess) return fail("side stream");
       if (std::getenv("GELIM_BIG_NET") == nullptr || std::atoi(std::getenv("GELIM_BIG_NET")) != 0)

@@ -37,10 +37,10 @@ __global__ __launch_bounds__(256) void zero_words_kernel(unsigned* __restrict__ 
 }
 
 template <typename T>
-__global__ void init_synthetic_kernel(T* __restrict__ A, int64_t lda, int n) {
+__global__ void init_synthetic_kernel(T* __restrict__ A, int64_t lda, int n, int row0) {
   // A[i][j] = 2*min(i+1, j+1), b[i] = i in column n (P1i:59-69)
   const int j = blockIdx.x * blockDim.x + threadIdx.x;
-  const int i = blockIdx.y;
+  const int i = row0 + (int)blockIdx.y;
   if (j > n) return;
   T v = (j == n) ? (T)i : (T)(2 * ((j < i) ? (j + 1) : (i + 1)));
   A[(int64_t)i * lda + j] = v;
@@ -98,12 +98,15 @@ int copy2d_async(void* dst, size_t dpitch, const void* src, size_t spitch, size_
   if (width == 0 || rows == 0) return GELIM_OK;
   if ((width | dpitch | spitch) % 4 || ((uintptr_t)dst | (uintptr_t)src) % 4)
     return GELIM_FAIL(GELIM_E_ARG, "copy2d_async: not 4-byte aligned");
-  if (rows > 65535) return GELIM_FAIL(GELIM_E_ARG, "copy2d_async: more than 65535 rows");
   const int64_t w = (int64_t)(width / 4);
   const unsigned bx = (unsigned)std::min<int64_t>((w + 255) / 256, 64);
-  hipLaunchKernelGGL(copy2d_words_kernel, dim3(bx, (unsigned)rows), dim3(256), 0, s, static_cast<unsigned*>(dst),
-                     (int64_t)(dpitch / 4), static_cast<const unsigned*>(src), (int64_t)(spitch / 4), w);
-  HIP_TRY(hipGetLastError());
+  for (size_t r = 0; r < rows; r += 65535) {  // grid.y limit: one launch per 65535 rows
+    const size_t nr = std::min<size_t>(65535, rows - r);
+    hipLaunchKernelGGL(copy2d_words_kernel, dim3(bx, (unsigned)nr), dim3(256), 0, s,
+                       static_cast<unsigned*>(dst) + r * (dpitch / 4), (int64_t)(dpitch / 4),
+                       static_cast<const unsigned*>(src) + r * (spitch / 4), (int64_t)(spitch / 4), w);
+    HIP_TRY(hipGetLastError());
+  }
   return GELIM_OK;
 }
 
@@ -134,16 +137,20 @@ int zero_async(void* p, size_t bytes, struct ihipStream_t* s) {
 }
 
 int init_synthetic_f64(double* A, int64_t lda, int64_t n, hipStream_t s) {
-  dim3 grid((unsigned)((n + 1 + 255) / 256), (unsigned)n);
-  hipLaunchKernelGGL(init_synthetic_kernel<double>, grid, dim3(256), 0, s, A, lda, (int)n);
-  HIP_TRY(hipGetLastError());
+  for (int64_t r = 0; r < n; r += 65535) {  // grid.y limit
+    dim3 grid((unsigned)((n + 1 + 255) / 256), (unsigned)std::min<int64_t>(65535, n - r));
+    hipLaunchKernelGGL(init_synthetic_kernel<double>, grid, dim3(256), 0, s, A, lda, (int)n, (int)r);
+    HIP_TRY(hipGetLastError());
+  }
   return GELIM_OK;
 }
 
 int init_synthetic_f32(float* A, int64_t lda, int64_t n, hipStream_t s) {
-  dim3 grid((unsigned)((n + 1 + 255) / 256), (unsigned)n);
-  hipLaunchKernelGGL(init_synthetic_kernel<float>, grid, dim3(256), 0, s, A, lda, (int)n);
-  HIP_TRY(hipGetLastError());
+  for (int64_t r = 0; r < n; r += 65535) {  // grid.y limit
+    dim3 grid((unsigned)((n + 1 + 255) / 256), (unsigned)std::min<int64_t>(65535, n - r));
+    hipLaunchKernelGGL(init_synthetic_kernel<float>, grid, dim3(256), 0, s, A, lda, (int)n, (int)r);
+    HIP_TRY(hipGetLastError());
+  }
   return GELIM_OK;
 }
 

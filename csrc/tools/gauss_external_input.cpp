@@ -114,12 +114,9 @@ int main(int argc, char* argv[]) {
   } else {
     for (int64_t i = 0; i < n; ++i) A[i * lda + n] = R[i];
     int algo = backend == cli::HIP_BLOCKED ? GELIM_GPU_BLOCKED : GELIM_GPU_PIVOT;
+    // the blocked LU takes any order up to gelim_gpu_leaf_max_rows() (262144,
+    // beyond one GPU's 288 GB at fp64): no silent fallback to hip-pivot
     gelim_gauss_plan* plan = gelim_gauss_plan_create(n, algo, GELIM_PIVOT_PARTIAL, 8, use_graph);
-    if (!plan && algo == GELIM_GPU_BLOCKED) {
-      fprintf(stderr, "note: %s; falling back to hip-pivot\n", gelim_last_error());
-      backend = cli::HIP_PIVOT;
-      plan = gelim_gauss_plan_create(n, GELIM_GPU_PIVOT, GELIM_PIVOT_PARTIAL, 8, use_graph);
-    }
     if (!plan) cli::die("plan_create");
     double *dA = nullptr, *dx = nullptr;
     CLI_HIP(hipMalloc((void**)&dA, A.size() * sizeof(double)));

@@ -33,15 +33,29 @@ GPU ranks use the wide-panel engine (D = 256 by default, a multiple of the
 32-column leaf; the system is padded to a multiple of 32 with an identity
 block, which never wins a pivot search): the owner factors its panel with
 the multi-workgroup leaves (csrc/hip/dist_panel.hip, one native call per
-step), the broadcast carries [panel | leaf pair lists], and the per-block
-sequence has lookahead 1 -- the owner of block g+1 applies panel g to that
-block first, factors it and starts its broadcast, which then travels over
-xGMI while every rank (the owner too) applies panel g to the rest of its
-columns:
+step), the broadcast carries [panel | leaf pair lists], and the schedule has
+lookahead (on at every rank count) with TWO streams per rank:
 
-  rank o(g+1):  [apply g -> block g+1] [factor g+1] [bcast g+1 ...........]
-  every rank:                                       [apply g -> the rest  ]
-                                                                 [wait g+1]
+  main  (owner of g+1): [wait panel g] [apply g -> block g+1] [factor g+1]
+                        [bcast g+1 ......]
+  side  (every rank):   [wait panel g] [apply g -> the next block this rank
+                        will factor] (event) [apply g -> every other column]
+
+so an owner's leaf chain runs beside its own trailing update (the side
+stream's kernels use a capped grid, leaving CUs free for the leaves --
+plan.hip's big-engine rule), the broadcast of g+1 travels under both, and
+the panel buffers rotate over three slots (a slot is refilled only after the
+side stream has finished the panel that used it).  The reference's workers
+likewise all update rows at every step while the master overlaps its own
+B update with the transfers (gauss_mpi/gauss_internal_input.c:141-175).
+
+The last <= 2048 columns (GPU, lookahead) are not eliminated panel by
+panel: their fully updated trailing system is all_gathered once and solved
+redundantly on every rank by the single-GPU 2048 engine (GaussSolver: fused
+register-resident steps + resident LU, one graph replay), then y_top = b_top
+- U[:K, K:] x_tail is one local GEMV per rank + one all_reduce, and the top
+K columns are back-substituted as above.  At 8192 that replaces 8 latency-
+bound panel rounds by one 4 ms solve.
 
 Runs on CPU tensors with gloo as well (the native CPU building blocks, the
 original D = 64 sub-panel path), which is how the multi-rank path is tested
@@ -102,21 +116,25 @@ class ColumnLayout:
 
 
 LEAF = 32  # leaf width of the wide-panel engine (csrc/hip/biglu.hip)
+TAIL_ROWS = 2048  # GPU: the trailing system of at most this order goes to the single-GPU 2048 engine
+NBUF = 3  # GPU panel buffers in rotation
 
 
 class DistributedGauss:
     """Column block-cyclic distributed solver of one n x n system.
 
     block: columns per block (GPU default 256, a multiple of 32; CPU 64).
-    lookahead: overlap the next panel's broadcast with the trailing update
-    (GPU path; default on with more than one rank -- on one rank there is
-    nothing to hide and the split apply costs 50.8 -> 59.4 ms at n = 8192;
-    off while checkpointing, whose snapshots need quiet block boundaries)."""
+    lookahead: GPU path -- factor the next panel on the main stream while the
+    trailing update runs on a side stream, and finish with the 2048 engine
+    (default on; off while checkpointing, whose snapshots need quiet block
+    boundaries, and for lookahead=False: one stream, every block a panel).
+    tail: order of the trailing system handed to the single-GPU engine
+    (default TAIL_ROWS; 0 = none)."""
 
     def __init__(self, comm: Communicator, n: int, block: int | None = None, pivot: str = "partial",
-                 lookahead: bool | None = None):
+                 lookahead: bool | None = None, tail: int | None = None):
         if lookahead is None:
-            lookahead = comm.world_size > 1
+            lookahead = True
         self.device = comm.device
         self.wide = self.device.type == "cuda"
         if block is None:
@@ -126,6 +144,7 @@ class DistributedGauss:
         if self.wide and block % LEAF:
             raise ValueError(f"GPU blocks are multiples of the {LEAF}-column leaf (got {block})")
         self.comm, self.n, self.pivot, self.lookahead = comm, n, pivot, lookahead
+        self.tail_rows = TAIL_ROWS if tail is None else int(tail)
         # GPU: the system is padded to a multiple of the leaf width
         self.n_pad = -(-n // LEAF) * LEAF if self.wide else n
         self.layout = ColumnLayout(self.n_pad, comm.world_size, block)
@@ -140,7 +159,10 @@ class DistributedGauss:
             nl = D // LEAF
             self._npd = -(-nl * self._slot // 2)  # pair lists, in doubles
             self._bufs = [torch.empty(self.n_pad * D + self._npd, dtype=torch.float64, device=self.device)
-                          for _ in range(2)]
+                          for _ in range(NBUF)]
+            self._side = torch.cuda.Stream(self.device)
+            self._cap = int(lib.gelim_dist_side_cap(self.n_pad))
+            self._tail_solver = None
             self._pairs = torch.zeros(nl * self._slot, dtype=torch.int32, device=self.device)
             self._ipiv = torch.zeros(self.n_pad + 64, dtype=torch.int32, device=self.device)
             self._ws = torch.zeros(int(lib.gelim_gpu_leaf_workspace_bytes()) // 8, dtype=torch.float64,
@@ -148,6 +170,7 @@ class DistributedGauss:
         else:
             self._buf = torch.empty((n + 1) * D, dtype=torch.float64, device=self.device)
             self._piv = torch.zeros(D + 64, dtype=torch.int32, device=self.device)
+        self._xt = None  # solution of the tail system (GPU lookahead path), set by factor_
 
     # -- data placement -----------------------------------------------------
     def empty_local(self) -> torch.Tensor:
@@ -297,23 +320,145 @@ class DistributedGauss:
         L = self.layout
         return (self.n_pad - g * L.D) * L.width(g) + self._npd
 
-    def _panel_apply(self, loc: torch.Tensor, g: int, buf: torch.Tensor, cb: int, ce: int) -> None:
-        """Panel g (from buf) applied to local columns [cb, ce)."""
+    def _panel_apply(self, loc: torch.Tensor, g: int, buf: torch.Tensor, cb: int, ce: int,
+                     stream: torch.cuda.Stream | None = None, cap: int = 0) -> None:
+        """Panel g (from buf) applied to local columns [cb, ce), on `stream`
+        (default: the current one), every launch on at most `cap` CUs."""
         if ce <= cb:
             return
         L, n = self.layout, self.n_pad
         k, wg = g * L.D, L.width(g)
         m = n - k
         pairs = buf[m * wg:m * wg + self._npd]
+        sh = stream.cuda_stream if stream is not None else stream_handle(self.device)
         _native.check(_native.lib().gelim_dist_panel_apply(ptr(loc), loc.stride(0), n, k, cb, ce, ptr(buf), wg, wg,
-                                                           ptr(pairs), stream_handle(self.device)),
-                      "dist_panel_apply")
+                                                           ptr(pairs), cap, sh), "dist_panel_apply")
+
+    def _block_at_local_col(self, c: int) -> int:
+        """Global block index of this rank's local block starting at local column c."""
+        return self.comm.rank + (c // self.layout.D) * self.layout.P
+
+    def _panel_blocks(self, use_tail: bool) -> int:
+        """Blocks eliminated as broadcast panels; the rest is the tail system."""
+        L = self.layout
+        if not use_tail or self.tail_rows <= 0:
+            return L.nblocks
+        return max(0, -(-(self.n_pad - self.tail_rows) // L.D))
+
+    def _factor_lookahead(self, loc: torch.Tensor, G: int, fault_at_block: int | None) -> None:
+        """Panels 0..G-1 with the two-stream lookahead schedule (module
+        docstring); every column of this rank -- the tail's included --
+        receives every panel."""
+        L, r, comm = self.layout, self.comm.rank, self.comm
+        if G == 0:
+            return
+        end = self.nloc + 1  # local columns + b
+        main = torch.cuda.current_stream(self.device)
+        side = self._side
+        side.wait_stream(main)  # loc / buffers as the caller left them
+        B = self._bufs
+        nb = len(B)
+        ev_avail = [torch.cuda.Event() for _ in range(G)]
+        ev_first = [torch.cuda.Event() for _ in range(G)]
+        ev_rest = [torch.cuda.Event() for _ in range(G)]
+        leaf = 0
+        handles = {}
+        o = L.owner(0)
+        if r == o:
+            leaf = self._panel_factor(loc, 0, B[0], leaf)
+        handles[0] = comm.broadcast_async(B[0][:self._bsize(0)], src=o)
+        for g in range(G):
+            maybe_inject_fault(g, r, fault_at_block)
+            buf = B[g % nb]
+            handles.pop(g).wait()  # main waits for panel g
+            ev_avail[g].record(main)
+            c0 = L.first_local_col_after(g, r)
+            nxt = g + 1 < G
+            o1 = L.owner(g + 1) if nxt else -1
+            if o1 == r:
+                # block g+1: its last update (panel g) on main, then its factorisation;
+                # panel g-1 reached it first on the side stream (ev_first[g-1])
+                w1 = L.width(g + 1)
+                if g >= 1:
+                    main.wait_event(ev_first[g - 1])
+                self._panel_apply(loc, g, buf, c0, c0 + w1)
+                if g + 1 >= nb:
+                    main.wait_event(ev_rest[g + 1 - nb])  # its buffer slot is free again
+                leaf = self._panel_factor(loc, g + 1, B[(g + 1) % nb], leaf)
+                c0 += w1
+            if nxt:
+                if o1 != r and g + 1 >= nb:
+                    main.wait_event(ev_rest[g + 1 - nb])
+                handles[g + 1] = comm.broadcast_async(B[(g + 1) % nb][:self._bsize(g + 1)], src=o1)
+            # side: the next block this rank factors first, then everything else
+            wf = L.width(self._block_at_local_col(c0)) if c0 < self.nloc else 0
+            side.wait_event(ev_avail[g])
+            with torch.cuda.stream(side):
+                self._panel_apply(loc, g, buf, c0, c0 + wf, side, self._cap)
+                ev_first[g].record(side)
+                self._panel_apply(loc, g, buf, c0 + wf, end, side, self._cap)
+                ev_rest[g].record(side)
+        main.wait_event(ev_rest[G - 1])
+
+    def _tail_solve(self, loc: torch.Tensor, G: int) -> None:
+        """The trailing system (rows and columns from K = G*D, every panel
+        applied) gathered onto every rank and solved by the single-GPU engine;
+        sets self._xt (tail solution) and self._ytop (b_top - U[:K, K:] x_t)."""
+        L, P, r, comm = self.layout, self.comm.world_size, self.comm.rank, self.comm
+        D, n = L.D, self.n_pad
+        K = G * D
+        mt = n - K
+        nt = L.nblocks - G
+        per = -(-nt // P)
+        mine_b = [b for b in L.local_blocks(r) if b >= G]
+        mine = torch.zeros((per, mt, D), dtype=torch.float64, device=self.device)
+        for i, b in enumerate(mine_b):
+            c, w = L.local_col(b), L.width(b)
+            mine[i, :, :w] = loc[K:, c:c + w]
+        gathered = torch.empty((P, per, mt, D), dtype=torch.float64, device=self.device)
+        comm.all_gather(gathered.view(-1), mine.view(-1))
+        aug = torch.empty((mt, padded_ld(mt + 1)), dtype=torch.float64, device=self.device)
+        for t in range(nt):
+            b = G + t
+            q = b % P
+            first_q = G + ((q - G) % P)
+            w = L.width(b)
+            aug[:, t * D:t * D + w] = gathered[q, (b - first_q) // P, :, :w]
+        aug[:, mt] = loc[K:, self.nloc]
+        if self._tail_solver is None or self._tail_solver.n != mt:
+            from ..models.gauss_solver import GaussSolver
+
+            # emulated ranks are threads of one process on one device: a graph
+            # capture in one thread would collide with the others' launches on
+            # the shared legacy stream, so they launch the tail engine eagerly
+            self._tail_solver = GaussSolver(mt, backend="hip", pivot=self.pivot, device=self.device,
+                                            use_graph=self.comm.backend != "emulated")
+        xt = self._tail_solver.solve(aug)
+        tinfo = self._tail_solver.info()  # raises on a hand-off error of the tail engine
+        if tinfo:
+            col = torch.full_like(self._info[:1], K + tinfo)
+            self._info[:1] = torch.where(self._info[:1] == 0, col, self._info[:1])
+        contrib = torch.zeros(K, dtype=torch.float64, device=self.device)
+        if K:
+            for b in mine_b:
+                c, w = L.local_col(b), L.width(b)
+                contrib += loc[:K, c:c + w] @ xt[(b - G) * D:(b - G) * D + w]
+        comm.all_reduce(contrib)
+        self._ytop = loc[:K, self.nloc] - contrib
+        self._xt = xt
 
     def _factor_wide(self, loc: torch.Tensor, ckpt: Checkpointer | None, resume: bool,
                      fault_at_block: int | None) -> None:
         L, r, comm = self.layout, self.comm.rank, self.comm
         self._info.zero_()
         self._ws.zero_()
+        self._xt = None
+        if self.lookahead and ckpt is None:
+            G = self._panel_blocks(use_tail=True)
+            self._factor_lookahead(loc, G, fault_at_block)
+            if G < L.nblocks:
+                self._tail_solve(loc, G)
+            return
         g0 = 0
         if ckpt is not None and resume:
             st = ckpt.load()
@@ -321,35 +466,22 @@ class DistributedGauss:
                 loc.copy_(st.loc.to(loc.device))
                 self._info.copy_(st.info.to(self._info.device))
                 g0 = st.block
-        la = self.lookahead and ckpt is None
+        # single stream, every block a broadcast panel (lookahead off, or
+        # checkpointing: snapshots are taken at quiet block boundaries)
         end = self.nloc + 1  # local columns + b
         leaf = 0
         B = self._bufs
         if g0 < L.nblocks:
-            if not la:
-                maybe_inject_fault(g0, r, fault_at_block)
+            maybe_inject_fault(g0, r, fault_at_block)
             o = L.owner(g0)
             if r == o:
                 leaf = self._panel_factor(loc, g0, B[g0 & 1], leaf)
             h = comm.broadcast_async(B[g0 & 1][:self._bsize(g0)], src=o)
         for g in range(g0, L.nblocks):
-            if la:
-                maybe_inject_fault(g, r, fault_at_block)
             h.wait()
             buf = B[g & 1]
-            c0 = L.first_local_col_after(g, r)
-            nxt = g + 1 < L.nblocks
-            if nxt and la:
-                # lookahead: block g+1 first (its owner), its broadcast under the rest
-                o1 = L.owner(g + 1)
-                if r == o1:
-                    w1 = L.width(g + 1)
-                    self._panel_apply(loc, g, buf, c0, c0 + w1)
-                    leaf = self._panel_factor(loc, g + 1, B[(g + 1) & 1], leaf)
-                    c0 += w1
-                h = comm.broadcast_async(B[(g + 1) & 1][:self._bsize(g + 1)], src=o1)
-            self._panel_apply(loc, g, buf, c0, end)
-            if nxt and not la:
+            self._panel_apply(loc, g, buf, L.first_local_col_after(g, r), end)
+            if g + 1 < L.nblocks:
                 maybe_inject_fault(g + 1, r, fault_at_block)
                 if ckpt is not None and ckpt.due(g + 1):
                     ckpt.save(g + 1, loc, self._info)
@@ -379,23 +511,26 @@ class DistributedGauss:
         return 0 if val == sentinel else val
 
     # -- back substitution ----------------------------------------------------
-    def backsolve(self, loc: torch.Tensor) -> torch.Tensor:
+    def backsolve(self, loc: torch.Tensor, y: torch.Tensor | None = None, ntop: int | None = None) -> torch.Tensor:
         """U x = y with U column-distributed, y replicated; returns x on every
-        rank."""
-        L, n, P, D, r = self.layout, self.layout.n, self.comm.world_size, self.layout.D, self.comm.rank
+        rank.  ntop: only the leading ntop x ntop triangle (a multiple of D;
+        y then has ntop entries -- the tail path's y_top)."""
+        L, P, D, r = self.layout, self.comm.world_size, self.layout.D, self.comm.rank
+        n = L.n if ntop is None else ntop
+        nblk = -(-n // D)
         S = P * D
         nsuper = math.ceil(n / S)
         # one all_gather of every super-block's diagonal columns
         mine = torch.zeros((nsuper, S, D), dtype=torch.float64, device=self.device)
         for s in range(nsuper):
             g = s * P + r
-            if g < L.nblocks:
+            if g < nblk:
                 s0, e = s * S, min((s + 1) * S, n)
                 c, w = L.local_col(g), L.width(g)
                 mine[s, :e - s0, :w] = loc[s0:e, c:c + w]
         gathered = torch.empty((P, nsuper, S, D), dtype=torch.float64, device=self.device)
         self.comm.all_gather(gathered.view(-1), mine.view(-1))
-        y = loc[:, self.nloc].contiguous()
+        y = (loc[:n, self.nloc] if y is None else y).contiguous()
         acc = torch.zeros((n, 1), dtype=torch.float64, device=self.device)  # -sum U x (own cols)
         x = torch.zeros(n, dtype=torch.float64, device=self.device)
         for s in reversed(range(nsuper)):
@@ -408,7 +543,7 @@ class DistributedGauss:
             xs = lu.backsub(Uss, rhs)
             x[s0:e] = xs
             g = s * P + r
-            if g < L.nblocks and s0 > 0:
+            if g < nblk and s0 > 0:
                 c, w = L.local_col(g), L.width(g)
                 xp = xs[r * D:r * D + w].contiguous().view(w, 1)
                 lu.gemm_update(acc[:s0], loc[:s0, c:c + w], xp)
@@ -424,4 +559,8 @@ class DistributedGauss:
                                                     "workgroups of a leaf were not co-resident; factors incomplete")
         if self.info() != 0:
             raise _native.SingularMatrixError(_native.E_SINGULAR, "The matrix is singular")
+        if self._xt is not None:
+            K = self.n_pad - self._xt.numel()
+            xtop = self.backsolve(loc, self._ytop, K) if K else self._ytop
+            return torch.cat([xtop, self._xt])[:self.n]
         return self.backsolve(loc)[:self.n]

@@ -27,7 +27,7 @@ def timeit(fn, reps=10):
 
 
 def main() -> None:
-    m = int(sys.argv[1]) if len(sys.argv) > 1 else 8192
+    m = int(sys.argv[1]) if len(sys.argv) > 1 and sys.argv[1].isdigit() else 8192
     dev = torch.device("cuda:0")
     lib = _native.lib()
     sh = stream_handle(dev)
@@ -48,7 +48,11 @@ def main() -> None:
         A.copy_(A0)
 
     t_leaf = timeit(leaf) - timeit(copy_only)
-    print(f"leaf m={m}: {t_leaf:.1f} us ({t_leaf / 32:.2f} us/column)")
+    import os
+    print(f"leaf m={m} (GELIM_LEAF_WAVES={os.environ.get('GELIM_LEAF_WAVES', 'default')}, "
+          f"{lib.gelim_gpu_leaf_participants(m)} participants): {t_leaf:.1f} us ({t_leaf / 32:.2f} us/column)")
+    if "--time-only" in sys.argv:
+        return
     leaf()
     torch.cuda.synchronize()
 
@@ -62,7 +66,7 @@ def main() -> None:
 
     print(f"trsm only over {m + 1} columns: {timeit(trsm):.1f} us")
     # phase stamps
-    P = (m + 255) // 256
+    P = int(lib.gelim_gpu_leaf_participants(m))
     st = torch.zeros(P * 32 * 8, dtype=torch.int64, device=dev)
     A.copy_(A0)
     _native.check(lib.gelim_debug_leaf_stamps(ptr(A), lda, m, ptr(ws), ptr(st), sh), "stamps")

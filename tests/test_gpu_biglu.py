@@ -314,3 +314,16 @@ def test_panel_trsm_matches_torch(gelim, cuda, nb, ncols, cap):
     torch.cuda.synchronize()
     assert torch.allclose(Cg.cpu()[:, :ncols], ref, rtol=1e-11, atol=1e-11)
     assert torch.equal(Cg.cpu()[:, ncols:], C[:, ncols:])
+
+
+def test_big_solver_past_old_leaf_cap(gelim, cuda):
+    """n = 40000 (12.8 GB): past the round-2 cap of 32768 rows per leaf."""
+    n = 40000
+    aug = gelim.random_system(n, seed=4, device=cuda)
+    s = gelim.GaussSolver(n, backend="hip", device=cuda)
+    x = s.solve(aug, check=True)
+    s.close()
+    ref = torch.linalg.solve(aug[:, :n], aug[:, n].clone())
+    assert ((x - ref).abs().max() / ref.abs().max()).item() < 1e-7
+    del aug, ref
+    torch.cuda.empty_cache()

@@ -58,25 +58,31 @@ extern "C" int64_t gelim_dist_pair_slot(void) { return kSlot; }
 // rows), its net row movement to pairs + l * slot; info[0] = 1 + the first
 // zero-pivot column (global).  ws: the leaf exchange workspace, zeroed before
 // the first leaf of a solve; leaf0: the solve's running leaf counter.
+// upd_end > lc + wg: every leaf also updates local columns [lc + wg, upd_end)
+// -- the next block when this rank factors it next (one rank: plan.hip's
+// lookahead form, so that block is up to date the moment this panel is) --
+// after waiting, once leaf 0 is factored, for wait_ev (may be null): the
+// event after which those columns carry every earlier panel.
 extern "C" int gelim_dist_panel_factor(double* A, int64_t lda, int64_t n, int64_t k, int64_t lc, int64_t wg,
                                        int pivot, int32_t* ipiv, int32_t* pairs, int32_t* info, void* ws, int leaf0,
-                                       void* stream) {
+                                       int64_t upd_end, void* wait_ev, void* stream) {
   using namespace gelim;
   hipStream_t s = (hipStream_t)stream;
   if (wg <= 0 || wg % kLW || n % kLW || k + wg > n || (lc & 1) || (lda & 1))
     return GELIM_FAIL(GELIM_E_ARG, "dist_panel_factor: widths must be multiples of 32 (even offsets)");
+  const int64_t ue = std::max(upd_end, lc + wg);
   for (int64_t l = 0; l * kLW < wg; ++l) {
     const int64_t c0 = k + l * kLW, col = lc + l * kLW;
     int* pr = pairs + l * kSlot;
     GELIM_TRY(big::leaf_factor(A + c0 * lda + col, lda, n - c0, c0, pivot, ipiv, pr, info, ws, leaf0 + (int)l, s));
-    // the leaf's row movement on the panel's other columns, TRSM of its U
-    // rows on the panel columns right of it
-    GELIM_TRY(big::laswp_trsm(A + c0 * lda, lda, col, lc, col, col + kLW, lc + wg, lc + wg, n - c0, pr, s, nullptr,
-                              0));
+    if (l == 0 && wait_ev != nullptr && ue > lc + wg) HIP_TRY(hipStreamWaitEvent(s, (hipEvent_t)wait_ev, 0));
+    // the leaf's row movement on the panel's other columns (and the next
+    // block's), TRSM of its U rows on the columns right of it
+    GELIM_TRY(big::laswp_trsm(A + c0 * lda, lda, col, lc, col, col + kLW, ue, ue, n - c0, pr, s, nullptr, 0));
     const int64_t c1 = col + kLW, r1 = c0 + kLW;
-    if (c1 < lc + wg && r1 < n)
-      GELIM_TRY(dgemm(A + r1 * lda + c1, lda, A + r1 * lda + col, lda, A + c0 * lda + c1, lda, n - r1, lc + wg - c1,
-                      kLW, -1.0, s));
+    if (c1 < ue && r1 < n)
+      GELIM_TRY(dgemm(A + r1 * lda + c1, lda, A + r1 * lda + col, lda, A + c0 * lda + c1, lda, n - r1, ue - c1, kLW,
+                      -1.0, s));
   }
   return GELIM_OK;
 }

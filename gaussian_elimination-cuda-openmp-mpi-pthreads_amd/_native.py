@@ -77,7 +77,8 @@ _PROTOS = {
     "gelim_debug_leaf_stamps": (_int, [_vp, _i64, _i64, _vp, _vp, _vp]),
     "gelim_gpu_laswp_trsm": (_int, [_vp, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _vp, _vp]),
     "gelim_dist_pair_slot": (_i64, []),
-    "gelim_dist_panel_factor": (_int, [_vp, _i64, _i64, _i64, _i64, _i64, _int, _vp, _vp, _vp, _vp, _int, _vp]),
+    "gelim_dist_panel_factor": (_int, [_vp, _i64, _i64, _i64, _i64, _i64, _int, _vp, _vp, _vp, _vp, _int, _i64, _vp,
+                                       _vp]),
     "gelim_dist_panel_apply": (_int, [_vp, _i64, _i64, _i64, _i64, _i64, _vp, _i64, _i64, _vp, _int, _vp]),
     "gelim_dist_side_cap": (_int, [_i64]),
     "gelim_gpu_panel_trsm": (_int, [_vp, _i64, _i64, _i64, _vp, _i64, _int, _vp]),

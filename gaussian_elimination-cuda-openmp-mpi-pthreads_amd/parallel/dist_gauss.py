@@ -301,16 +301,20 @@ class DistributedGauss:
                     lu.gemm_update(C[so + ws:], buf[so + ws:m, so:so + ws], C[so:so + ws])
 
     # -- GPU: wide-panel engine with lookahead -----------------------------------
-    def _panel_factor(self, loc: torch.Tensor, g: int, buf: torch.Tensor, leaf: int) -> int:
+    def _panel_factor(self, loc: torch.Tensor, g: int, buf: torch.Tensor, leaf: int, upd_end: int = 0,
+                      wait_ev: torch.cuda.Event | None = None) -> int:
         """Owner: factor block g (up to date) in place and pack [panel |
-        pair lists] into buf; returns the next leaf counter."""
+        pair lists] into buf; returns the next leaf counter.  upd_end: the
+        leaves also update local columns [end of block g, upd_end) -- the
+        next block, once wait_ev has passed (one-rank lookahead)."""
         L, n = self.layout, self.n_pad
         k, wg, lc = g * L.D, L.width(g), L.local_col(g)
         m = n - k
         lib = _native.lib()
         _native.check(lib.gelim_dist_panel_factor(ptr(loc), loc.stride(0), n, k, lc, wg, lu._pivot_code(self.pivot),
                                                   ptr(self._ipiv), ptr(self._pairs), ptr(self._info), ptr(self._ws),
-                                                  leaf, stream_handle(self.device)), "dist_panel_factor")
+                                                  leaf, upd_end, wait_ev.cuda_event if wait_ev is not None else None,
+                                                  stream_handle(self.device)), "dist_panel_factor")
         buf[:m * wg].view(m, wg).copy_(loc[k:, lc:lc + wg])
         nl = wg // LEAF
         buf[m * wg:m * wg + self._npd].view(torch.int32)[:nl * self._slot].copy_(self._pairs[:nl * self._slot])
@@ -348,10 +352,13 @@ class DistributedGauss:
     def _factor_lookahead(self, loc: torch.Tensor, G: int, fault_at_block: int | None) -> None:
         """Panels 0..G-1 with the two-stream lookahead schedule (module
         docstring); every column of this rank -- the tail's included --
-        receives every panel."""
+        receives every panel.  One rank: block g+1's update by panel g is
+        fused into panel g's leaves (plan.hip's form), so the next panel
+        factorisation starts the moment this one ends."""
         L, r, comm = self.layout, self.comm.rank, self.comm
         if G == 0:
             return
+        fuse = comm.world_size == 1
         end = self.nloc + 1  # local columns + b
         main = torch.cuda.current_stream(self.device)
         side = self._side
@@ -361,11 +368,15 @@ class DistributedGauss:
         ev_avail = [torch.cuda.Event() for _ in range(G)]
         ev_first = [torch.cuda.Event() for _ in range(G)]
         ev_rest = [torch.cuda.Event() for _ in range(G)]
+
+        def fused_end(g: int) -> int:  # update range of panel g's leaves (one rank): through block g+1
+            return L.local_col(g + 1) + L.width(g + 1) if fuse and g + 1 < L.nblocks else 0
+
         leaf = 0
         handles = {}
         o = L.owner(0)
         if r == o:
-            leaf = self._panel_factor(loc, 0, B[0], leaf)
+            leaf = self._panel_factor(loc, 0, B[0], leaf, fused_end(0))
         handles[0] = comm.broadcast_async(B[0][:self._bsize(0)], src=o)
         for g in range(G):
             maybe_inject_fault(g, r, fault_at_block)
@@ -375,29 +386,35 @@ class DistributedGauss:
             c0 = L.first_local_col_after(g, r)
             nxt = g + 1 < G
             o1 = L.owner(g + 1) if nxt else -1
+            # side first (its events must exist before main waits on them):
+            # panel g on the next block this rank factors after g+1, then on
+            # everything else; block g+1 is main's
+            cs = c0 + (L.width(g + 1) if (o1 == r or (fuse and g + 1 < L.nblocks)) else 0)
+            wf = L.width(self._block_at_local_col(cs)) if cs < self.nloc else 0
+            side.wait_event(ev_avail[g])
+            with torch.cuda.stream(side):
+                self._panel_apply(loc, g, buf, cs, cs + wf, side, self._cap)
+                ev_first[g].record(side)
+                self._panel_apply(loc, g, buf, cs + wf, end, side, self._cap)
+                ev_rest[g].record(side)
             if o1 == r:
-                # block g+1: its last update (panel g) on main, then its factorisation;
-                # panel g-1 reached it first on the side stream (ev_first[g-1])
-                w1 = L.width(g + 1)
-                if g >= 1:
-                    main.wait_event(ev_first[g - 1])
-                self._panel_apply(loc, g, buf, c0, c0 + w1)
+                if not fuse:
+                    # block g+1: its last update (panel g) on main, then its
+                    # factorisation; panel g-1 reached it first on the side
+                    # stream (ev_first[g-1])
+                    if g >= 1:
+                        main.wait_event(ev_first[g - 1])
+                    self._panel_apply(loc, g, buf, c0, c0 + L.width(g + 1))
                 if g + 1 >= nb:
                     main.wait_event(ev_rest[g + 1 - nb])  # its buffer slot is free again
-                leaf = self._panel_factor(loc, g + 1, B[(g + 1) % nb], leaf)
-                c0 += w1
+                # fused: panel g+1's leaves update block g+2 once panel g has
+                # reached it on the side stream (ev_first[g])
+                leaf = self._panel_factor(loc, g + 1, B[(g + 1) % nb], leaf, fused_end(g + 1),
+                                          ev_first[g] if fuse else None)
             if nxt:
                 if o1 != r and g + 1 >= nb:
                     main.wait_event(ev_rest[g + 1 - nb])
                 handles[g + 1] = comm.broadcast_async(B[(g + 1) % nb][:self._bsize(g + 1)], src=o1)
-            # side: the next block this rank factors first, then everything else
-            wf = L.width(self._block_at_local_col(c0)) if c0 < self.nloc else 0
-            side.wait_event(ev_avail[g])
-            with torch.cuda.stream(side):
-                self._panel_apply(loc, g, buf, c0, c0 + wf, side, self._cap)
-                ev_first[g].record(side)
-                self._panel_apply(loc, g, buf, c0 + wf, end, side, self._cap)
-                ev_rest[g].record(side)
         main.wait_event(ev_rest[G - 1])
 
     def _tail_solve(self, loc: torch.Tensor, G: int) -> None:
@@ -518,6 +535,9 @@ class DistributedGauss:
         L, P, D, r = self.layout, self.comm.world_size, self.layout.D, self.comm.rank
         n = L.n if ntop is None else ntop
         nblk = -(-n // D)
+        if P == 1:  # local columns are the global ones: one back substitution
+            yv = loc[:n, self.nloc] if y is None else y
+            return lu.backsub(loc[:n, :n], yv)
         S = P * D
         nsuper = math.ceil(n / S)
         # one all_gather of every super-block's diagonal columns

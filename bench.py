@@ -258,13 +258,18 @@ def main() -> None:
         _section(result, "dist_matmul_16384", lambda: bench_dist_matmul(comm, gelim, torch, 16384))
         # single-GPU large systems (each rank its own: weak)
         _section(result, "gauss_8192_1gpu", lambda: bench_single(comm, gelim, torch, 8192, seed=77 + rank))
+        # past the round-2 cap of 32768 rows per leaf (8.6 GB per system)
+        _section(result, "gauss_32768_1gpu", lambda: bench_single(comm, gelim, torch, 32768, seed=78 + rank, reps=1))
         _section(result, "hip_pivot_2048", lambda: bench_pivot(comm, gelim, torch, n))
         _section(result, "external_matrices", lambda: bench_external(comm, gelim, torch))
     for key, short in (("dist_gauss_8192", "dist_gauss_8192_s"), ("dist_matmul_16384", "dist_matmul_16384_s"),
-                       ("gauss_8192_1gpu", "gauss_8192_1gpu_s")):
+                       ("gauss_8192_1gpu", "gauss_8192_1gpu_s"), ("gauss_32768_1gpu", "gauss_32768_1gpu_s")):
         v = result.get(key)
         if isinstance(v, dict) and "time_s" in v:
             result[short] = v["time_s"]
+    dm = result.get("dist_matmul_16384")
+    if isinstance(dm, dict) and "summa" in dm:
+        result["dist_matmul_16384_summa_s"] = dm["summa"]["time_s"]
 
     # -- speedup vs the reference's sequential loops --------------------------
     seq = None
@@ -339,10 +344,19 @@ def bench_dist_gauss(comm, gelim, torch, n: int) -> dict:
 
 
 def bench_dist_matmul(comm, gelim, torch, n: int) -> dict:
-    """16384^2 fp32 matmul over ALL ranks (strong): A/C row blocks, B
-    gathered in column chunks (all_gather_into_tensor) under the MFMA GEMM;
-    the single-link ring timed alongside when there is more than one rank."""
+    """16384^2 fp32 matmul over ALL ranks (strong scaling), three
+    decompositions timed side by side:
+      allgather  A/C row blocks, B gathered in column chunks
+                 (all_gather_into_tensor) under the MFMA GEMM, the own k-block
+                 under the first gather (the default, `time_s`);
+      summa      2-D pr x pc block decomposition (BASELINE.json config 5):
+                 row / column sub-communicator broadcasts of A and B k-panels,
+                 double-buffered and asynchronous under the GEMM of the
+                 previous panel;
+      ring       B blocks passed around a ring of batched isend/irecv
+                 (more than one rank)."""
     from gelim.parallel import allgather_matmul, ring_matmul
+    from gelim.parallel.dist_matmul import default_chunks, grid_shape, make_summa_groups, summa_matmul
 
     dev, P, r = comm.device, comm.world_size, comm.rank
     g = torch.Generator(device=dev).manual_seed(1 + r)
@@ -355,13 +369,22 @@ def bench_dist_matmul(comm, gelim, torch, n: int) -> dict:
         fn(comm, Aloc, Bloc)
         dt = _timed(comm, torch, dev, lambda: fn(comm, Aloc, Bloc), reps=2)
         out[name] = {"time_s": dt, "tflops_total": 2 * n ** 3 / dt * 1e-12}
+    out["allgather"]["chunks"] = default_chunks(P)
+    del Aloc, Bloc
+    pr, pc = grid_shape(P)
+    Ablk = torch.randn(n // pr, n // pc, generator=g, device=dev)
+    Bblk = torch.randn(n // pr, n // pc, generator=g, device=dev)
+    groups = make_summa_groups(comm, pr, pc)
+    summa_matmul(comm, Ablk, Bblk, (pr, pc), groups=groups)
+    dt = _timed(comm, torch, dev, lambda: summa_matmul(comm, Ablk, Bblk, (pr, pc), groups=groups), reps=2)
+    out["summa"] = {"time_s": dt, "tflops_total": 2 * n ** 3 / dt * 1e-12, "grid": f"{pr}x{pc}"}
     out["time_s"] = out["allgather"]["time_s"]
     out["algo"] = "allgather (chunked all_gather_into_tensor of B overlapped with the MFMA GEMM)"
     out["ranks"] = P
     return out
 
 
-def bench_single(comm, gelim, torch, n: int, seed: int) -> dict:
+def bench_single(comm, gelim, torch, n: int, seed: int, reps: int = 3) -> dict:
     """One n^2 system per GPU on the single-GPU solver (n > 2048: wide-panel
     leaves + fp64 MFMA GEMM + the 2048 engine on the tail)."""
     dev = comm.device
@@ -369,7 +392,7 @@ def bench_single(comm, gelim, torch, n: int, seed: int) -> dict:
     s = gelim.GaussSolver(n, backend="hip", device=dev)
     holder = {}
     s.solve(aug)
-    dt = _timed(comm, torch, dev, lambda: holder.__setitem__("x", s.solve(aug)), reps=3)
+    dt = _timed(comm, torch, dev, lambda: holder.__setitem__("x", s.solve(aug)), reps=reps)
     res = {"time_s": dt, "tflops": (2.0 / 3.0) * n ** 3 / dt * 1e-12,
            "error": gelim.ops.gauss.error_metric(holder["x"]), "singular": s.info() != 0}
     s.close()

@@ -159,6 +159,8 @@ class Communicator:
     def subgroup(self, ranks: list[int]) -> "Communicator":
         """Communicator over a subset of ranks (SUMMA rows/columns).  Must be
         called by every rank with the same list (torch requirement)."""
+        if not self.distributed:  # one rank: the only subgroup is itself
+            return Communicator(0, 1, self.device, self.backend, None)
         g = dist.new_group(ranks=ranks, backend=self.backend if self.backend != "none" else None)
         if self.rank not in ranks:
             return Communicator(0, 1, self.device, self.backend, None)

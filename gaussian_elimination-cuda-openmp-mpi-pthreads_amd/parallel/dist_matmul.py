@@ -7,8 +7,10 @@ allgather_matmul (1-D, default)
   A and C row-partitioned, B row-partitioned into P k-blocks.  B is gathered
   in column chunks with all_gather_into_tensor -- one RCCL collective per
   chunk, which spreads over every xGMI link of the node (the ring below
-  drives ONE neighbour link per step) -- and chunk c+1's gather runs on the
-  RCCL stream while the MFMA GEMM computes C[:, chunk c] = A_loc @ B[:, c].
+  drives ONE neighbour link per step).  The rank's own k-block needs no
+  communication, so C = A_loc[:, own] @ B_loc runs first, under the first
+  chunk's gather; then chunk c+1's gather runs on the RCCL stream while the
+  MFMA GEMM adds the other ranks' k-blocks of chunk c.
 
 ring_matmul (1-D)
   A and C row-partitioned, B row-partitioned into P k-blocks.  P steps: each
@@ -19,10 +21,12 @@ ring_matmul (1-D)
   Per step each GPU sends/receives one K/P x N block over one xGMI link.
 
 summa_matmul (2-D, pr x pc grid)
-  A (M/pr x K/pc) and B (K/pr x N/pc) blocks; for each of lcm(pr,pc)
-  k-panels the owning column broadcasts its A panel along the process row
-  and the owning row its B panel along the process column, then every rank
-  accumulates its C block.  Uses row/column sub-communicators.
+  A (M/pr x K/pc) and B (K/pr x N/pc) blocks; for each k-panel (a multiple
+  of lcm(pr, pc) of them) the owning column broadcasts its A panel along the
+  process row and the owning row its B panel along the process column, then
+  every rank accumulates its C block.  Row/column sub-communicators; the
+  broadcasts are asynchronous into double buffers, so panel l+1 travels
+  while panel l multiplies.
 
 Compute runs on the native kernels (`gelim_gpu_matmul_f32_ex`, accumulate
 mode); on CPU ranks (gloo tests) the accumulate is torch.addmm.
@@ -82,12 +86,19 @@ def ring_matmul(comm: Communicator, A_loc: torch.Tensor, B_loc: torch.Tensor, ke
     return C
 
 
-def allgather_matmul(comm: Communicator, A_loc: torch.Tensor, B_loc: torch.Tensor, chunks: int = 4,
+def default_chunks(P: int) -> int:
+    """Column chunks of the allgather: enough to hide each gather under the
+    previous chunk's GEMM, few enough that each GEMM still fills the GPU."""
+    return 2 if P <= 2 else 4
+
+
+def allgather_matmul(comm: Communicator, A_loc: torch.Tensor, B_loc: torch.Tensor, chunks: int | None = None,
                      kernel: str = "mfma") -> torch.Tensor:
     """A_loc: (M/P, K) rows of A; B_loc: (K/P, N) rows of B (equal blocks,
     rank order).  Returns C_loc = A_loc @ B (M/P, N).  B travels as `chunks`
-    column chunks, each gathered (async) while the previous one multiplies."""
-    P = comm.world_size
+    column chunks, each gathered (async) while the previous one multiplies;
+    the rank's own k-block multiplies under the first gather."""
+    P, r = comm.world_size, comm.rank
     kb, N = B_loc.shape
     if A_loc.shape[1] != kb * P:
         raise ValueError("allgather_matmul needs K divisible by the world size")
@@ -95,7 +106,7 @@ def allgather_matmul(comm: Communicator, A_loc: torch.Tensor, B_loc: torch.Tenso
     if P == 1:
         matmul_acc_(C, A_loc, B_loc, accumulate=False, kernel=kernel)
         return C
-    chunks = max(1, min(chunks, N))
+    chunks = max(1, min(chunks or default_chunks(P), N))
     bounds = [N * c // chunks for c in range(chunks + 1)]
     wmax = max(bounds[c + 1] - bounds[c] for c in range(chunks))
     send = [torch.empty((kb, wmax), dtype=torch.float32, device=A_loc.device) for _ in range(2)]
@@ -109,12 +120,18 @@ def allgather_matmul(comm: Communicator, A_loc: torch.Tensor, B_loc: torch.Tenso
         return comm.all_gather_async(out, snd.contiguous()), out.view(P * kb, w)
 
     pending = post(0)
+    # own k-block: no communication needed, runs under the first gather
+    matmul_acc_(C, A_loc[:, r * kb:(r + 1) * kb], B_loc, accumulate=False, kernel=kernel)
     for c in range(chunks):
         h, Bc = pending
         h.wait()
         if c + 1 < chunks:
             pending = post(c + 1)  # on the RCCL stream while chunk c multiplies
-        matmul_acc_(C[:, bounds[c]:bounds[c + 1]], A_loc, Bc, accumulate=False, kernel=kernel)
+        Cc = C[:, bounds[c]:bounds[c + 1]]
+        if r > 0:
+            matmul_acc_(Cc, A_loc[:, :r * kb], Bc[:r * kb], accumulate=True, kernel=kernel)
+        if r < P - 1:
+            matmul_acc_(Cc, A_loc[:, (r + 1) * kb:], Bc[(r + 1) * kb:], accumulate=True, kernel=kernel)
     return C
 
 
@@ -127,9 +144,11 @@ def grid_shape(P: int) -> tuple[int, int]:
 
 
 def summa_matmul(comm: Communicator, A_blk: torch.Tensor, B_blk: torch.Tensor, grid: tuple[int, int] | None = None,
-                 kernel: str = "mfma", groups: tuple | None = None) -> torch.Tensor:
+                 kernel: str = "mfma", groups: tuple | None = None, panels: int | None = None) -> torch.Tensor:
     """A_blk: block (i, j) of A (M/pr x K/pc); B_blk: block (i, j) of B
-    (K/pr x N/pc); rank = i*pc + j.  Returns C block (i, j)."""
+    (K/pr x N/pc); rank = i*pc + j.  Returns C block (i, j).  panels: number
+    of k-panels (a multiple of lcm(pr, pc) dividing K; default: lcm(pr, pc)
+    split further until a panel is <= 1024 deep, for overlap)."""
     P, r = comm.world_size, comm.rank
     pr, pc = grid or grid_shape(P)
     if pr * pc != P:
@@ -141,22 +160,42 @@ def summa_matmul(comm: Communicator, A_blk: torch.Tensor, B_blk: torch.Tensor, g
     K = ka * pc
     if kb_rows * pr != K:
         raise ValueError("inconsistent K split")
-    Lp = pr * pc // math.gcd(pr, pc)  # number of k-panels
+    base = pr * pc // math.gcd(pr, pc)
+    if panels is None:
+        panels = base
+        while K // panels > 1024 and K % (panels * 2) == 0:
+            panels *= 2
+    if panels % base or K % panels:
+        raise ValueError(f"panels must be a multiple of {base} dividing K={K}")
+    Lp = panels
     kp = K // Lp
-    C = torch.empty((mb, nb), dtype=torch.float32, device=A_blk.device)
-    a_pan = torch.empty((mb, kp), dtype=torch.float32, device=A_blk.device)
-    b_pan = torch.empty((kp, nb), dtype=torch.float32, device=A_blk.device)
-    for l in range(Lp):
+    dev = A_blk.device
+    C = torch.empty((mb, nb), dtype=torch.float32, device=dev)
+    a_pan = [torch.empty((mb, kp), dtype=torch.float32, device=dev) for _ in range(2)]
+    b_pan = [torch.empty((kp, nb), dtype=torch.float32, device=dev) for _ in range(2)]
+
+    def post(l: int):
+        """Panel l into buffer l % 2: copies and broadcasts enqueued after the
+        GEMM of panel l-2 (stream order), so its buffer is free."""
         k0 = l * kp
         ja, off_a = divmod(k0, ka)  # process column owning this A panel
         ib, off_b = divmod(k0, kb_rows)  # process row owning this B panel
         if j == ja:
-            a_pan.copy_(A_blk[:, off_a:off_a + kp])
-        row_comm.broadcast(a_pan, src=ja)
+            a_pan[l % 2].copy_(A_blk[:, off_a:off_a + kp])
+        ha = row_comm.broadcast_async(a_pan[l % 2], src=ja)
         if i == ib:
-            b_pan.copy_(B_blk[off_b:off_b + kp, :])
-        col_comm.broadcast(b_pan, src=ib)
-        matmul_acc_(C, a_pan, b_pan, accumulate=l > 0, kernel=kernel)
+            b_pan[l % 2].copy_(B_blk[off_b:off_b + kp, :])
+        hb = col_comm.broadcast_async(b_pan[l % 2], src=ib)
+        return ha, hb
+
+    pending = post(0)
+    for l in range(Lp):
+        ha, hb = pending
+        ha.wait()
+        hb.wait()
+        if l + 1 < Lp:
+            pending = post(l + 1)  # travels while panel l multiplies
+        matmul_acc_(C, a_pan[l % 2], b_pan[l % 2], accumulate=l > 0, kernel=kernel)
     return C
 
 

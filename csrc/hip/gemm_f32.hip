@@ -35,6 +35,7 @@ struct Mat {
   float* C;
   int64_t ldc;
   int M, N, K, acc;
+  float alpha;  // MFMA path: C (+)= alpha * A B (the blocked no-pivot LU's update passes -1)
 };
 
 __global__ void naive_row_kernel(Mat p) {
@@ -219,7 +220,8 @@ __global__ __launch_bounds__(kMmThreads, 2) void mfma_gemm_kernel(Mat p, int til
         const int row = m0 + wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * kh;
         if (!CHECK || (row < M && col < N)) {
           float* c = p.C + (int64_t)row * p.ldc + col;
-          *c = p.acc ? *c + acc[i][j][r] : acc[i][j][r];
+          const float v = p.alpha * acc[i][j][r];
+          *c = p.acc ? *c + v : v;
         }
       }
     }
@@ -233,12 +235,13 @@ struct Shape {
 }  // namespace
 
 int matmul_f32(const float* A, int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc,
-               int64_t M, int64_t N, int64_t K, int accumulate, int kernel, hipStream_t s) {
+               int64_t M, int64_t N, int64_t K, int accumulate, int kernel, hipStream_t s, float alpha) {
   if (M <= 0 || N <= 0 || K <= 0) return GELIM_FAIL(GELIM_E_ARG, "matmul: bad shape");
+  if (alpha != 1.0f && kernel != GELIM_MM_MFMA) return GELIM_FAIL(GELIM_E_ARG, "matmul: alpha needs the MFMA kernel");
   if (M > INT32_MAX || N > INT32_MAX || K > INT32_MAX)
     return GELIM_FAIL(GELIM_E_ARG, "matmul: dimension exceeds 2^31");
   if (lda < K || ldb < N || ldc < N) return GELIM_FAIL(GELIM_E_ARG, "matmul: leading dimension too small");
-  Mat p{A, lda, B, ldb, C, ldc, (int)M, (int)N, (int)K, accumulate};
+  Mat p{A, lda, B, ldb, C, ldc, (int)M, (int)N, (int)K, accumulate, alpha};
   switch (kernel) {
     case GELIM_MM_NAIVE_ROW: {
       const int threads = (int)std::min<int64_t>(1024, N);
@@ -299,12 +302,12 @@ int matmul_f32(const float* A, int64_t lda, const float* B, int64_t ldb, float* 
 
 extern "C" int gelim_gpu_matmul_f32(const float* dA, const float* dB, float* dC, int64_t M,
                                     int64_t N, int64_t K, int kernel, void* stream) {
-  return gelim::matmul_f32(dA, K, dB, N, dC, N, M, N, K, 0, kernel, (hipStream_t)stream);
+  return gelim::matmul_f32(dA, K, dB, N, dC, N, M, N, K, 0, kernel, (hipStream_t)stream, 1.0f);
 }
 
 extern "C" int gelim_gpu_matmul_f32_ex(const float* dA, int64_t lda, const float* dB, int64_t ldb,
                                        float* dC, int64_t ldc, int64_t M, int64_t N, int64_t K,
                                        int accumulate, int kernel, void* stream) {
   return gelim::matmul_f32(dA, lda, dB, ldb, dC, ldc, M, N, K, accumulate, kernel,
-                           (hipStream_t)stream);
+                           (hipStream_t)stream, 1.0f);
 }

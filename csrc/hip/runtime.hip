@@ -19,9 +19,11 @@ __global__ __launch_bounds__(256) void copy2d_words_kernel(unsigned* __restrict_
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < w; i += (int64_t)gridDim.x * 256) drow[i] = srow[i];
 }
 
-// r[i] = aug[i][n] - sum_j aug[i][j] x[j] (fp64; one wave per row)
+// r[i] = aug[i][n] - sum_j aug[i][j] x[j] (fp64; one wave per row); with
+// matvec set, r[i] = sum_j aug[i][j] x[j] (the GMRES products of the mixed engine)
 __global__ __launch_bounds__(256) void residual_kernel(const double* __restrict__ aug, int64_t ld, int n,
-                                                       const double* __restrict__ x, double* __restrict__ r) {
+                                                       const double* __restrict__ x, double* __restrict__ r,
+                                                       int matvec) {
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= n) return;
@@ -29,7 +31,10 @@ __global__ __launch_bounds__(256) void residual_kernel(const double* __restrict_
   double s = 0.0;
   for (int j = lane; j < n; j += 64) s = fma(a[j], x[j], s);
   s = dev::wave_sum(s);
-  if (lane == 0) r[row] = a[n] - s;
+  if (lane == 0) {
+    if (matvec) r[row] = s;
+    else r[row] = a[n] - s;
+  }
 }
 
 __global__ __launch_bounds__(256) void zero_words_kernel(unsigned* __restrict__ p, int64_t nwords) {
@@ -110,8 +115,8 @@ int copy2d_async(void* dst, size_t dpitch, const void* src, size_t spitch, size_
   return GELIM_OK;
 }
 
-int residual_f64(const double* aug, int64_t ld, int64_t n, const double* x, double* r, hipStream_t s) {
-  hipLaunchKernelGGL(residual_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, s, aug, ld, (int)n, x, r);
+int residual_f64(const double* aug, int64_t ld, int64_t n, const double* x, double* r, hipStream_t s, int matvec) {
+  hipLaunchKernelGGL(residual_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, s, aug, ld, (int)n, x, r, matvec);
   HIP_TRY(hipGetLastError());
   return GELIM_OK;
 }
@@ -248,5 +253,11 @@ extern "C" int gelim_gpu_error_metric(const double* dx, int64_t n, double* d_err
 extern "C" int gelim_gpu_residual(const double* daug, int64_t ld, int64_t n, const double* dx, double* dr,
                                   void* stream) {
   if (n <= 0 || ld < n + 1) return GELIM_FAIL(GELIM_E_ARG, "residual: bad n / ld");
-  return gelim::residual_f64(daug, ld, n, dx, dr, (hipStream_t)stream);
+  return gelim::residual_f64(daug, ld, n, dx, dr, (hipStream_t)stream, 0);
+}
+
+// y = A x for the n x n matrix of an augmented fp64 system.
+extern "C" int gelim_gpu_matvec(const double* daug, int64_t ld, int64_t n, const double* dx, double* dy, void* stream) {
+  if (n <= 0 || ld < n) return GELIM_FAIL(GELIM_E_ARG, "matvec: bad n / ld");
+  return gelim::residual_f64(daug, ld, n, dx, dy, (hipStream_t)stream, 1);
 }

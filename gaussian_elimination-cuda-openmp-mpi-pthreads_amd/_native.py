@@ -73,6 +73,13 @@ _PROTOS = {
     "gelim_gpu_leaf_factor_ws": (_int, [_vp, _i64, _i64, _i64, _int, _vp, _vp, _vp, _vp, _int, _vp]),
     "gelim_gpu_leaf_workspace_bytes": (_i64, []),
     "gelim_gpu_leaf_participants": (_i32, [_i64]),
+    "gelim_mixed_max_n": (_i64, []),
+    "gelim_gpu_matvec": (_int, [_vp, _i64, _i64, _vp, _vp, _vp]),
+    "gelim_mixed_padded": (_i64, [_i64]),
+    "gelim_mixed_plan_create": (_vp, [_i64, _vp, _vp]),
+    "gelim_mixed_plan_destroy": (None, [_vp]),
+    "gelim_mixed_factor": (_int, [_vp, _vp, _i64, _vp]),
+    "gelim_mixed_apply": (_int, [_vp, _vp, _i64, _vp, _vp]),
     "gelim_gpu_leaf_max_rows": (_i64, []),
     "gelim_debug_leaf_stamps": (_int, [_vp, _i64, _i64, _vp, _vp, _vp]),
     "gelim_gpu_laswp_trsm": (_int, [_vp, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _vp, _vp]),

@@ -8,6 +8,12 @@ Backends
                       the whole solve replayed from a captured hipGraph (fp64)
   hip-pivot         : the reference per-pivot algorithm on the GPU
                       (unit-diagonal elimination, fp64 or fp32)
+  hip-mixed         : random butterfly transform + NO-pivoting blocked LU in
+                      fp32 on the matrix cores + fp64 iterative refinement on
+                      the original system, falling back to `hip` (fp64,
+                      partial pivoting) whenever it does not reach the fp64
+                      error class (csrc/hip/lu_mixed.hip); also selected by
+                      backend="hip", dtype=torch.float32
   seq / omp / pthreads-v1 / pthreads-v2 / pthreads-v3 : the reference CPU
                       strategies (csrc/cpu/gauss_cpu.cpp), fp64
 
@@ -26,9 +32,10 @@ from ..ops import lu
 from ..utils.tensors import ptr, row_major_ld, stream_handle
 
 GPU_BACKENDS = {"hip": _native.GPU_BLOCKED, "hip-blocked": _native.GPU_BLOCKED, "hip-pivot": _native.GPU_PIVOT}
+MIXED_BACKEND = "hip-mixed"
 CPU_BACKENDS = tuple(cpu_ops.CPU_BACKENDS)
 RESOLVE_LDS_BYTES = 160 * 1024  # lower_resolve_kernel (csrc/hip/gauss_pivot.hip)
-BACKENDS = tuple(GPU_BACKENDS) + CPU_BACKENDS
+BACKENDS = tuple(GPU_BACKENDS) + (MIXED_BACKEND,) + CPU_BACKENDS
 
 
 class GaussSolver:
@@ -41,8 +48,17 @@ class GaussSolver:
         self.n, self.backend, self.pivot, self.dtype = n, backend, pivot, dtype
         self.threads, self.affinity = threads, affinity
         self._plan = None
-        self.gpu = backend in GPU_BACKENDS
-        if self.gpu:
+        self._mixed = None
+        self._fp64 = None
+        self.last_steps = 0
+        self.last_inner = 0
+        self.last_fallback = None
+        if backend in ("hip", "hip-blocked") and dtype == torch.float32:
+            backend = self.backend = MIXED_BACKEND
+        self.gpu = backend in GPU_BACKENDS or backend == MIXED_BACKEND
+        if backend == MIXED_BACKEND:
+            self._init_mixed(device, seed=0x5eed)
+        elif self.gpu:
             self.device = torch.device(device if device is not None else "cuda")
             if dtype == torch.float32 and backend != "hip-pivot":
                 raise ValueError("fp32 elimination is only offered by hip-pivot (fp64 is required for "
@@ -58,6 +74,145 @@ class GaussSolver:
             if dtype != torch.float64:
                 raise ValueError("CPU backends are fp64 (reference precision)")
             self.device = torch.device("cpu")
+
+    # -- mixed precision (RBT + fp32 no-pivot LU + fp64 refinement) -----------
+    def _init_mixed(self, device, seed: int) -> None:
+        import numpy as np
+
+        self.device = torch.device(device if device is not None else "cuda")
+        self.dtype = torch.float32  # the factorisation's precision; x is fp64
+        lib = _native.lib()
+        n = self.n
+        npad = int(lib.gelim_mixed_padded(n))
+        if npad > int(lib.gelim_mixed_max_n()):
+            self._mixed_unavailable = f"n = {n} beyond the mixed engine's {int(lib.gelim_mixed_max_n())}"
+            return
+        self._mixed_unavailable = None
+        rng = np.random.default_rng(seed)
+        # butterfly diagonals exp(r / 10), r uniform in [-1/2, 1/2] (8 arrays of npad/4 each, for U and V)
+        self._ud = np.exp((rng.random(2 * npad) - 0.5) / 10.0)
+        self._vd = np.exp((rng.random(2 * npad) - 0.5) / 10.0)
+        with torch.cuda.device(self.device):
+            plan = lib.gelim_mixed_plan_create(n, self._ud.ctypes.data, self._vd.ctypes.data)
+        if not plan:
+            raise _native.GelimError(_native.E_ARG, _native.last_error())
+        self._mixed = plan
+
+    def _fallback(self, aug64: torch.Tensor, reason: str, check: bool) -> torch.Tensor:
+        self.last_fallback = reason
+        if self._fp64 is None:
+            self._fp64 = GaussSolver(self.n, backend="hip", pivot=self.pivot, device=self.device)
+        return self._fp64.solve(aug64, check=check)
+
+    def _gmres(self, aug64: torch.Tensor, r: torch.Tensor, restart: int = 30, tol: float = 1e-6) -> torch.Tensor:
+        """d ~ A^-1 r by left-preconditioned GMRES in fp64 (Carson-Higham
+        GMRES-IR): M^-1 = V (LU)^-1 U^T from the fp32 factors, A v on the
+        fp64 system (native mat-vec), classical Gram-Schmidt with one
+        re-orthogonalisation, Givens rotations on the host.  Stops when the
+        preconditioned residual has dropped by `tol` or after `restart`
+        iterations."""
+        import numpy as np
+
+        n, dev = self.n, self.device
+        lib = _native.lib()
+        sh = stream_handle(dev)
+        ld = aug64.stride(0)
+        Vb = torch.empty((restart + 1, n), dtype=torch.float64, device=dev)
+        w = torch.empty(n, dtype=torch.float64, device=dev)
+        z = torch.empty(n, dtype=torch.float64, device=dev)
+        _native.check(lib.gelim_mixed_apply(self._mixed, ptr(r), 1, ptr(z), sh), "mixed_apply")
+        beta = float(z.norm())
+        if not beta > 0.0 or beta != beta:
+            return torch.zeros(n, dtype=torch.float64, device=dev)
+        Vb[0] = z / beta
+        H = np.zeros((restart + 1, restart))
+        cs, sn = np.zeros(restart), np.zeros(restart)
+        g = np.zeros(restart + 1)
+        g[0] = beta
+        k = 0
+        for j in range(restart):
+            _native.check(lib.gelim_gpu_matvec(ptr(aug64), ld, n, ptr(Vb[j]), ptr(w), sh), "matvec")
+            _native.check(lib.gelim_mixed_apply(self._mixed, ptr(w), 1, ptr(z), sh), "mixed_apply")
+            B = Vb[:j + 1]
+            h = B @ z
+            z -= B.T @ h
+            h2 = B @ z
+            z -= B.T @ h2
+            h += h2
+            hv = torch.cat([h, z.norm().reshape(1)]).cpu().numpy()
+            H[:j + 2, j] = hv
+            self.last_inner += 1
+            k = j + 1
+            if not hv[-1] > 0.0:  # breakdown: the Krylov space holds the solution
+                for i in range(j):
+                    a, b = H[i, j], H[i + 1, j]
+                    H[i, j], H[i + 1, j] = cs[i] * a + sn[i] * b, -sn[i] * a + cs[i] * b
+                break
+            Vb[j + 1] = z / hv[-1]
+            for i in range(j):  # previous rotations on the new column
+                a, b = H[i, j], H[i + 1, j]
+                H[i, j], H[i + 1, j] = cs[i] * a + sn[i] * b, -sn[i] * a + cs[i] * b
+            den = float(np.hypot(H[j, j], H[j + 1, j]))
+            cs[j], sn[j] = H[j, j] / den, H[j + 1, j] / den
+            H[j, j], H[j + 1, j] = den, 0.0
+            g[j + 1] = -sn[j] * g[j]
+            g[j] = cs[j] * g[j]
+            if abs(g[j + 1]) <= tol * beta:
+                break
+        y = np.zeros(k)
+        for i in reversed(range(k)):  # H[:k, :k] upper triangular now
+            y[i] = (g[i] - H[i, i + 1:k] @ y[i + 1:k]) / H[i, i]
+        return Vb[:k].T @ torch.from_numpy(y).to(dev)
+
+    def _solve_mixed(self, aug: torch.Tensor, max_steps: int = 6, check: bool = False) -> torch.Tensor:
+        """x of the augmented system: RBT + fp32 LU, then x <- x + d with d
+        from GMRES preconditioned by the fp32 factors (fp64 residual on the
+        ORIGINAL system, Carson-Higham GMRES-IR) until ||r|| <= sqrt(n)
+        eps64 ||A|| ||x|| (LAPACK dsgesv's test), at most max_steps outer
+        corrections; a stall, a zero pivot or too many steps hand the system
+        to the fp64 partial-pivoting engine (last_fallback says why;
+        last_steps counts outer corrections, last_inner GMRES iterations)."""
+        import math
+
+        n, dev = self.n, self.device
+        lib = _native.lib()
+        aug64 = aug.to(dev, torch.float64)
+        if aug64.shape[0] != n or aug64.shape[1] < n + 1 or aug64.stride(1) != 1:
+            aug64 = aug64[:, :n + 1].contiguous()
+        self.last_steps, self.last_inner, self.last_fallback = 0, 0, None
+        if self._mixed is None:
+            return self._fallback(aug64, self._mixed_unavailable or "no mixed plan", check)
+        ld = aug64.stride(0)
+        sh = stream_handle(dev)
+        rc = lib.gelim_mixed_factor(self._mixed, ptr(aug64), ld, sh)
+        _native.check(rc, "mixed_factor")
+        if rc > 0:
+            return self._fallback(aug64, f"no-pivot LU: zero or non-finite pivot at column {rc - 1}", check)
+        b = aug64[:, n]
+        x = torch.empty(n, dtype=torch.float64, device=dev)
+        _native.check(lib.gelim_mixed_apply(self._mixed, ptr(b), ld, ptr(x), sh), "mixed_apply")
+        # backward-error targets: 4 eps ||A|| ||x|| (keep refining), the dsgesv
+        # bound sqrt(n) eps ||A|| ||x|| (accepted once refinement stagnates)
+        anorm_eps = float(aug64[:, :n].abs().sum(1).max()) * torch.finfo(torch.float64).eps
+        strict, loose = 4.0 * anorm_eps, math.sqrt(n) * anorm_eps
+        r = torch.empty(n, dtype=torch.float64, device=dev)
+        prev, best = math.inf, None
+        for it in range(max_steps + 1):
+            _native.check(lib.gelim_gpu_residual(ptr(aug64), ld, n, ptr(x), ptr(r), sh), "residual")
+            rn, xn = torch.stack([r.abs().max(), x.abs().max()]).tolist()
+            self.last_steps = it
+            if rn <= xn * strict:
+                return x
+            if not rn < prev or it == max_steps:  # NaN, stagnated or out of steps
+                if best is not None and best[0] <= best[1] * loose:
+                    return best[2]
+                if rn <= xn * loose:
+                    return x
+                return self._fallback(aug64, f"refinement stalled after {it} corrections "
+                                             f"(||r|| = {rn:.3e} > {xn * loose:.3e})", check)
+            prev, best = rn, (rn, xn, x.clone())
+            x += self._gmres(aug64, r)
+        raise AssertionError("unreachable")
 
     # -- GPU ---------------------------------------------------------------
     def _solve_gpu(self, aug: torch.Tensor, want_bnorm: bool):
@@ -75,6 +230,8 @@ class GaussSolver:
 
     def info(self) -> int:
         """0 if the last solve was non-singular, else 1 + first zero-pivot column."""
+        if self.backend == MIXED_BACKEND:
+            return self._fp64.info() if (self.last_fallback and self._fp64 is not None) else 0
         if not self.gpu:
             return 0
         return _native.check(_native.lib().gelim_gauss_plan_info(self._plan, stream_handle(self.device)),
@@ -93,6 +250,10 @@ class GaussSolver:
         """Solve the augmented system; returns x (and the reference's
         transformed b when return_bnorm).  check=True synchronises and raises
         SingularMatrixError on a zero pivot."""
+        if self.backend == MIXED_BACKEND:
+            if return_bnorm:
+                raise ValueError("hip-mixed solves a transformed system: no reference-style B")
+            return self._solve_mixed(aug, check=check)
         if self.gpu:
             x, bn = self._solve_gpu(aug, return_bnorm)
             if check and self.info() != 0:
@@ -137,6 +298,9 @@ class GaussSolver:
         the path that lets the fp32 elimination reach fp64-level error on
         the `.dat` matrices.
         """
+        if self.backend == MIXED_BACKEND:
+            x = self._solve_mixed(aug, max_steps=max(max_steps, 1), check=check)
+            return x, self.last_steps
         n = self.n
         dev = self.device
         aug64 = aug[:, :n + 1].to(dev, torch.float64).contiguous()
@@ -181,6 +345,12 @@ class GaussSolver:
         if self._plan:
             _native.lib().gelim_gauss_plan_destroy(self._plan)
             self._plan = None
+        if self._mixed:
+            _native.lib().gelim_mixed_plan_destroy(self._mixed)
+            self._mixed = None
+        if self._fp64 is not None:
+            self._fp64.close()
+            self._fp64 = None
 
     def __del__(self):
         # never tear down HIP objects during interpreter shutdown (the HIP

@@ -158,8 +158,21 @@ __global__ __launch_bounds__(1024) void diag_lu_kernel(float* __restrict__ A, in
     if (row > k) {
       const float p = S[k * kLdsLd + k];
       const float l = S[row * kLdsLd + k] / p;
-      for (int j = k + 1 + c8; j < NB; j += 8) S[row * kLdsLd + j] = fmaf(-l, S[k * kLdsLd + j], S[row * kLdsLd + j]);
-      if (c8 == 0) S[row * kLdsLd + k] = l;
+      // the row's 16 columns as one batch of independent LDS reads / FMAs /
+      // writes (a static loop, predicated on j > k), not a dependent chain
+      float v[NB / 8], u[NB / 8];
+#pragma unroll
+      for (int q = 0; q < NB / 8; ++q) {
+        const int j = c8 + 8 * q;
+        v[q] = S[row * kLdsLd + j];
+        u[q] = S[k * kLdsLd + j];
+      }
+#pragma unroll
+      for (int q = 0; q < NB / 8; ++q) {
+        const int j = c8 + 8 * q;
+        if (j > k) S[row * kLdsLd + j] = fmaf(-l, u[q], v[q]);
+      }
+      if (c8 == (k & 7)) S[row * kLdsLd + k] = l;
     }
     __syncthreads();
   }
@@ -187,7 +200,20 @@ __device__ __forceinline__ void tile_lower_solve(float* __restrict__ X, const fl
   const int t = threadIdx.x, c = t & 63, rg = t >> 6;
   for (int k = 0; k < NB - 1; ++k) {
     const float xk = UNIT ? X[k * kXld + c] : X[k * kXld + c] * rinv[k];
-    for (int i = k + 1 + ((rg - k - 1) & 3); i < NB; i += 4) X[i * kXld + c] = fmaf(-L[i * kLld + k], xk, X[i * kXld + c]);
+    // this thread's 32 rows i = 4 q + rg as one batch (static loop, predicated
+    // on i > k): independent LDS reads, FMAs and writes, pipelined
+    float v[NB / 4], l[NB / 4];
+#pragma unroll
+    for (int q = 0; q < NB / 4; ++q) {
+      const int i = 4 * q + rg;
+      v[q] = X[i * kXld + c];
+      l[q] = L[i * kLld + k];
+    }
+#pragma unroll
+    for (int q = 0; q < NB / 4; ++q) {
+      const int i = 4 * q + rg;
+      if (i > k) X[i * kXld + c] = fmaf(-l[q], xk, v[q]);
+    }
     __syncthreads();
   }
   if (!UNIT)

@@ -67,7 +67,8 @@ def test_mixed_falls_back_when_fp32_cannot_converge(gelim, cuda):
     x = s.solve(aug, check=True)
     assert s.last_fallback is not None
     ref = torch.linalg.solve(A, aug[:, n])
-    assert ((x - ref).abs().max() / ref.abs().max()).item() < 1e-6
+    # both are fp64 solves of a cond = 1e12 system: they agree to ~cond * eps64
+    assert ((x - ref).abs().max() / ref.abs().max()).item() < 1e-3
 
 
 def test_mixed_singular_raises(gelim, cuda):

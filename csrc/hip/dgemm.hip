@@ -30,6 +30,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <string>
 
 #include "device_common.h"
@@ -38,11 +39,23 @@
 namespace gelim {
 namespace {
 
-constexpr int BM = 128, BN = 128, BK = 16;
+constexpr int BM = 128, BN = 128, BK = 16;  // the default (large) tile
 constexpr int kThreads = 256;
-constexpr int SA = BM + 16, SB = BN + 16;   // LDS row strides (doubles)
-constexpr int WM = 64, WN = 64;             // per-wave tile
-constexpr int MB = WM / 16, NB = WN / 16;   // 16x16 blocks per wave
+constexpr int SA = BM + 16, SB = BN + 16;   // LDS row strides (doubles) of the large tile
+
+// Tile geometry: T x T workgroup tile (T = 128, or 64 for thin problems whose
+// 128-tiles would leave most CUs idle -- the in-panel K = 32 updates of the
+// wide-panel LU, e.g. 8192 x 224), 2 x 2 waves of (T/2) x (T/2).
+template <int T>
+struct Geo {
+  static_assert(T == 128 || T == 64, "tile: 128 or 64");
+  static constexpr int TM = T, TN = T;
+  static constexpr int SA = T + 16, SB = T + 16;
+  static constexpr int WM = T / 2, WN = T / 2;
+  static constexpr int MB = WM / 16, NB = WN / 16;
+  static constexpr int kCA = T * BK / 2 / kThreads, kCB = BK * T / 2 / kThreads;
+  static constexpr int kLds = 2 * BK * SA + 2 * BK * SB;
+};
 
 struct Args {
   double* C;
@@ -56,16 +69,16 @@ struct Args {
   double alpha;
 };
 
-// 16-byte chunks per thread per tile: A 128x16 -> 1024 chunks, B 16x128 -> 1024
-constexpr int kCA = BM * BK / 2 / kThreads, kCB = BK * BN / 2 / kThreads;
-
+// 16-byte chunks per thread per tile: A Tx16 -> T*8 chunks, B 16xT -> T*8
+template <int T>
 struct Stage {
-  double2 a[kCA];
-  double2 b[kCB];
+  double2 a[Geo<T>::kCA];
+  double2 b[Geo<T>::kCB];
 };
 
-template <bool FULL>
-__device__ __forceinline__ void load_stage(Stage& st, const Args& g, int m0, int n0, int k0, int t) {
+template <bool FULL, int T>
+__device__ __forceinline__ void load_stage(Stage<T>& st, const Args& g, int m0, int n0, int k0, int t) {
+  constexpr int kCA = Geo<T>::kCA, kCB = Geo<T>::kCB;
 #pragma unroll
   for (int h = 0; h < kCA; ++h) {
     const int idx = t + kThreads * h;
@@ -84,7 +97,7 @@ __device__ __forceinline__ void load_stage(Stage& st, const Args& g, int m0, int
 #pragma unroll
   for (int h = 0; h < kCB; ++h) {
     const int idx = t + kThreads * h;
-    const int kr = idx >> 6, nc = (idx & 63) * 2;  // 64 chunks per B row of the tile
+    const int kr = idx >> (T == 128 ? 6 : 5), nc = (idx & (T / 2 - 1)) * 2;  // T/2 chunks per B row of the tile
     if constexpr (FULL) {
       st.b[h] = *reinterpret_cast<const double2*>(g.B + (int64_t)(k0 + kr) * g.ldb + n0 + nc);
     } else {
@@ -98,27 +111,31 @@ __device__ __forceinline__ void load_stage(Stage& st, const Args& g, int m0, int
   }
 }
 
-__device__ __forceinline__ void store_stage(const Stage& st, double* As, double* Bs, double alpha, int t) {
+template <int T>
+__device__ __forceinline__ void store_stage(const Stage<T>& st, double* As, double* Bs, double alpha, int t) {
+  constexpr int kCA = Geo<T>::kCA, kCB = Geo<T>::kCB, SA_ = Geo<T>::SA, SB_ = Geo<T>::SB;
 #pragma unroll
   for (int h = 0; h < kCA; ++h) {
     const int idx = t + kThreads * h;
     const int row = idx >> 3, kc = (idx & 7) * 2;
-    As[kc * SA + row] = alpha * st.a[h].x;
-    As[(kc + 1) * SA + row] = alpha * st.a[h].y;
+    As[kc * SA_ + row] = alpha * st.a[h].x;
+    As[(kc + 1) * SA_ + row] = alpha * st.a[h].y;
   }
 #pragma unroll
   for (int h = 0; h < kCB; ++h) {
     const int idx = t + kThreads * h;
-    const int kr = idx >> 6, nc = (idx & 63) * 2;
-    *reinterpret_cast<double2*>(&Bs[kr * SB + nc]) = st.b[h];
+    const int kr = idx >> (T == 128 ? 6 : 5), nc = (idx & (T / 2 - 1)) * 2;
+    *reinterpret_cast<double2*>(&Bs[kr * SB_ + nc]) = st.b[h];
   }
 }
 
-// One 128 x 128 tile by the 256 threads t = 0..255 (4 waves) over the LDS
+// One T x T tile by the 256 threads t = 0..255 (4 waves) over the LDS
 // double buffer at lds.  store = false: computed, not written (a persistent
 // workgroup's idle half, which still has to meet every barrier).
-template <bool FULL>
+template <bool FULL, int T = 128>
 __device__ __forceinline__ void tile_body(const Args& g, int m0, int n0, double* lds, int t, bool store = true) {
+  using G = Geo<T>;
+  constexpr int SA = G::SA, SB = G::SB, WM = G::WM, WN = G::WN, MB = G::MB, NB = G::NB;
   double* As[2] = {lds, lds + BK * SA};
   double* Bs[2] = {lds + 2 * BK * SA, lds + 2 * BK * SA + BK * SB};
   const int lane = t & 63, wave = t >> 6;
@@ -139,14 +156,14 @@ __device__ __forceinline__ void tile_body(const Args& g, int m0, int n0, double*
       }
     }
 
-  Stage st;
-  load_stage<FULL>(st, g, m0, n0, 0, t);
-  store_stage(st, As[0], Bs[0], g.alpha, t);
+  Stage<T> st;
+  load_stage<FULL, T>(st, g, m0, n0, 0, t);
+  store_stage<T>(st, As[0], Bs[0], g.alpha, t);
   __syncthreads();
   const int nk = (g.K + BK - 1) / BK;
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
-    if (kt + 1 < nk) load_stage<FULL>(st, g, m0, n0, (kt + 1) * BK, t);
+    if (kt + 1 < nk) load_stage<FULL, T>(st, g, m0, n0, (kt + 1) * BK, t);
     const double* a_s = As[cur] + wm + r16;
     const double* b_s = Bs[cur] + wn + r16;
 #pragma unroll
@@ -163,7 +180,7 @@ __device__ __forceinline__ void tile_body(const Args& g, int m0, int n0, double*
         for (int j = 0; j < NB; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[i], bf[j], acc[i][j], 0, 0, 0);
     }
-    if (kt + 1 < nk) store_stage(st, As[cur ^ 1], Bs[cur ^ 1], g.alpha, t);
+    if (kt + 1 < nk) store_stage<T>(st, As[cur ^ 1], Bs[cur ^ 1], g.alpha, t);
     __syncthreads();
   }
 
@@ -180,18 +197,19 @@ __device__ __forceinline__ void tile_body(const Args& g, int m0, int n0, double*
     }
 }
 
+template <int T>
 __global__ __launch_bounds__(kThreads, 2) void dgemm_kernel(Args g) {
-  __shared__ __attribute__((aligned(16))) double lds[2 * BK * SA + 2 * BK * SB];
+  __shared__ __attribute__((aligned(16))) double lds[Geo<T>::kLds];
   // XCD-aware bijective remap: XCD x (blocks x, x+8, ...) gets a contiguous
   // run of tiles, so tiles sharing an A row panel share that XCD's L2
   const int orig = blockIdx.x;
   const int q = g.ntiles / 8, rem = g.ntiles % 8, xcd = orig % 8;
   const int tile = (xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q) + orig / 8;
-  const int m0 = (tile / g.tiles_n) * BM, n0 = (tile % g.tiles_n) * BN;
-  if (m0 + BM <= g.M && n0 + BN <= g.N && (g.K % BK) == 0)
-    tile_body<true>(g, m0, n0, lds, threadIdx.x);
+  const int m0 = (tile / g.tiles_n) * T, n0 = (tile % g.tiles_n) * T;
+  if (m0 + T <= g.M && n0 + T <= g.N && (g.K % BK) == 0)
+    tile_body<true, T>(g, m0, n0, lds, threadIdx.x);
   else
-    tile_body<false>(g, m0, n0, lds, threadIdx.x);
+    tile_body<false, T>(g, m0, n0, lds, threadIdx.x);
 }
 
 // Persistent form for a grid capped below the CU count (the lookahead side
@@ -223,9 +241,9 @@ __global__ __launch_bounds__(kPThreads, 1) void dgemm_persist_kernel(Args g) {
     int tt = t;
     asm volatile("" : "+v"(tt));
     if (m0 + BM <= g.M && n0 + BN <= g.N && (g.K % BK) == 0)
-      tile_body<true>(g, m0, n0, lds, tt, store);
+      tile_body<true, 128>(g, m0, n0, lds, tt, store);
     else
-      tile_body<false>(g, m0, n0, lds, tt, store);
+      tile_body<false, 128>(g, m0, n0, lds, tt, store);
     __syncthreads();  // the next pair's first stage overwrites this one's LDS
   }
 }
@@ -260,7 +278,28 @@ int dgemm_capped(double* C, int64_t ldc, const double* A, int64_t lda, const dou
     hipLaunchKernelGGL(dgemm_persist_kernel, dim3((unsigned)std::max(grid, 8)), dim3(kPThreads), 2 * kStageBytes, s,
                        g);
   } else {
-    hipLaunchKernelGGL(dgemm_kernel, dim3((unsigned)(tm * tn)), dim3(kThreads), 0, s, g);
+    // thin problems (fewer 128-tiles than twice the CU count, e.g. the
+    // in-panel K = 32 updates, 8192 x 224): 64-tiles, 4x the workgroups
+    static const int ncu = [] {
+      int dev = 0, cus = 256;
+      (void)hipGetDevice(&dev);
+      (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+      return cus;
+    }();
+    static const int force = [] {
+      const char* e = std::getenv("GELIM_DGEMM_TILE");
+      return e ? std::atoi(e) : 0;
+    }();
+    const bool small = force ? force == 64 : (int64_t)tm * tn < 2 * (int64_t)ncu;
+    if (small && cap == 0) {
+      const int tm6 = (int)((M + 63) / 64), tn6 = (int)((N + 63) / 64);
+      Args g6 = g;
+      g6.tiles_n = tn6;
+      g6.ntiles = tm6 * tn6;
+      hipLaunchKernelGGL(dgemm_kernel<64>, dim3((unsigned)(tm6 * tn6)), dim3(kThreads), 0, s, g6);
+    } else {
+      hipLaunchKernelGGL(dgemm_kernel<128>, dim3((unsigned)(tm * tn)), dim3(kThreads), 0, s, g);
+    }
   }
   HIP_TRY(hipGetLastError());
   return GELIM_OK;

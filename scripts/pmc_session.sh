@@ -17,7 +17,7 @@ PASSES=(
 )
 WORKLOADS=(
   "matmul|$ROOT/bin/hip_matmul 2048 --no-seq --no-omp"
-  "gauss|python3 $ROOT/bench.py --steps 2 --warmup 1 --no-matmul"
+  "gauss|python3 $ROOT/bench.py --steps 2 --warmup 1 --no-matmul --headline-only"
 )
 for wl in "${WORKLOADS[@]}"; do
   name="${wl%%|*}"

@@ -278,7 +278,7 @@ int dgemm_capped(double* C, int64_t ldc, const double* A, int64_t lda, const dou
     hipLaunchKernelGGL(dgemm_persist_kernel, dim3((unsigned)std::max(grid, 8)), dim3(kPThreads), 2 * kStageBytes, s,
                        g);
   } else {
-    // thin problems (fewer 128-tiles than twice the CU count, e.g. the
+    // thin problems (fewer 128-tiles than CUs, e.g. the
     // in-panel K = 32 updates, 8192 x 224): 64-tiles, 4x the workgroups
     static const int ncu = [] {
       int dev = 0, cus = 256;
@@ -290,7 +290,7 @@ int dgemm_capped(double* C, int64_t ldc, const double* A, int64_t lda, const dou
       const char* e = std::getenv("GELIM_DGEMM_TILE");
       return e ? std::atoi(e) : 0;
     }();
-    const bool small = force ? force == 64 : (int64_t)tm * tn < 2 * (int64_t)ncu;
+    const bool small = force ? force == 64 : (int64_t)tm * tn < (int64_t)ncu;
     if (small && cap == 0) {
       const int tm6 = (int)((M + 63) / 64), tn6 = (int)((N + 63) / 64);
       Args g6 = g;

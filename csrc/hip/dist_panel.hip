@@ -43,6 +43,11 @@ int panel_trsm(double* C, int64_t ldc, int64_t ncols, int64_t nb, const double* 
                int max_wg = 0);
 bool trsm_fused();
 int leaf_cus(int64_t m);
+int compose_pairs(int64_t n, int64_t c0, int nleaves, const int* pairs, int64_t slot, int* net, hipStream_t s);
+int laswp_net_max();
+int64_t compose_max_rows();
+int laswp_net(double* A, int64_t lda, const int* net, int64_t lbeg, int64_t lend, int64_t rbeg, int64_t rend,
+              hipStream_t s, int max_wg);
 }  // namespace big
 }  // namespace gelim
 
@@ -52,6 +57,34 @@ constexpr int64_t kSlot = 1 + 4 * 32 + 3;  // ints per leaf pair list (plan.hip'
 }  // namespace
 
 extern "C" int64_t gelim_dist_pair_slot(void) { return kSlot; }
+
+// Ints of a panel's composed row movement: [valid, count, (dst, src) x
+// laswp_net_max()] -- valid = 0 when the panel is too tall for the LDS row
+// map of the composition (the pair lists are replayed instead).
+extern "C" int64_t gelim_dist_net_ints(void) { return 2 + 2 * (int64_t)gelim::big::laswp_net_max(); }
+
+namespace {
+__global__ void set_word_kernel(int* p, int v) {
+  if (threadIdx.x == 0) *p = v;
+}
+}  // namespace
+
+// The panel's leaf pair lists (nleaves lists at pairs, kSlot ints apart)
+// composed into ONE permutation of <= 64 rows per leaf (net: see
+// gelim_dist_net_ints), or net[0] = 0 when the panel's m rows exceed the
+// composition's LDS map: then every apply replays the lists instead.
+// Returns 1 when composed, 0 when not (decided on the host from n - k and
+// nleaves, so callers know without a device read), < 0 on errors.
+extern "C" int gelim_dist_panel_compose(int64_t n, int64_t k, int nleaves, const int32_t* pairs, int32_t* net,
+                                        void* stream) {
+  using namespace gelim;
+  hipStream_t s = (hipStream_t)stream;
+  const bool ok = n - k <= big::compose_max_rows() && nleaves * 2 * kLW <= big::laswp_net_max();
+  if (ok) GELIM_TRY(big::compose_pairs(n, k, nleaves, pairs, kSlot, net + 1, s));
+  hipLaunchKernelGGL(set_word_kernel, dim3(1), dim3(64), 0, s, net, ok ? 1 : 0);
+  HIP_TRY(hipGetLastError());
+  return ok ? 1 : 0;
+}
 
 // Factor rows [k, n) x local columns [lc, lc + wg) of the slab A in place
 // (wg a multiple of 32).  Leaf l's pivots go to ipiv[k + 32 l + J] (global
@@ -90,19 +123,25 @@ extern "C" int gelim_dist_panel_factor(double* A, int64_t lda, int64_t n, int64_
 // Apply a factored panel (its rows [k, n) as a row-major (n - k) x wg block L
 // with leading dimension ldl, and its leaf pair lists) to local columns
 // [cb, ce) of the slab C: the leaves' row movement, U12 = L11^-1 A12 on rows
-// [k, k + wg), A22 -= L21 U12 on rows [k + wg, n).  max_wg > 0: every launch
-// on at most max_wg CUs (the lookahead side stream, which must leave the
-// leaves of the concurrent panel factorisation free CUs; plan.hip's cap).
+// [k, k + wg), A22 -= L21 U12 on rows [k + wg, n).  net (may be null): the
+// panel's composed movement (gelim_dist_panel_compose); when valid it is
+// applied as one gather/scatter instead of replaying the lists per column
+// (~90 us a call, round-3 trace).  max_wg > 0: every launch on at most
+// max_wg CUs (the lookahead side stream, which must leave the leaves of the
+// concurrent panel factorisation free CUs; plan.hip's cap).
 extern "C" int gelim_dist_panel_apply(double* C, int64_t ldc, int64_t n, int64_t k, int64_t cb, int64_t ce,
-                                      const double* L, int64_t ldl, int64_t wg, const int32_t* pairs, int max_wg,
-                                      void* stream) {
+                                      const double* L, int64_t ldl, int64_t wg, const int32_t* pairs,
+                                      const int32_t* net, int net_valid, int max_wg, void* stream) {
   using namespace gelim;
   hipStream_t s = (hipStream_t)stream;
   if (ce <= cb) return GELIM_OK;
   if (wg <= 0 || wg % kLW || n % kLW || k + wg > n || (cb & 1) || (ldc & 1) || (ldl & 1))
     return GELIM_FAIL(GELIM_E_ARG, "dist_panel_apply: widths must be multiples of 32 (even offsets)");
   const int nl = (int)(wg / kLW);
-  GELIM_TRY(big::laswp_panel(C, ldc, n, k, nl, pairs, kSlot, 0, 0, cb, ce, s, max_wg));
+  if (net != nullptr && net_valid)
+    GELIM_TRY(big::laswp_net(C + k * ldc, ldc, net + 1, 0, 0, cb, ce, s, max_wg));
+  else
+    GELIM_TRY(big::laswp_panel(C, ldc, n, k, nl, pairs, kSlot, 0, 0, cb, ce, s, max_wg));
   if (big::trsm_fused() && wg <= 256) {
     GELIM_TRY(big::panel_trsm(C + k * ldc + cb, ldc, ce - cb, wg, L, ldl, s, max_wg));
   } else {

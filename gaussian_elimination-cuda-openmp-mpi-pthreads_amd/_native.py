@@ -86,7 +86,10 @@ _PROTOS = {
     "gelim_dist_pair_slot": (_i64, []),
     "gelim_dist_panel_factor": (_int, [_vp, _i64, _i64, _i64, _i64, _i64, _int, _vp, _vp, _vp, _vp, _int, _i64, _vp,
                                        _vp]),
-    "gelim_dist_panel_apply": (_int, [_vp, _i64, _i64, _i64, _i64, _i64, _vp, _i64, _i64, _vp, _int, _vp]),
+    "gelim_dist_panel_apply": (_int, [_vp, _i64, _i64, _i64, _i64, _i64, _vp, _i64, _i64, _vp, _vp, _int, _int,
+                                      _vp]),
+    "gelim_dist_net_ints": (_i64, []),
+    "gelim_dist_panel_compose": (_int, [_i64, _i64, _int, _vp, _vp, _vp]),
     "gelim_dist_side_cap": (_int, [_i64]),
     "gelim_gpu_panel_trsm": (_int, [_vp, _i64, _i64, _i64, _vp, _i64, _int, _vp]),
     "gelim_gpu_laswp_panel": (_int, [_vp, _i64, _i64, _i64, _int, _vp, _i64, _i64, _i64, _i64, _i64, _int, _vp]),

@@ -118,6 +118,7 @@ class ColumnLayout:
 LEAF = 32  # leaf width of the wide-panel engine (csrc/hip/biglu.hip)
 TAIL_ROWS = 2048  # GPU: the trailing system of at most this order goes to the single-GPU 2048 engine
 NBUF = 3  # GPU panel buffers in rotation
+COMPOSE_MAX_ROWS = 160 * 1024 // 4 - 1  # biglu.hip compose_max_rows(): one int per panel row in LDS
 
 
 class DistributedGauss:
@@ -157,7 +158,9 @@ class DistributedGauss:
             lib = _native.lib()
             self._slot = int(lib.gelim_dist_pair_slot())
             nl = D // LEAF
-            self._npd = -(-nl * self._slot // 2)  # pair lists, in doubles
+            self._nnet = int(lib.gelim_dist_net_ints())
+            # [leaf pair lists | composed movement | composed? flag], in doubles
+            self._npd = -(-(nl * self._slot + self._nnet + 2) // 2)
             self._bufs = [torch.empty(self.n_pad * D + self._npd, dtype=torch.float64, device=self.device)
                           for _ in range(NBUF)]
             self._side = torch.cuda.Stream(self.device)
@@ -317,7 +320,15 @@ class DistributedGauss:
                                                   stream_handle(self.device)), "dist_panel_factor")
         buf[:m * wg].view(m, wg).copy_(loc[k:, lc:lc + wg])
         nl = wg // LEAF
-        buf[m * wg:m * wg + self._npd].view(torch.int32)[:nl * self._slot].copy_(self._pairs[:nl * self._slot])
+        tail = buf[m * wg:m * wg + self._npd].view(torch.int32)
+        ns = nl * self._slot
+        tail[:ns].copy_(self._pairs[:ns])
+        # the panel's row movement composed ONCE here, shipped with the panel:
+        # every rank's apply is then one gather/scatter, not a per-column
+        # replay of the leaves' lists (~90 us a call)
+        ok = _native.check(lib.gelim_dist_panel_compose(n, k, nl, ptr(self._pairs), ptr(tail[ns:]),
+                                                        stream_handle(self.device)), "dist_panel_compose")
+        tail[ns + self._nnet].fill_(ok)
         return leaf + nl
 
     def _bsize(self, g: int) -> int:
@@ -333,10 +344,19 @@ class DistributedGauss:
         L, n = self.layout, self.n_pad
         k, wg = g * L.D, L.width(g)
         m = n - k
-        pairs = buf[m * wg:m * wg + self._npd]
+        tail = buf[m * wg:m * wg + self._npd].view(torch.int32)
+        ns = (wg // LEAF) * self._slot
+        # composed or not is a host-side function of (m, wg): the same test as
+        # gelim_dist_panel_compose, so no device read is needed here
+        net_ok = self._net_ok(m, wg // LEAF)
         sh = stream.cuda_stream if stream is not None else stream_handle(self.device)
         _native.check(_native.lib().gelim_dist_panel_apply(ptr(loc), loc.stride(0), n, k, cb, ce, ptr(buf), wg, wg,
-                                                           ptr(pairs), cap, sh), "dist_panel_apply")
+                                                           ptr(tail), ptr(tail[ns:]), int(net_ok), cap, sh),
+                      "dist_panel_apply")
+
+    def _net_ok(self, m: int, nleaves: int) -> bool:
+        net_max = (self._nnet - 2) // 2
+        return m <= COMPOSE_MAX_ROWS and nleaves * 2 * LEAF <= net_max
 
     def _block_at_local_col(self, c: int) -> int:
         """Global block index of this rank's local block starting at local column c."""

@@ -148,3 +148,24 @@ def test_emulated_dist_matmul_16384_8ranks(cuda, algo):
         ref = A[r0:r0 + 2048].double() @ B.double()
         err = max(err, ((C[r0:r0 + 2048].double() - ref).abs().max() / ref.abs().max()).item())
     assert err < 1e-5
+
+
+def test_emulated_dist_gauss_past_leaf_cap(gelim, cuda):
+    """n = 40000 on 2 emulated ranks: every owner panel is taller than the
+    round-2 leaf cap (32768 rows); agrees with the single-GPU solver."""
+    n, P = 40000, 2
+
+    def body(c):
+        dg = DistributedGauss(c, n)
+        return dg.solve_(dg.generate_random(seed=31))
+
+    xs = run_emulated(P, body, device=cuda, timeout_s=300)
+    aug = gelim.random_system(n, seed=31, device=cuda)
+    s = gelim.GaussSolver(n, backend="hip", device=cuda)
+    ref = s.solve(aug, check=True)
+    s.close()
+    del aug
+    torch.cuda.empty_cache()
+    for x in xs:
+        assert torch.equal(x, xs[0])
+        assert ((x - ref).abs().max() / ref.abs().max()).item() < 1e-8

@@ -67,6 +67,7 @@ struct Args {
   int M, N, K;
   int tiles_n, ntiles;
   double alpha;
+  int acc;  // 1: C += alpha A B, 0: C = alpha A B (C is not read)
 };
 
 // 16-byte chunks per thread per tile: A Tx16 -> T*8 chunks, B 16xT -> T*8
@@ -152,7 +153,8 @@ __device__ __forceinline__ void tile_body(const Args& g, int m0, int n0, double*
       for (int r = 0; r < 4; ++r) {
         const int row = m0 + wm + 16 * i + q + 4 * r;
         // edge tiles: clamped address, the value is never stored back
-        acc[i][j][r] = g.C[(int64_t)(FULL ? row : min(row, g.M - 1)) * g.ldc + (FULL ? col : min(col, g.N - 1))];
+        acc[i][j][r] = g.acc ? g.C[(int64_t)(FULL ? row : min(row, g.M - 1)) * g.ldc + (FULL ? col : min(col, g.N - 1))]
+                             : 0.0;
       }
     }
 
@@ -253,7 +255,7 @@ __global__ __launch_bounds__(kPThreads, 1) void dgemm_persist_kernel(Args g) {
 // C (M x N, ldc) += alpha * A (M x K, lda) * B (K x N, ldb); alpha in {+1, -1}
 // in practice (any value works: A is scaled once on its way into LDS).
 int dgemm_capped(double* C, int64_t ldc, const double* A, int64_t lda, const double* B, int64_t ldb, int64_t M,
-                 int64_t N, int64_t K, double alpha, int max_wg, hipStream_t s) {
+                 int64_t N, int64_t K, double alpha, int max_wg, hipStream_t s, int accumulate = 1) {
   if (M <= 0 || N <= 0 || K <= 0) return GELIM_OK;
   if (M > INT32_MAX || N > INT32_MAX || K > INT32_MAX) return GELIM_FAIL(GELIM_E_ARG, "dgemm: dimension > 2^31");
   // 16-byte operand chunks: 16-byte aligned A and B, even leading dimensions
@@ -263,7 +265,7 @@ int dgemm_capped(double* C, int64_t ldc, const double* A, int64_t lda, const dou
     return GELIM_FAIL(GELIM_E_ARG, "dgemm: unsupported alignment / leading dimensions (K=" + std::to_string(K) +
                                        " lda=" + std::to_string(lda) + " ldb=" + std::to_string(ldb) + ")");
   const int tm = (int)((M + BM - 1) / BM), tn = (int)((N + BN - 1) / BN);
-  Args g{C, ldc, A, lda, B, ldb, (int)M, (int)N, (int)K, tn, tm * tn, alpha};
+  Args g{C, ldc, A, lda, B, ldb, (int)M, (int)N, (int)K, tn, tm * tn, alpha, accumulate ? 1 : 0};
   // max_wg > 0: at most max_wg CUs (rounded down to a multiple of 8)
   const int cap = max_wg > 0 ? std::max(8, max_wg / 8 * 8) : 0;
   // few tiles: one 256-thread workgroup per tile already stays within the
@@ -308,6 +310,12 @@ int dgemm_capped(double* C, int64_t ldc, const double* A, int64_t lda, const dou
 int dgemm(double* C, int64_t ldc, const double* A, int64_t lda, const double* B, int64_t ldb, int64_t M,
           int64_t N, int64_t K, double alpha, hipStream_t s) {
   return dgemm_capped(C, ldc, A, lda, B, ldb, M, N, K, alpha, 0, s);
+}
+
+// C = alpha * A * B (accumulate = 0: C is written, never read) or C += ...
+int dgemm_ex(double* C, int64_t ldc, const double* A, int64_t lda, const double* B, int64_t ldb, int64_t M,
+             int64_t N, int64_t K, double alpha, int accumulate, hipStream_t s) {
+  return dgemm_capped(C, ldc, A, lda, B, ldb, M, N, K, alpha, 0, s, accumulate);
 }
 
 }  // namespace gelim

@@ -30,7 +30,7 @@ namespace gelim {
 int dgemm(double* C, int64_t ldc, const double* A, int64_t lda, const double* B, int64_t ldb, int64_t M,
           int64_t N, int64_t K, double alpha, hipStream_t s);
 int dgemm_capped(double* C, int64_t ldc, const double* A, int64_t lda, const double* B, int64_t ldb, int64_t M,
-                 int64_t N, int64_t K, double alpha, int max_wg, hipStream_t s);
+                 int64_t N, int64_t K, double alpha, int max_wg, hipStream_t s, int accumulate = 1);
 namespace big {
 int leaf_width();
 int leaf_factor(double* A, int64_t lda, int64_t m, int64_t c0, int mode, int* ipiv, int* pairs, int* info,

@@ -1,45 +1,58 @@
-// Mixed-precision solver (GaussSolver backend "hip-mixed"): a random
-// butterfly transform (RBT) of the system, a NO-pivoting blocked LU of the
-// transformed matrix in fp32 on the matrix cores, and fp64 iterative
-// refinement against the original system (the loop is in
-// models/gauss_solver.py; when it does not reach the fp64 error class the
-// solver falls back to the fp64 partial-pivoting engine by itself).
+// Randomised no-pivoting engines (GaussSolver backends "hip-mixed" and
+// "hip-rbt"): a random butterfly transform (RBT) of the system, a NO-pivoting
+// blocked LU of the transformed matrix on the matrix cores -- fp32 factors
+// ("hip-mixed") or fp64 factors ("hip-rbt") -- and fp64 iterative refinement
+// against the original system (the loop is in models/gauss_solver.py; when it
+// does not reach the fp64 error class the solver falls back to the fp64
+// partial-pivoting engine by itself).
 //
 // Why: every exact partial-pivoting engine here is bound by its pivot chain
-// (one global arg-max per column: ~4 us per column on the wide-panel leaves
-// at n = 8192, profiles/leaf_fused_vs_2hop.txt), so an fp32 copy of the same
-// algorithm would be just as slow.  A two-sided recursive butterfly
-// transform U^T A V (Parker 1995; Baboulin, Dongarra et al. 2013) makes
-// pivoting unnecessary with probability close to one, and the factorisation
-// is then panel-free in the latency sense: per 128-column block one
-// workgroup factors the 128 x 128 diagonal block, two column-/row-parallel
-// triangular solves produce U12 and L21, and one fp32 MFMA GEMM
-// (gemm_f32.hip, alpha = -1) updates the trailing matrix.  fp64 refinement
-// (residual in fp64 on the ORIGINAL system) restores the fp64 error class
-// (SURVEY.md §4.3 requires it: fp32 elimination alone fails saylr4 /
-// orsreg_1).  The reference has no refinement and no fp32 Gauss
-// (OpenMP_and_MPI/gauss_openmp/gauss_external_input.c:153-182 is fp64).
+// (one global arg-max per column: ~3 us per column on the wide-panel leaves
+// at n = 8192, profiles/leaf_fused_vs_2hop.txt).  A two-sided recursive
+// butterfly transform U^T A V (Parker 1995; Baboulin, Dongarra et al. 2013)
+// makes pivoting unnecessary with probability close to one, and without
+// pivoting the factorisation has no per-column global reduction at all.  The
+// reference's loop (OpenMP_and_MPI/gauss_openmp/gauss_external_input.c:153-182,
+// fp64, partial pivoting) is what the refinement answers to: the residual is
+// always taken in fp64 on the ORIGINAL system.
+//
+// Factorisation (T = float or double): block LDU without pivoting, 128-column
+// blocks.  Per block k:
+//  * diag_inv_kernel: ONE workgroup inverts the (Schur) diagonal block A_kk
+//    by Gauss-Jordan in fp64 registers (8 x 8 tiles per thread, one uniform
+//    rank-1 update and one barrier per column) -> Dinv_k (kept for the solves);
+//  * W = A_kk^-1 A_k,rest and A_rest,rest -= A_rest,k W on the matrix cores
+//    (fp64 dgemm.hip v_mfma_f64_16x16x4f64, or fp32 gemm_f32.hip
+//    v_mfma_f32_32x32x2f32 with a rounded copy of the inverse).  A_rest,k and
+//    A_k,rest stay in place as the factor's off-diagonal blocks.
+// The fp32 engine still inverts in fp64: an fp32 Gauss-Jordan of a no-pivoting
+// block with cond ~1e7 would be useless, while a correctly rounded copy of an
+// accurate inverse only costs eps32 relative in W.
+//
+// Solves (blk_trsv_kernel, one persistent launch per direction): workgroup w
+// owns block row b (128 equations); it applies the solved blocks before it in
+// chain order (the next block's factor loads in flight under the current
+// block's FMAs), then multiplies by the stored inverse -- a mat-vec, not a
+// 128-step chain -- in fp64 arithmetic over the T factor, and publishes its
+// block (agent-scope stores, drain, barrier, one chain counter).  Spins are
+// bounded (200 ms) and report through an error word.
 //
 // Depth-2 recursive butterfly: W = L1 L0, L0 = B<n> = 1/sqrt2 [R S; R -S]
 // on (i, i + n/2), L1 = diag(B<n/2>_a, B<n/2>_b) on (i, i + n/4) and
 // (i + n/2, i + 3n/4); R, S diagonal with entries exp(r / 10), r uniform in
 // [-1/2, 1/2].  Both levels act on the index groups {i, i + h, i + 2h,
 // i + 3h} (h = n/4) as one 4 x 4 matrix W_i, so M = U^T A V is ONE pass over
-// A: every 4 x 4 group of entries becomes U_i^T A_g V_j (and fp32 on the way
-// out).  The system is padded to np = a multiple of 128 with an identity
-// block (b padded with zeros).
-//
-// Storage of the factors: L (unit lower, below the diagonal) and U (on and
-// above it) overwrite the fp32 matrix, LAPACK style.  Solves: backsub.hip's
-// persistent forward (unit lower) and back (upper) substitutions, fp64
-// accumulation over the fp32 factors (np <= 16384: every 64-row block
-// resident).
+// A: every 4 x 4 group of entries becomes U_i^T A_g V_j.  The system is
+// padded to np = a multiple of 128 with an identity block (b padded with
+// zeros).  Storage: L (unit lower, below the diagonal) and U (on and above it)
+// overwrite the transformed matrix, LAPACK style.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
 #include <cmath>
 #include <cstdint>
 #include <string>
+#include <utility>
 
 #include "device_common.h"
 #include "gelim/internal.h"
@@ -47,16 +60,17 @@
 namespace gelim {
 int matmul_f32(const float* A, int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc, int64_t M, int64_t N,
                int64_t K, int accumulate, int kernel, hipStream_t s, float alpha);
-int backsub_f32(const float* U, int64_t ldu, const float* y, int64_t incy, double* x, double* bnorm, int64_t n,
-                int unit, double* yw, hipStream_t s, const int* perm, int* err);
-int fwdsub_unit_f32(const float* L, int64_t ldl, const double* y, float* out, int64_t n, double* xs,
-                    unsigned* flags, hipStream_t s);
+int dgemm_ex(double* C, int64_t ldc, const double* A, int64_t lda, const double* B, int64_t ldb, int64_t M,
+             int64_t N, int64_t K, double alpha, int accumulate, hipStream_t s);
 
 namespace {
 
-constexpr int NB = 128;        // LU block
-constexpr int kPadTo = NB;     // np multiple
-constexpr int kLdsLd = NB + 1;  // diagonal-block LDS row stride (floats)
+constexpr int NB = 128;         // LU block = solve block
+constexpr int kPadTo = NB;      // np multiple
+constexpr int kDT = 512;        // solve workgroup: 128 rows x 4 column quarters
+constexpr int kQW = NB / 4;     // columns per quarter
+constexpr int kMaxBlocks = 256;  // persistent solves: every block row resident
+constexpr unsigned long long kSpinTicks = 20000000ull;  // 200 ms at 100 MHz
 
 // ---- the butterfly group matrices -------------------------------------------
 // d: 8 arrays of h doubles: R0[i], R0[i+h], S0[i], S0[i+h], Ra[i], Sa[i], Rb[i], Sb[i]
@@ -79,9 +93,10 @@ __device__ __forceinline__ void group_w(const double* __restrict__ d, int h, int
 
 // M[g] = U_i^T A_g V_j for every 4 x 4 group; A is the n x n system (row
 // major, lda), padded on the fly to np with an identity block.
+template <typename T>
 __global__ __launch_bounds__(256) void rbt_matrix_kernel(const double* __restrict__ A, int64_t lda, int n, int np,
                                                         const double* __restrict__ ud, const double* __restrict__ vd,
-                                                        float* __restrict__ M, int64_t ldm) {
+                                                        T* __restrict__ M, int64_t ldm) {
   const int h = np / 4;
   const int j = blockIdx.x * 256 + threadIdx.x;  // column group
   const int i = blockIdx.y;                      // row group
@@ -114,7 +129,7 @@ __global__ __launch_bounds__(256) void rbt_matrix_kernel(const double* __restric
       double v = 0.0;
 #pragma unroll
       for (int c = 0; c < 4; ++c) v += t[q][c] * V[c][p];
-      M[(int64_t)(i + q * h) * ldm + j + p * h] = (float)v;
+      M[(int64_t)(i + q * h) * ldm + j + p * h] = (T)v;
     }
 }
 
@@ -122,7 +137,7 @@ __global__ __launch_bounds__(256) void rbt_matrix_kernel(const double* __restric
 // (b: n entries with stride incb; the padding reads as 0)
 __global__ __launch_bounds__(256) void rbt_vec_kernel(const double* __restrict__ b, int64_t incb, int n, int np,
                                                      const double* __restrict__ d, int transpose,
-                                                     double* __restrict__ out) {
+                                                     double* __restrict__ out, int nout) {
   const int h = np / 4;
   const int i = blockIdx.x * 256 + threadIdx.x;
   if (i >= h) return;
@@ -139,129 +154,319 @@ __global__ __launch_bounds__(256) void rbt_vec_kernel(const double* __restrict__
     double s = 0.0;
 #pragma unroll
     for (int c = 0; c < 4; ++c) s += (transpose ? W[c][q] : W[q][c]) * v[c];
-    out[i + q * h] = s;
+    if (i + q * h < nout) out[i + q * h] = s;
   }
 }
 
-// ---- blocked no-pivot LU ------------------------------------------------------
-// One workgroup factors the NB x NB diagonal block at (k0, k0) in LDS: 8
-// threads per row, one barrier per column.  info[0] = 1 + the first column
-// whose pivot is zero or not finite (kept if set).
-__global__ __launch_bounds__(1024) void diag_lu_kernel(float* __restrict__ A, int64_t lda, int k0,
+// ---- diagonal block inverse: Gauss-Jordan without pivoting ---------------------
+// Block LDU (no pivoting): A = [I 0; A21 A11^-1 I] [A11 A12; 0 S], S = A22 -
+// A21 (A11^-1 A12).  So a block step needs only A11^-1 (kept, fp64, for the
+// solves) and two GEMMs, W = A11^-1 A12 and A22 -= A21 W; A21 / A12 stay in
+// place as the factor's off-diagonal blocks.
+//
+// One workgroup of 256 threads (one wave per SIMD) inverts the 128 x 128
+// block in place in registers: thread (rg, cg) = (t >> 4, t & 15) holds the
+// 8 x 8 tile rows 8 rg.., columns 8 cg...  Step k of Gauss-Jordan is ONE
+// uniform rank-1 update of the whole block,
+//   a[i][j] -= g_i u_j,  g_i = a[i][k] - [i == k],  u_j = a[k][j] / a[k][k] (j != k),  u_k = 1 + 1 / a[k][k],
+// which gives a'[k][k] = 1/a_kk, a'[k][j] = a_kj/a_kk, a'[i][k] = -a_ik/a_kk
+// and the Schur update elsewhere with no special cases.  Row k and column k
+// are published raw through parity-buffered LDS one step ahead (one barrier
+// per step), and the step loop is unrolled by 8 so every in-tile index (k % 8)
+// is static: publishing is a predicated store, not a register pick.  ~500
+// cycles per step, 128 steps (the earlier LU + two triangular-inverse loops
+// with one row per lane: 330 us per block, instruction-bound).
+constexpr int kGT = 256;  // threads
+constexpr int kTl = 8;    // tile edge
+
+template <typename TI>
+struct alignas(16) GjLds {
+  TI row[2][NB];
+  TI col[2][NB];
+};
+
+template <int KK>
+__device__ __forceinline__ void gj_step(double (&a)[kTl][kTl], GjLds<double>& sh, int kg, int rg, int cg) {
+  const int k = kTl * kg + KK;
+  constexpr int par = KK & 1;  // kTl is even: k and KK share parity
+  const double pk = 1.0 / sh.row[par][k];
+  double u[kTl], g[kTl];
+#pragma unroll
+  for (int j = 0; j < kTl; j += 2) {
+    const double2 v = *reinterpret_cast<const double2*>(&sh.row[par][kTl * cg + j]);
+    u[j] = v.x * pk;
+    u[j + 1] = v.y * pk;
+  }
+#pragma unroll
+  for (int i = 0; i < kTl; i += 2) {
+    const double2 v = *reinterpret_cast<const double2*>(&sh.col[par][kTl * rg + i]);
+    g[i] = v.x;
+    g[i + 1] = v.y;
+  }
+  u[KK] = (cg == kg) ? 1.0 + pk : u[KK];
+  g[KK] -= (rg == kg) ? 1.0 : 0.0;
+#pragma unroll
+  for (int i = 0; i < kTl; ++i)
+#pragma unroll
+    for (int j = 0; j < kTl; ++j) a[i][j] = fma(-g[i], u[j], a[i][j]);
+  // publish step k + 1 (raw row / column of the updated block)
+  if (k + 1 < NB) {
+    constexpr int kk1 = (KK + 1) % kTl;
+    const int kg1 = KK + 1 == kTl ? kg + 1 : kg;
+    if (rg == kg1) {
+#pragma unroll
+      for (int j = 0; j < kTl; j += 2)
+        *reinterpret_cast<double2*>(&sh.row[par ^ 1][kTl * cg + j]) = make_double2(a[kk1][j], a[kk1][j + 1]);
+    }
+    if (cg == kg1) {
+#pragma unroll
+      for (int i = 0; i < kTl; i += 2)
+        *reinterpret_cast<double2*>(&sh.col[par ^ 1][kTl * rg + i]) = make_double2(a[i][kk1], a[i + 1][kk1]);
+    }
+  }
+  __syncthreads();
+}
+
+template <int... KK>
+__device__ __forceinline__ void gj_steps(double (&a)[kTl][kTl], GjLds<double>& sh, int kg, int rg, int cg,
+                                         std::integer_sequence<int, KK...>) {
+  (gj_step<KK>(a, sh, kg, rg, cg), ...);
+}
+
+// Dinv = A[k0.., k0..]^-1 (fp64, row-major NB x NB) of the T block of A; with
+// Tinv, also a T copy (the fp32 engine's GEMM operand).  The block is read,
+// not modified.  info: atomicMin of 1 + k0 when the inverse is not finite (a
+// zero / tiny pivot).
+template <typename T>
+__global__ __launch_bounds__(kGT) void diag_inv_kernel(const T* __restrict__ A, int64_t lda, int k0,
+                                                      double* __restrict__ Dinv, T* __restrict__ Tinv,
                                                       int* __restrict__ info) {
-  extern __shared__ float S[];  // [NB][kLdsLd]
-  const int t = threadIdx.x, row = t >> 3, c8 = t & 7;
-  float* Ar = A + (int64_t)(k0 + row) * lda + k0;
-  for (int j = c8; j < NB; j += 8) S[row * kLdsLd + j] = Ar[j];
-  __syncthreads();
-  for (int k = 0; k < NB - 1; ++k) {
-    if (row > k) {
-      const float p = S[k * kLdsLd + k];
-      const float l = S[row * kLdsLd + k] / p;
-      // the row's 16 columns as one batch of independent LDS reads / FMAs /
-      // writes (a static loop, predicated on j > k), not a dependent chain
-      float v[NB / 8], u[NB / 8];
+  __shared__ GjLds<double> sh;
+  const int t = threadIdx.x, rg = t >> 4, cg = t & 15;
+  double a[kTl][kTl];
 #pragma unroll
-      for (int q = 0; q < NB / 8; ++q) {
-        const int j = c8 + 8 * q;
-        v[q] = S[row * kLdsLd + j];
-        u[q] = S[k * kLdsLd + j];
+  for (int i = 0; i < kTl; ++i) {
+    const T* src = A + (int64_t)(k0 + kTl * rg + i) * lda + k0 + kTl * cg;
+#pragma unroll
+    for (int j = 0; j < kTl; ++j) a[i][j] = (double)src[j];
+  }
+  if (rg == 0) {
+#pragma unroll
+    for (int j = 0; j < kTl; ++j) sh.row[0][kTl * cg + j] = a[0][j];
+  }
+  if (cg == 0) {
+#pragma unroll
+    for (int i = 0; i < kTl; ++i) sh.col[0][kTl * rg + i] = a[i][0];
+  }
+  __syncthreads();
+  for (int kg = 0; kg < NB / kTl; ++kg) gj_steps(a, sh, kg, rg, cg, std::make_integer_sequence<int, kTl>{});
+  bool fin = true;
+#pragma unroll
+  for (int i = 0; i < kTl; ++i) {
+    double* dst = Dinv + (int64_t)(kTl * rg + i) * NB + kTl * cg;
+#pragma unroll
+    for (int j = 0; j < kTl; ++j) {
+      fin = fin && isfinite(a[i][j]);
+      dst[j] = a[i][j];
+    }
+    if (Tinv) {
+      T* tdst = Tinv + (int64_t)(kTl * rg + i) * NB + kTl * cg;
+#pragma unroll
+      for (int j = 0; j < kTl; ++j) tdst[j] = (T)a[i][j];
+    }
+  }
+  if (!fin) atomicMin(info, k0 + 1);
+}
+
+// ---- persistent block triangular solves ----------------------------------------
+
+__device__ __forceinline__ unsigned long long rtc() {
+  unsigned long long t;
+  asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  return t;
+}
+
+__device__ __forceinline__ double bcast_lane(double v, int l) {
+  const uint64_t b = __builtin_bit_cast(uint64_t, v);
+  return __builtin_bit_cast(double, ((uint64_t)(unsigned)__builtin_amdgcn_readlane((int)(b >> 32), l) << 32) |
+                                        (unsigned)__builtin_amdgcn_readlane((int)b, l));
+}
+
+// x = F^-1 c for the unit-lower (UPPER = false) or upper (UPPER = true)
+// triangle of the factor F (np x np, ldf), with the diagonal blocks' inverses
+// Dinv (nblk x NB x NB fp64, row-major).  Workgroup w handles block row b = w
+// (lower) or nblk - 1 - w (upper): chain position w, so the first block of the
+// chain is the first workgroup dispatched.  Blocks are solved strictly in
+// chain order, so ONE counter (`done` = blocks solved) replaces per-block
+// flags: a workgroup polls only when it has consumed every block the counter
+// promised, and otherwise streams through the solved blocks with the next
+// block's factor loads in flight under the current block's FMAs (a poll is an
+// atomic load, whose wait would drain every outstanding load).  Thread (r, q):
+// equation 128 b + r, columns 32 q .. 32 q + 31 of every 128-column block.
+template <typename T>
+__device__ __forceinline__ void load_blk(T (&u)[kQW], const T* __restrict__ p) {
+#pragma unroll
+  for (int j = 0; j < kQW; ++j) u[j] = p[j];
+}
+
+__device__ __forceinline__ int poll_done(const unsigned* done, int need, int* err) {
+  int got = 0;
+  if (__lane_id() == 0) {
+    unsigned v = __hip_atomic_load(done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if ((int)v < need) {
+      const unsigned long long t0 = rtc();
+      while ((int)(v = __hip_atomic_load(done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) < need) {
+        if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0 || rtc() - t0 > kSpinTicks) {
+          __hip_atomic_store(err, 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          v = 0;
+          break;
+        }
       }
-#pragma unroll
-      for (int q = 0; q < NB / 8; ++q) {
-        const int j = c8 + 8 * q;
-        if (j > k) S[row * kLdsLd + j] = fmaf(-l, u[q], v[q]);
-      }
-      if (c8 == (k & 7)) S[row * kLdsLd + k] = l;
     }
-    __syncthreads();
+    got = (int)v;
   }
-  if (c8 == 0) {
-    const float p = S[row * kLdsLd + row];
-    if (!(p != 0.0f) || !isfinite(p)) atomicMin(info, k0 + row + 1);
-  }
-  for (int j = c8; j < NB; j += 8) Ar[j] = S[row * kLdsLd + j];
+  return __shfl(got, 0);
 }
 
-// Both off-diagonal triangular solves are lower-triangular solves on a
-// 128 x 64 tile X held in LDS, one barrier per column k (row k of X is final
-// once step k-1 is done and nobody writes it at step k):
-//   U12 = L11^-1 A12        X = a 64-column slice of A12, L = L11 (unit);
-//   L21 = A21 U11^-1  <=>  L21^T = U11^-T A21^T: X = a 64-row slice of A21,
-//                           transposed, L = U11^T (its diagonal divisions
-//                           deferred to the end: row k is not touched after
-//                           its step).
-// 256 threads: lane = column of X, wave = row group (rows i = rg mod 4).
-constexpr int kXld = 65, kLld = NB + 1, kTile = 64;
-
-template <bool UNIT>
-__device__ __forceinline__ void tile_lower_solve(float* __restrict__ X, const float* __restrict__ L,
-                                                 const float* __restrict__ rinv) {
-  const int t = threadIdx.x, c = t & 63, rg = t >> 6;
-  for (int k = 0; k < NB - 1; ++k) {
-    const float xk = UNIT ? X[k * kXld + c] : X[k * kXld + c] * rinv[k];
-    // this thread's 32 rows i = 4 q + rg as one batch (static loop, predicated
-    // on i > k): independent LDS reads, FMAs and writes, pipelined
-    float v[NB / 4], l[NB / 4];
+template <typename T, bool UPPER>
+__global__ __launch_bounds__(kDT) void blk_trsv_kernel(const T* __restrict__ F, int64_t ldf,
+                                                      const double* __restrict__ Dinv, const double* __restrict__ c,
+                                                      double* __restrict__ x, double* __restrict__ ysave, int nblk,
+                                                      unsigned* __restrict__ done, int* __restrict__ err) {
+  __shared__ double part[4][NB];
+  __shared__ double rb[NB];
+  __shared__ int bad;
+  const int t = threadIdx.x, r = t & (NB - 1), lane = t & 63;
+  const int q = __builtin_amdgcn_readfirstlane(t >> 7);
+  const int w = blockIdx.x;
+  const int b = UPPER ? nblk - 1 - w : w;
+  const int row = NB * b + r;
+  if (t == 0) bad = 0;
+  // this block's inverse row (independent of everything: loaded first)
+  double dv[kQW];
+  {
+    const double* d = Dinv + ((int64_t)b * NB + r) * NB + kQW * q;
 #pragma unroll
-    for (int q = 0; q < NB / 4; ++q) {
-      const int i = 4 * q + rg;
-      v[q] = X[i * kXld + c];
-      l[q] = L[i * kLld + k];
-    }
-#pragma unroll
-    for (int q = 0; q < NB / 4; ++q) {
-      const int i = 4 * q + rg;
-      if (i > k) X[i * kXld + c] = fmaf(-l[q], xk, v[q]);
-    }
-    __syncthreads();
+    for (int j = 0; j < kQW; ++j) dv[j] = d[j];
   }
-  if (!UNIT)
-    for (int i = rg; i < NB; i += 4) X[i * kXld + c] *= rinv[i];
+  const double cv = c[row];
+  double acc = 0.0;
+  int avail = 0;
+  const T* frow = F + (int64_t)row * ldf + kQW * q;
+  auto blk = [&](int i) { return frow + (int64_t)NB * (UPPER ? nblk - 1 - i : i); };
+  bool ok = true;
+  T ua[kQW], ub[kQW];
+  if (w > 0) load_blk(ua, blk(0));
+  for (int i = 0; i < w; i += 2) {
+    // block i (in ua); block i + 1's loads go out after block i's x
+    if (i >= avail) {
+      avail = poll_done(done, i + 1, err);
+      if (avail <= i) { ok = false; break; }
+    }
+    {
+      const int jb = UPPER ? nblk - 1 - i : i;
+      const double xl = lane < kQW ? __builtin_bit_cast(double, __hip_atomic_load(
+                                                                    reinterpret_cast<const unsigned long long*>(
+                                                                        x + NB * jb + kQW * q + lane),
+                                                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+                                   : 0.0;
+      if (i + 1 < w) load_blk(ub, blk(i + 1));
+#pragma unroll
+      for (int j = 0; j < kQW; ++j) acc = fma(-(double)ua[j], bcast_lane(xl, j), acc);
+    }
+    if (i + 1 >= w) break;
+    if (i + 1 >= avail) {
+      avail = poll_done(done, i + 2, err);
+      if (avail <= i + 1) { ok = false; break; }
+    }
+    {
+      const int jb = UPPER ? nblk - 2 - i : i + 1;
+      const double xl = lane < kQW ? __builtin_bit_cast(double, __hip_atomic_load(
+                                                                    reinterpret_cast<const unsigned long long*>(
+                                                                        x + NB * jb + kQW * q + lane),
+                                                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+                                   : 0.0;
+      if (i + 2 < w) load_blk(ua, blk(i + 2));
+#pragma unroll
+      for (int j = 0; j < kQW; ++j) acc = fma(-(double)ub[j], bcast_lane(xl, j), acc);
+    }
+  }
+  part[q][r] = acc;
+  if (!ok && lane == 0) bad = 1;
   __syncthreads();
+  if (bad) return;  // uniform: a timed-out wave makes the whole workgroup stop
+  if (q == 0) {
+    const double y = cv + part[0][r] + part[1][r] + part[2][r] + part[3][r];
+    rb[r] = y;
+    if (ysave) ysave[row] = y;
+  }
+  __syncthreads();
+  double xs = 0.0;
+#pragma unroll
+  for (int j = 0; j < kQW; ++j) xs = fma(dv[j], rb[kQW * q + j], xs);
+  __syncthreads();  // everyone has read rb / part
+  part[q][r] = xs;
+  __syncthreads();
+  if (q == 0) {
+    const double xv = part[0][r] + part[1][r] + part[2][r] + part[3][r];
+    __hip_atomic_store(reinterpret_cast<unsigned long long*>(x + row), __builtin_bit_cast(unsigned long long, xv),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  if (t == 0) __hip_atomic_store(done, (unsigned)(w + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// U12 = L11^-1 A12 in place for columns [c0, c0 + ncols), 64 per workgroup.
-__global__ __launch_bounds__(256) void trsm_u12_kernel(float* __restrict__ A, int64_t lda, int k0, int c0, int ncols) {
-  extern __shared__ float lds[];
-  float* L = lds;                // [NB][kLld]
-  float* X = lds + NB * kLld;    // [NB][kXld]
-  const int t = threadIdx.x, c = t & 63, rg = t >> 6;
-  for (int e = t; e < NB * NB; e += 256) L[(e / NB) * kLld + e % NB] = A[(int64_t)(k0 + e / NB) * lda + k0 + e % NB];
-  const int col = c0 + blockIdx.x * kTile + c;
-  const bool ok = col < c0 + ncols;
-  for (int i = rg; i < NB; i += 4) X[i * kXld + c] = ok ? A[(int64_t)(k0 + i) * lda + col] : 0.0f;
-  __syncthreads();
-  tile_lower_solve<true>(X, L, nullptr);
-  if (ok)
-    for (int i = rg; i < NB; i += 4) A[(int64_t)(k0 + i) * lda + col] = X[i * kXld + c];
+// Block LDU factorisation of the transformed matrix in place: per block k,
+// Dinv_k = A_kk^-1, W = A_kk^-1 A_k,rest (side buffer), A_rest,rest -= A_rest,k W.
+template <typename T>
+int factor_impl(T* M, int64_t ldm, int64_t np, double* Dinv, T* W, T* Tinv, int* info, hipStream_t s) {
+  for (int64_t k0 = 0; k0 < np; k0 += NB) {
+    double* Di = Dinv + (k0 / NB) * NB * NB;
+    hipLaunchKernelGGL(diag_inv_kernel<T>, dim3(1), dim3(kGT), 0, s, M, ldm, (int)k0, Di,
+                       sizeof(T) == 8 ? (T*)nullptr : Tinv, info);
+    HIP_TRY(hipGetLastError());
+    const int64_t rest = np - k0 - NB;
+    if (rest <= 0) break;
+    T* A12 = M + k0 * ldm + k0 + NB;
+    T* A21 = M + (k0 + NB) * ldm + k0;
+    T* A22 = M + (k0 + NB) * ldm + k0 + NB;
+    if constexpr (sizeof(T) == 8) {
+      GELIM_TRY(dgemm_ex(W, rest, Di, NB, A12, ldm, NB, rest, NB, 1.0, 0, s));        // W = A11^-1 A12
+      GELIM_TRY(dgemm_ex(A22, ldm, A21, ldm, W, rest, rest, rest, NB, -1.0, 1, s));  // A22 -= A21 W
+    } else {
+      GELIM_TRY(matmul_f32(Tinv, NB, A12, ldm, W, rest, NB, rest, NB, 0, GELIM_MM_MFMA, s, 1.0f));
+      GELIM_TRY(matmul_f32(A21, ldm, W, rest, A22, ldm, rest, rest, NB, 1, GELIM_MM_MFMA, s, -1.0f));
+    }
+  }
+  return GELIM_OK;
 }
 
-// L21 = A21 U11^-1 in place for rows [r0, r0 + nrows), 64 per workgroup.
-__global__ __launch_bounds__(256) void trsm_l21_kernel(float* __restrict__ A, int64_t lda, int k0, int r0, int nrows) {
-  extern __shared__ float lds[];
-  float* L = lds;                    // [NB][kLld]: L[i][k] = U11[k][i]
-  float* X = lds + NB * kLld;        // [NB][kXld]: X[i][c] = A21[row c][i]
-  float* rinv = X + NB * kXld;       // [NB]
-  const int t = threadIdx.x;
-  for (int e = t; e < NB * NB; e += 256) {
-    const int k = e / NB, i = e % NB;  // coalesced along U11's row k
-    L[i * kLld + k] = A[(int64_t)(k0 + k) * lda + k0 + i];
-  }
-  if (t < NB) rinv[t] = 1.0f / A[(int64_t)(k0 + t) * lda + k0 + t];
-  const int rbase = r0 + blockIdx.x * kTile;
-  for (int e = t; e < kTile * NB; e += 256) {
-    const int c = e / NB, i = e % NB;  // coalesced along the row of A21
-    const int row = rbase + c;
-    X[i * kXld + c] = row < r0 + nrows ? A[(int64_t)row * lda + k0 + i] : 0.0f;
-  }
-  __syncthreads();
-  tile_lower_solve<false>(X, L, rinv);
-  for (int e = t; e < kTile * NB; e += 256) {
-    const int c = e / NB, i = e % NB;
-    const int row = rbase + c;
-    if (row < r0 + nrows) A[(int64_t)row * lda + k0 + i] = X[i * kXld + c];
-  }
+// Block-LDU solve: forward z_k = D_k^-1 (c_k - sum_{j<k} A_kj z_j) keeping
+// y_k = c_k - sum (the block-unit-lower solve's result), then backward
+// x_k = D_k^-1 (y_k - sum_{j>k} A_kj x_j).  c -> (z, y) -> x (x may alias c).
+template <typename T>
+int solve_impl(const T* M, int64_t ldm, int64_t np, const double* Dinv, const double* c, double* z, double* y,
+               double* x, unsigned* flags, hipStream_t s) {
+  const int nblk = (int)(np / NB);
+  static const bool fits = [] {
+    int a = 0, b = 0;
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(&a, blk_trsv_kernel<T, false>, kDT, 0) == hipSuccess &&
+           hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, blk_trsv_kernel<T, true>, kDT, 0) == hipSuccess &&
+           a >= 1 && b >= 1;
+  }();
+  if (!fits || nblk > kMaxBlocks || !coresident(1, nblk))
+    return GELIM_FAIL(GELIM_E_ARG, "mixed solve: the block rows of this order cannot all be resident");
+  // flags[0]: lower-solve counter, flags[1]: upper-solve counter, flags[2]: error word
+  int* err = reinterpret_cast<int*>(flags + 2);
+  GELIM_TRY(zero_async(flags, 16, s));
+  hipLaunchKernelGGL((blk_trsv_kernel<T, false>), dim3(nblk), dim3(kDT), 0, s, M, ldm, Dinv, c, z, y, nblk, flags,
+                     err);
+  HIP_TRY(hipGetLastError());
+  hipLaunchKernelGGL((blk_trsv_kernel<T, true>), dim3(nblk), dim3(kDT), 0, s, M, ldm, Dinv, y, x, (double*)nullptr,
+                     nblk, flags + 1, err);
+  HIP_TRY(hipGetLastError());
+  return GELIM_OK;
 }
 
 }  // namespace
@@ -269,23 +474,27 @@ __global__ __launch_bounds__(256) void trsm_l21_kernel(float* __restrict__ A, in
 
 struct gelim_mixed_plan {
   int64_t n = 0, np = 0, ldm = 0;
-  float* M = nullptr;       // np x ldm: the transformed matrix, then its LU factors
+  int fp64 = 0;             // factor precision: 0 fp32 ("hip-mixed"), 1 fp64 ("hip-rbt")
+  void* M = nullptr;        // np x ldm: the transformed matrix, then its block-LDU factor
+  double* Dinv = nullptr;   // nblk x NB x NB: inverse of every (Schur) diagonal block, fp64
+  void* W = nullptr;        // NB x np: A_kk^-1 A_k,rest of the current block
+  void* Tinv = nullptr;     // NB x NB: fp32 copy of the current inverse (fp32 engine)
   double* ud = nullptr;     // U's butterfly diagonals (8 x np/4)
   double* vd = nullptr;     // V's
-  unsigned* flags = nullptr;  // forward substitution hand-off flags (np / 64 + 2)
+  unsigned* flags = nullptr;  // solve counters (lower, upper) + error word
   double* c = nullptr;      // U^T r (np)
-  float* y = nullptr;       // L^-1 c (np, fp32)
+  double* y = nullptr;      // L^-1 c (np)
   double* z = nullptr;      // U^-1 y (np)
-  double* yw = nullptr;     // back-substitution workspace (np + 2)
   int* info = nullptr;
+  int err_host = 0;
 };
 
-extern "C" int64_t gelim_mixed_max_n(void) { return 16384; }
+extern "C" int64_t gelim_mixed_max_n(void) { return (int64_t)gelim::kMaxBlocks * gelim::NB; }
 
 extern "C" void gelim_mixed_plan_destroy(gelim_mixed_plan* p) {
   if (!p) return;
-  for (void* q : {(void*)p->M, (void*)p->ud, (void*)p->vd, (void*)p->flags, (void*)p->c, (void*)p->y, (void*)p->z,
-                  (void*)p->yw, (void*)p->info})
+  for (void* q : {p->M, (void*)p->Dinv, p->W, p->Tinv, (void*)p->ud, (void*)p->vd, (void*)p->flags, (void*)p->c,
+                  (void*)p->y, (void*)p->z, (void*)p->info})
     (void)hipFree(q);
   delete p;
 }
@@ -294,39 +503,50 @@ extern "C" void gelim_mixed_plan_destroy(gelim_mixed_plan* p) {
 // each (np = gelim_mixed_padded(n)), exp(r/10) with r uniform in [-1/2, 1/2].
 extern "C" int64_t gelim_mixed_padded(int64_t n) { return (n + gelim::kPadTo - 1) / gelim::kPadTo * gelim::kPadTo; }
 
-extern "C" gelim_mixed_plan* gelim_mixed_plan_create(int64_t n, const double* ud, const double* vd) {
+// fp64 = 0: fp32 factors (GMRES-IR in the caller), 1: fp64 factors.
+extern "C" gelim_mixed_plan* gelim_mixed_plan_create2(int64_t n, const double* ud, const double* vd, int fp64) {
   const int64_t np = gelim_mixed_padded(n);
   if (n <= 0 || np > gelim_mixed_max_n()) {
     GELIM_FAIL(GELIM_E_ARG, "mixed plan: n must be in [1, " + std::to_string(gelim_mixed_max_n()) +
-                                "] (persistent triangular solves: every 64-row block resident)");
+                                "] (persistent triangular solves: every 128-row block resident)");
     return nullptr;
   }
   auto* p = new gelim_mixed_plan;
   p->n = n;
   p->np = np;
-  p->ldm = np + 4;  // 16-byte rows, off the power-of-two stride
+  p->fp64 = fp64 ? 1 : 0;
+  const size_t es = fp64 ? 8 : 4;
+  p->ldm = np + (fp64 ? 2 : 4);  // 16-byte rows, off the power-of-two stride
   auto fail = [&](const char* what) -> gelim_mixed_plan* {
     GELIM_FAIL(GELIM_E_NOMEM, std::string("mixed plan: ") + what);
     gelim_mixed_plan_destroy(p);
     return nullptr;
   };
   const size_t nd = (size_t)2 * np;  // 8 arrays of np/4
-  if (hipMalloc((void**)&p->M, sizeof(float) * (size_t)np * p->ldm) != hipSuccess) return fail("matrix");
+  const int64_t nblk = np / gelim::NB;
+  if (hipMalloc(&p->M, es * (size_t)np * p->ldm) != hipSuccess) return fail("matrix");
+  if (hipMalloc((void**)&p->Dinv, sizeof(double) * (size_t)np * gelim::NB) != hipSuccess) return fail("inverses");
+  if (hipMalloc(&p->W, es * (size_t)np * gelim::NB) != hipSuccess) return fail("W buffer");
+  if (!fp64 && hipMalloc(&p->Tinv, es * (size_t)gelim::NB * gelim::NB) != hipSuccess) return fail("fp32 inverse");
   if (hipMalloc((void**)&p->ud, sizeof(double) * nd) != hipSuccess) return fail("ud");
   if (hipMalloc((void**)&p->vd, sizeof(double) * nd) != hipSuccess) return fail("vd");
-  if (hipMalloc((void**)&p->flags, sizeof(unsigned) * (np / 64 + 2)) != hipSuccess) return fail("flags");
+  (void)nblk;
+  if (hipMalloc((void**)&p->flags, 16) != hipSuccess) return fail("flags");
   if (hipMalloc((void**)&p->c, sizeof(double) * np) != hipSuccess) return fail("c");
-  if (hipMalloc((void**)&p->y, sizeof(float) * np) != hipSuccess) return fail("y");
+  if (hipMalloc((void**)&p->y, sizeof(double) * np) != hipSuccess) return fail("y");
   if (hipMalloc((void**)&p->z, sizeof(double) * np) != hipSuccess) return fail("z");
-  if (hipMalloc((void**)&p->yw, sizeof(double) * (np + 2)) != hipSuccess) return fail("yw");
   if (hipMalloc((void**)&p->info, 16) != hipSuccess) return fail("info");
   if (hipMemcpy(p->ud, ud, sizeof(double) * nd, hipMemcpyHostToDevice) != hipSuccess) return fail("ud copy");
   if (hipMemcpy(p->vd, vd, sizeof(double) * nd, hipMemcpyHostToDevice) != hipSuccess) return fail("vd copy");
   return p;
 }
 
+extern "C" gelim_mixed_plan* gelim_mixed_plan_create(int64_t n, const double* ud, const double* vd) {
+  return gelim_mixed_plan_create2(n, ud, vd, 0);
+}
+
 // Transform the augmented fp64 system's matrix (n x n at aug, leading
-// dimension ld) into the plan's fp32 matrix and factor it without pivoting.
+// dimension ld) into the plan's matrix and factor it without pivoting.
 // Returns 0, or 1 + the first column whose pivot is zero / not finite (the
 // caller then falls back to partial pivoting); < 0 on errors.  Synchronises.
 extern "C" int gelim_mixed_factor(gelim_mixed_plan* p, const double* aug, int64_t ld, void* stream) {
@@ -335,35 +555,20 @@ extern "C" int gelim_mixed_factor(gelim_mixed_plan* p, const double* aug, int64_
   hipStream_t s = (hipStream_t)stream;
   const int64_t np = p->np, h = np / 4, ldm = p->ldm;
   HIP_TRY(hipMemsetAsync(p->info, 0x7f, 4, s));  // INT_MAX-ish: atomicMin keeps the first bad column
-  hipLaunchKernelGGL(rbt_matrix_kernel, dim3((unsigned)((h + 255) / 256), (unsigned)h), dim3(256), 0, s, aug, ld,
-                     (int)p->n, (int)np, p->ud, p->vd, p->M, ldm);
-  HIP_TRY(hipGetLastError());
-  static const bool attr = [] {
-    const int diag = (int)(sizeof(float) * NB * kLdsLd), tr = (int)(sizeof(float) * (NB * kLld + NB * kXld + NB));
-    return hipFuncSetAttribute((const void*)diag_lu_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, diag) ==
-               hipSuccess &&
-           hipFuncSetAttribute((const void*)trsm_u12_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, tr) ==
-               hipSuccess &&
-           hipFuncSetAttribute((const void*)trsm_l21_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, tr) ==
-               hipSuccess;
-  }();
-  if (!attr) return GELIM_FAIL(GELIM_E_HIP, "mixed_factor: LDS attributes refused");
-  float* M = p->M;
-  for (int64_t k0 = 0; k0 < np; k0 += NB) {
-    hipLaunchKernelGGL(diag_lu_kernel, dim3(1), dim3(1024), sizeof(float) * NB * kLdsLd, s, M, ldm, (int)k0, p->info);
+  const dim3 grid((unsigned)((h + 255) / 256), (unsigned)h);
+  if (p->fp64) {
+    auto* M = static_cast<double*>(p->M);
+    hipLaunchKernelGGL(rbt_matrix_kernel<double>, grid, dim3(256), 0, s, aug, ld, (int)p->n, (int)np, p->ud, p->vd, M,
+                       ldm);
     HIP_TRY(hipGetLastError());
-    const int64_t rest = np - k0 - NB;
-    if (rest <= 0) break;
-    const unsigned g = (unsigned)((rest + kTile - 1) / kTile);
-    const size_t tr = sizeof(float) * (NB * kLld + NB * kXld + NB);
-    hipLaunchKernelGGL(trsm_u12_kernel, dim3(g), dim3(256), tr, s, M, ldm, (int)k0, (int)(k0 + NB), (int)rest);
+    GELIM_TRY(factor_impl<double>(M, ldm, np, p->Dinv, static_cast<double*>(p->W), nullptr, p->info, s));
+  } else {
+    auto* M = static_cast<float*>(p->M);
+    hipLaunchKernelGGL(rbt_matrix_kernel<float>, grid, dim3(256), 0, s, aug, ld, (int)p->n, (int)np, p->ud, p->vd, M,
+                       ldm);
     HIP_TRY(hipGetLastError());
-    hipLaunchKernelGGL(trsm_l21_kernel, dim3(g), dim3(256), tr, s, M, ldm, (int)k0, (int)(k0 + NB), (int)rest);
-    HIP_TRY(hipGetLastError());
-    // A22 -= L21 U12 (fp32 MFMA, K = NB)
-    float* A22 = M + (k0 + NB) * ldm + k0 + NB;
-    GELIM_TRY(matmul_f32(M + (k0 + NB) * ldm + k0, ldm, M + k0 * ldm + k0 + NB, ldm, A22, ldm, rest, rest, NB, 1,
-                         GELIM_MM_MFMA, s, -1.0f));
+    GELIM_TRY(factor_impl<float>(M, ldm, np, p->Dinv, static_cast<float*>(p->W), static_cast<float*>(p->Tinv),
+                                 p->info, s));
   }
   int h_info = 0;
   HIP_TRY(hipMemcpyAsync(&h_info, p->info, 4, hipMemcpyDeviceToHost, s));
@@ -372,22 +577,55 @@ extern "C" int gelim_mixed_factor(gelim_mixed_plan* p, const double* aug, int64_
 }
 
 // d = V (LU)^-1 U^T [r; 0]: the correction of one refinement step (r, d:
-// n fp64 entries, r with stride incr).
+// n fp64 entries, r with stride incr).  fp64 arithmetic over the factors.
 extern "C" int gelim_mixed_apply(gelim_mixed_plan* p, const double* r, int64_t incr, double* d, void* stream) {
   using namespace gelim;
   if (!p || !r || !d) return GELIM_FAIL(GELIM_E_ARG, "mixed_apply: null argument");
   hipStream_t s = (hipStream_t)stream;
   const int64_t np = p->np, h = np / 4;
   const unsigned g = (unsigned)((h + 255) / 256);
-  hipLaunchKernelGGL(rbt_vec_kernel, dim3(g), dim3(256), 0, s, r, incr, (int)p->n, (int)np, p->ud, 1, p->c);
+  hipLaunchKernelGGL(rbt_vec_kernel, dim3(g), dim3(256), 0, s, r, incr, (int)p->n, (int)np, p->ud, 1, p->c, (int)np);
   HIP_TRY(hipGetLastError());
-  GELIM_TRY(fwdsub_unit_f32(p->M, p->ldm, p->c, p->y, np, p->z, p->flags, s));
-  GELIM_TRY(backsub_f32(p->M, p->ldm, p->y, 1, p->z, nullptr, np, 0, p->yw, s, nullptr, nullptr));
+  // c -> z (scratch), y (block-unit-lower result) -> c (the solution of the transformed system)
+  if (p->fp64)
+    GELIM_TRY(solve_impl<double>(static_cast<const double*>(p->M), p->ldm, np, p->Dinv, p->c, p->z, p->y, p->c,
+                                 p->flags, s));
+  else
+    GELIM_TRY(solve_impl<float>(static_cast<const float*>(p->M), p->ldm, np, p->Dinv, p->c, p->z, p->y, p->c,
+                                p->flags, s));
   // x = V z, only the first n entries are kept (the padding's are zero in exact arithmetic)
-  hipLaunchKernelGGL(rbt_vec_kernel, dim3(g), dim3(256), 0, s, p->z, (int64_t)1, (int)np, (int)np, p->vd, 0, p->c);
+  hipLaunchKernelGGL(rbt_vec_kernel, dim3(g), dim3(256), 0, s, p->c, (int64_t)1, (int)np, (int)np, p->vd, 0, d,
+                     (int)p->n);
   HIP_TRY(hipGetLastError());
-  HIP_TRY(hipMemcpyAsync(d, p->c, sizeof(double) * p->n, hipMemcpyDeviceToDevice, s));
   return GELIM_OK;
 }
 
+// Hand-off error word of the last solve (0: fine, 3: a bounded spin expired).
+extern "C" int gelim_mixed_solve_error(gelim_mixed_plan* p, void* stream) {
+  if (!p) return GELIM_FAIL(GELIM_E_ARG, "mixed_solve_error: null plan");
+  hipStream_t s = (hipStream_t)stream;
+  const int64_t nblk = p->np / gelim::NB;
+  (void)nblk;
+  HIP_TRY(hipMemcpyAsync(&p->err_host, p->flags + 2, 4, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  return p->err_host;
+}
+
 extern "C" int64_t gelim_mixed_plan_np(const gelim_mixed_plan* p) { return p ? p->np : 0; }
+
+// Device pointers of the plan's buffers (tests / debugging): out[0] = factor
+// (np x ldm), out[1] = diagonal-block inverses (nblk x 128 x 128 fp64),
+// out[2] = the W side buffer; returns ldm.
+extern "C" int64_t gelim_mixed_debug_ptrs(gelim_mixed_plan* p, void** out) {
+  if (!p || !out) return 0;
+  out[0] = p->M;
+  out[1] = p->Dinv;
+  out[2] = p->W;
+  return p->ldm;
+}
+
+// Synchronous device-to-device copy of `bytes` (tests: reading the buffers above).
+extern "C" int gelim_mixed_debug_copy(void* dst, const void* src, int64_t bytes) {
+  HIP_TRY(hipMemcpy(dst, src, (size_t)bytes, hipMemcpyDeviceToDevice));
+  return GELIM_OK;
+}

@@ -39,7 +39,7 @@ int backsub_f32(const float* U, int64_t ldu, const float* y, int64_t incy, doubl
 int dgemm(double* C, int64_t ldc, const double* A, int64_t lda, const double* B, int64_t ldb, int64_t M,
           int64_t N, int64_t K, double alpha, hipStream_t s);
 int dgemm_capped(double* C, int64_t ldc, const double* A, int64_t lda, const double* B, int64_t ldb, int64_t M,
-                 int64_t N, int64_t K, double alpha, int max_wg, hipStream_t s);
+                 int64_t N, int64_t K, double alpha, int max_wg, hipStream_t s, int accumulate = 1);
 namespace big {
 size_t workspace_bytes();
 int leaf_width();

@@ -20,20 +20,32 @@ __global__ __launch_bounds__(256) void copy2d_words_kernel(unsigned* __restrict_
 }
 
 // r[i] = aug[i][n] - sum_j aug[i][j] x[j] (fp64; one wave per row); with
-// matvec set, r[i] = sum_j aug[i][j] x[j] (the GMRES products of the mixed engine)
+// matvec set, r[i] = sum_j aug[i][j] x[j] (the GMRES products of the mixed
+// engine).  With w, also w[i] = |b_i| + sum_j |a_ij| |x_j| in the same pass
+// (the denominator of the componentwise backward error |r_i| / w_i).
 __global__ __launch_bounds__(256) void residual_kernel(const double* __restrict__ aug, int64_t ld, int n,
                                                        const double* __restrict__ x, double* __restrict__ r,
-                                                       int matvec) {
+                                                       int matvec, double* __restrict__ w) {
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= n) return;
   const double* a = aug + (int64_t)row * ld;
-  double s = 0.0;
-  for (int j = lane; j < n; j += 64) s = fma(a[j], x[j], s);
+  double s = 0.0, sa = 0.0;
+  if (w) {
+    for (int j = lane; j < n; j += 64) {
+      const double av = a[j], xv = x[j];
+      s = fma(av, xv, s);
+      sa = fma(fabs(av), fabs(xv), sa);
+    }
+    sa = dev::wave_sum(sa);
+  } else {
+    for (int j = lane; j < n; j += 64) s = fma(a[j], x[j], s);
+  }
   s = dev::wave_sum(s);
   if (lane == 0) {
     if (matvec) r[row] = s;
     else r[row] = a[n] - s;
+    if (w) w[row] = sa + (matvec ? 0.0 : fabs(a[n]));
   }
 }
 
@@ -115,8 +127,10 @@ int copy2d_async(void* dst, size_t dpitch, const void* src, size_t spitch, size_
   return GELIM_OK;
 }
 
-int residual_f64(const double* aug, int64_t ld, int64_t n, const double* x, double* r, hipStream_t s, int matvec) {
-  hipLaunchKernelGGL(residual_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, s, aug, ld, (int)n, x, r, matvec);
+int residual_f64(const double* aug, int64_t ld, int64_t n, const double* x, double* r, hipStream_t s, int matvec,
+                 double* w = nullptr) {
+  hipLaunchKernelGGL(residual_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, s, aug, ld, (int)n, x, r, matvec,
+                     w);
   HIP_TRY(hipGetLastError());
   return GELIM_OK;
 }
@@ -254,6 +268,13 @@ extern "C" int gelim_gpu_residual(const double* daug, int64_t ld, int64_t n, con
                                   void* stream) {
   if (n <= 0 || ld < n + 1) return GELIM_FAIL(GELIM_E_ARG, "residual: bad n / ld");
   return gelim::residual_f64(daug, ld, n, dx, dr, (hipStream_t)stream, 0);
+}
+
+// r = b - A x and w = |b| + |A| |x| in one pass (componentwise backward error).
+extern "C" int gelim_gpu_residual_cw(const double* daug, int64_t ld, int64_t n, const double* dx, double* dr,
+                                     double* dw, void* stream) {
+  if (n <= 0 || ld < n + 1 || !dw) return GELIM_FAIL(GELIM_E_ARG, "residual_cw: bad n / ld / w");
+  return gelim::residual_f64(daug, ld, n, dx, dr, (hipStream_t)stream, 0, dw);
 }
 
 // y = A x for the n x n matrix of an augmented fp64 system.

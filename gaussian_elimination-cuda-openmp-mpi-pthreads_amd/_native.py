@@ -77,6 +77,12 @@ _PROTOS = {
     "gelim_gpu_matvec": (_int, [_vp, _i64, _i64, _vp, _vp, _vp]),
     "gelim_mixed_padded": (_i64, [_i64]),
     "gelim_mixed_plan_create": (_vp, [_i64, _vp, _vp]),
+    "gelim_mixed_plan_create2": (_vp, [_i64, _vp, _vp, _int]),
+    "gelim_mixed_solve_error": (_int, [_vp, _vp]),
+    "gelim_mixed_debug_ptrs": (_i64, [_vp, _vp]),
+    "gelim_mixed_debug_copy": (_int, [_vp, _vp, _i64]),
+    "gelim_mixed_plan_np": (_i64, [_vp]),
+    "gelim_gpu_residual_cw": (_int, [_vp, _i64, _i64, _vp, _vp, _vp, _vp]),
     "gelim_mixed_plan_destroy": (None, [_vp]),
     "gelim_mixed_factor": (_int, [_vp, _vp, _i64, _vp]),
     "gelim_mixed_apply": (_int, [_vp, _vp, _i64, _vp, _vp]),

@@ -1,6 +1,8 @@
-"""The mixed-precision engine (GaussSolver backend "hip-mixed"): random
-butterfly transform + no-pivoting fp32 MFMA LU + fp64 iterative refinement
-with an automatic fp64 partial-pivoting fallback (csrc/hip/lu_mixed.hip).
+"""The randomised no-pivoting engines (GaussSolver backends "hip-mixed" and
+"hip-rbt"): random butterfly transform + no-pivoting MFMA LU (fp32 / fp64
+factors, triangular solves of the off-diagonal blocks as GEMMs with the
+diagonal blocks' inverses) + fp64 iterative refinement with an automatic fp64
+partial-pivoting fallback (csrc/hip/lu_mixed.hip).
 
 Oracles: the exact solution x_i = i + 1 of the random systems, the
 reference's fp64 `Error:` values of its .dat matrices and
@@ -76,6 +78,96 @@ def test_mixed_singular_raises(gelim, cuda):
     aug = gelim.random_system(n, seed=9, device=cuda)
     aug[:, 17] = 0.0
     s = gelim.GaussSolver(n, backend="hip-mixed", device=cuda)
+    with pytest.raises(gelim.SingularMatrixError):
+        s.solve(aug, check=True)
+    assert s.last_fallback is not None
+
+
+@pytest.mark.parametrize("backend", ["hip-mixed", "hip-rbt"])
+@pytest.mark.parametrize("n", [130, 1000])
+def test_diag_inverses_and_factor(gelim, cuda, backend, n):
+    """Every stored diagonal-block inverse (Gauss-Jordan, fp64) inverts the
+    Schur diagonal block the block-LDU factor left in place; fp64 oracle."""
+    import ctypes
+
+    aug = gelim.random_system(n, seed=3, device=cuda)
+    s = gelim.GaussSolver(n, backend=backend, device=cuda)
+    x = s.solve(aug, check=True)
+    assert s.last_fallback is None, s.last_fallback
+    lib = gelim._native.lib()
+    ptrs = (ctypes.c_void_p * 3)()
+    ldm = int(lib.gelim_mixed_debug_ptrs(s._mixed, ctypes.cast(ptrs, ctypes.c_void_p)))
+    np_ = int(lib.gelim_mixed_plan_np(s._mixed))
+    dt = torch.float64 if backend == "hip-rbt" else torch.float32
+
+    def view(addr, count, dtype=dt):
+        buf = torch.empty(count, dtype=dtype, device=cuda)
+        torch.cuda.synchronize()
+        gelim._native.check(lib.gelim_mixed_debug_copy(buf.data_ptr(), addr, count * buf.element_size()), "copy")
+        return buf
+
+    M = view(ptrs[0], np_ * ldm).view(np_, ldm)[:, :np_].double()
+    D = view(ptrs[1], np_ * 128, torch.float64).view(np_ // 128, 128, 128)
+    eye = torch.eye(128, dtype=torch.float64, device=cuda)
+    for b in range(np_ // 128):
+        blk = M[128 * b:128 * (b + 1), 128 * b:128 * (b + 1)]
+        # |D A - I| <= cond(A_bb) eps64-ish: without pivoting a Schur diagonal
+        # block of the transformed matrix can reach cond ~1e8
+        assert (D[b] @ blk - eye).abs().max().item() < 1e-6, b
+    assert gelim.ops.gauss.error_metric(x) < 1e-9
+    s.close()
+
+
+@pytest.mark.parametrize("n", [1, 100, 1000, 2048, 4000, 8192])
+def test_rbt_random_reaches_fp64(gelim, cuda, n):
+    """fp64 block-LDU factors: a few classic refinement steps (each
+    contracts the error by ~cond(A_bb) eps64 of the worst diagonal block)."""
+    aug = gelim.random_system(n, seed=n + 11, device=cuda)
+    s = gelim.GaussSolver(n, backend="hip-rbt", device=cuda)
+    x = s.solve(aug, check=True)
+    assert s.last_fallback is None, s.last_fallback
+    assert s.last_steps <= 5
+    ref = gelim.GaussSolver(n, backend="hip", device=cuda).solve(aug, check=True)
+    e_rbt = gelim.ops.gauss.error_metric(x)
+    e_fp64 = gelim.ops.gauss.error_metric(ref)
+    assert e_rbt <= max(10 * e_fp64, 1e-13), (e_rbt, e_fp64)
+    s.close()
+
+
+@pytest.mark.parametrize("name", ["jpwh_991", "sherman5", "orsreg_1", "sherman3", "saylr4"])
+def test_rbt_reference_matrices(gelim, cuda, name):
+    A = gelim.utils.io.load_fixture(name)
+    n = A.shape[0]
+    aug = gelim.augment_with_rhs(A).to(cuda)
+    s = gelim.GaussSolver(n, backend="hip-rbt", device=cuda)
+    x = s.solve(aug, check=True)
+    err = gelim.ops.gauss.error_metric(x)
+    assert err <= max(20 * GOLDEN_ERROR[name], 1e-13), (err, s.last_fallback, s.last_steps)
+
+
+def test_rbt_ill_conditioned_matches_torch(gelim, cuda):
+    """cond(A) = 1e12: fp64 factors still drive the refinement (or the
+    fallback takes over); either way x agrees with torch.linalg.solve to
+    ~cond * eps64."""
+    n = 512
+    g = torch.Generator(device=cuda).manual_seed(1)
+    Q1, _ = torch.linalg.qr(torch.randn(n, n, dtype=torch.float64, device=cuda, generator=g))
+    Q2, _ = torch.linalg.qr(torch.randn(n, n, dtype=torch.float64, device=cuda, generator=g))
+    A = (Q1 * torch.logspace(0, -12, n, dtype=torch.float64, device=cuda)) @ Q2
+    aug = torch.zeros(n, n + 8, dtype=torch.float64, device=cuda)
+    aug[:, :n] = A
+    aug[:, n] = A @ torch.arange(1, n + 1, dtype=torch.float64, device=cuda)
+    s = gelim.GaussSolver(n, backend="hip-rbt", device=cuda)
+    x = s.solve(aug, check=True)
+    ref = torch.linalg.solve(A, aug[:, n])
+    assert ((x - ref).abs().max() / ref.abs().max()).item() < 1e-3
+
+
+def test_rbt_singular_raises(gelim, cuda):
+    n = 256
+    aug = gelim.random_system(n, seed=9, device=cuda)
+    aug[:, 17] = 0.0
+    s = gelim.GaussSolver(n, backend="hip-rbt", device=cuda)
     with pytest.raises(gelim.SingularMatrixError):
         s.solve(aug, check=True)
     assert s.last_fallback is not None

@@ -22,6 +22,12 @@ between device syncs + barriers, max over ranks):
   dist_matmul_16384(_s) 16384^2 fp32 over ALL N ranks (strong scaling)
   gauss_8192_1gpu(_s)   one 8192^2 system per GPU on the single-GPU solver
   hip_pivot_2048        the per-pivot algorithm (fp64, fp32)
+  gauss_rbt             the randomised no-pivoting engines at 2048 / 8192: hip-rbt
+                        (butterfly transform + fp64 block-LDU on the matrix cores +
+                        fp64 refinement to a componentwise backward error <= 4 eps)
+                        and hip-mixed (same with fp32 trailing products + GMRES-IR);
+                        fp64-class answers by a different algorithm than the
+                        headline's partial pivoting, so reported beside it
   external_matrices     the reference's .dat matrices vs its best OpenMP times
   host_seq              sequential denominators (stored unless --measure-seq;
                         the field says which)
@@ -261,12 +267,19 @@ def main() -> None:
         # past the round-2 cap of 32768 rows per leaf (8.6 GB per system)
         _section(result, "gauss_32768_1gpu", lambda: bench_single(comm, gelim, torch, 32768, seed=78 + rank, reps=1))
         _section(result, "hip_pivot_2048", lambda: bench_pivot(comm, gelim, torch, n))
+        _section(result, "gauss_rbt", lambda: bench_rbt(comm, gelim, torch))
         _section(result, "external_matrices", lambda: bench_external(comm, gelim, torch))
     for key, short in (("dist_gauss_8192", "dist_gauss_8192_s"), ("dist_matmul_16384", "dist_matmul_16384_s"),
                        ("gauss_8192_1gpu", "gauss_8192_1gpu_s"), ("gauss_32768_1gpu", "gauss_32768_1gpu_s")):
         v = result.get(key)
         if isinstance(v, dict) and "time_s" in v:
             result[short] = v["time_s"]
+    rb = result.get("gauss_rbt")
+    if isinstance(rb, dict):
+        for nn in ("2048", "8192"):
+            v = rb.get(nn, {}).get("hip-rbt")
+            if isinstance(v, dict) and "time_s" in v:
+                result[f"gauss_{nn}_rbt_s"] = v["time_s"]
     dm = result.get("dist_matmul_16384")
     if isinstance(dm, dict) and "summa" in dm:
         result["dist_matmul_16384_summa_s"] = dm["summa"]["time_s"]
@@ -397,6 +410,29 @@ def bench_single(comm, gelim, torch, n: int, seed: int, reps: int = 3) -> dict:
            "error": gelim.ops.gauss.error_metric(holder["x"]), "singular": s.info() != 0}
     s.close()
     return res
+
+
+def bench_rbt(comm, gelim, torch) -> dict:
+    """Randomised no-pivoting engines (each rank its own system): the whole
+    solve (transform, factorisation, refinement) per call, with the
+    refinement's correction count, its final componentwise backward error and
+    whether it fell back to partial pivoting."""
+    dev = comm.device
+    out = {}
+    for n in (2048, 8192):
+        aug = gelim.random_system(n, seed=31 + n, device=dev)
+        res = {}
+        for backend in ("hip-rbt", "hip-mixed"):
+            s = gelim.GaussSolver(n, backend=backend, device=dev)
+            holder = {}
+            s.solve(aug)
+            dt = _timed(comm, torch, dev, lambda: holder.__setitem__("x", s.solve(aug)), reps=3)
+            res[backend] = {"time_s": dt, "error": gelim.ops.gauss.error_metric(holder["x"]),
+                            "corrections": s.last_steps, "gmres_iterations": s.last_inner,
+                            "backward_error": s.last_berr, "fallback": s.last_fallback}
+            s.close()
+        out[str(n)] = res
+    return out
 
 
 def bench_pivot(comm, gelim, torch, n: int) -> dict:

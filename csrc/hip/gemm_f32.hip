@@ -36,6 +36,7 @@ struct Mat {
   int64_t ldc;
   int M, N, K, acc;
   float alpha;  // MFMA path: C (+)= alpha * A B (the blocked no-pivot LU's update passes -1)
+  double* C64 = nullptr;  // MFMA path: an fp64 C instead (fp32 products, fp64 accumulation in C)
 };
 
 __global__ void naive_row_kernel(Mat p) {
@@ -219,9 +220,14 @@ __global__ __launch_bounds__(kMmThreads, 2) void mfma_gemm_kernel(Mat p, int til
       for (int r = 0; r < 16; ++r) {
         const int row = m0 + wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * kh;
         if (!CHECK || (row < M && col < N)) {
-          float* c = p.C + (int64_t)row * p.ldc + col;
           const float v = p.alpha * acc[i][j][r];
-          *c = p.acc ? *c + v : v;
+          if (p.C64) {
+            double* c = p.C64 + (int64_t)row * p.ldc + col;
+            *c = p.acc ? *c + (double)v : (double)v;
+          } else {
+            float* c = p.C + (int64_t)row * p.ldc + col;
+            *c = p.acc ? *c + v : v;
+          }
         }
       }
     }
@@ -235,13 +241,15 @@ struct Shape {
 }  // namespace
 
 int matmul_f32(const float* A, int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc,
-               int64_t M, int64_t N, int64_t K, int accumulate, int kernel, hipStream_t s, float alpha) {
+               int64_t M, int64_t N, int64_t K, int accumulate, int kernel, hipStream_t s, float alpha,
+               double* C64 = nullptr) {
   if (M <= 0 || N <= 0 || K <= 0) return GELIM_FAIL(GELIM_E_ARG, "matmul: bad shape");
   if (alpha != 1.0f && kernel != GELIM_MM_MFMA) return GELIM_FAIL(GELIM_E_ARG, "matmul: alpha needs the MFMA kernel");
   if (M > INT32_MAX || N > INT32_MAX || K > INT32_MAX)
     return GELIM_FAIL(GELIM_E_ARG, "matmul: dimension exceeds 2^31");
   if (lda < K || ldb < N || ldc < N) return GELIM_FAIL(GELIM_E_ARG, "matmul: leading dimension too small");
-  Mat p{A, lda, B, ldb, C, ldc, (int)M, (int)N, (int)K, accumulate, alpha};
+  if (C64 && kernel != GELIM_MM_MFMA) return GELIM_FAIL(GELIM_E_ARG, "matmul: an fp64 C needs the MFMA kernel");
+  Mat p{A, lda, B, ldb, C, ldc, (int)M, (int)N, (int)K, accumulate, alpha, C64};
   switch (kernel) {
     case GELIM_MM_NAIVE_ROW: {
       const int threads = (int)std::min<int64_t>(1024, N);

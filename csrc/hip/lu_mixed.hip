@@ -59,7 +59,7 @@
 
 namespace gelim {
 int matmul_f32(const float* A, int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc, int64_t M, int64_t N,
-               int64_t K, int accumulate, int kernel, hipStream_t s, float alpha);
+               int64_t K, int accumulate, int kernel, hipStream_t s, float alpha, double* C64);
 int dgemm_ex(double* C, int64_t ldc, const double* A, int64_t lda, const double* B, int64_t ldb, int64_t M,
              int64_t N, int64_t K, double alpha, int accumulate, hipStream_t s);
 
@@ -174,8 +174,11 @@ __global__ __launch_bounds__(256) void rbt_vec_kernel(const double* __restrict__
 // are published raw through parity-buffered LDS one step ahead (one barrier
 // per step), and the step loop is unrolled by 8 so every in-tile index (k % 8)
 // is static: publishing is a predicated store, not a register pick.  ~500
-// cycles per step, 128 steps (the earlier LU + two triangular-inverse loops
-// with one row per lane: 330 us per block, instruction-bound).
+// cycles per step, 128 steps: 72 us per block (the earlier LU + two
+// triangular-inverse loops with one row per lane: 330 us, instruction-bound;
+// a 4-column blocked Gauss-Jordan step -- explicit 4 x 4 pivot-block inverse,
+// rank-4 update -- was slower, 81 us, and lost accuracy: refinement needed
+// more corrections and fell back at n >= 4096).
 constexpr int kGT = 256;  // threads
 constexpr int kTl = 8;    // tile edge
 
@@ -417,26 +420,47 @@ __global__ __launch_bounds__(kDT) void blk_trsv_kernel(const T* __restrict__ F, 
   if (t == 0) __hip_atomic_store(done, (unsigned)(w + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Block LDU factorisation of the transformed matrix in place: per block k,
-// Dinv_k = A_kk^-1, W = A_kk^-1 A_k,rest (side buffer), A_rest,rest -= A_rest,k W.
-template <typename T>
-int factor_impl(T* M, int64_t ldm, int64_t np, double* Dinv, T* W, T* Tinv, int* info, hipStream_t s) {
+// Rounded fp32 copy of a rows x cols fp64 block (the fp32 engine's GEMM operands).
+__global__ __launch_bounds__(256) void to_f32_kernel(const double* __restrict__ src, int64_t sld,
+                                                    float* __restrict__ dst, int64_t dld, int cols) {
+  const int64_t r = blockIdx.y;
+  for (int c = blockIdx.x * 256 + threadIdx.x; c < cols; c += gridDim.x * 256)
+    dst[r * dld + c] = (float)src[r * sld + c];
+}
+
+int to_f32(const double* src, int64_t sld, float* dst, int64_t dld, int64_t rows, int64_t cols, hipStream_t s) {
+  const unsigned gx = (unsigned)std::min<int64_t>((cols + 255) / 256, 64);
+  hipLaunchKernelGGL(to_f32_kernel, dim3(gx, (unsigned)rows), dim3(256), 0, s, src, sld, dst, dld, (int)cols);
+  HIP_TRY(hipGetLastError());
+  return GELIM_OK;
+}
+
+// Block LDU factorisation of the transformed (fp64) matrix in place: per
+// block k, Dinv_k = A_kk^-1 (fp64 Gauss-Jordan), W = A_kk^-1 A_k,rest (fp64
+// MFMA), A_rest,rest -= A_rest,k W -- on the fp64 matrix cores, or (A21f /
+// Wf given: the fp32 engine) as an fp32 MFMA product of rounded copies
+// accumulated into the fp64 matrix.  Only that O(n^3) product is fp32: the
+// inverses and W stay fp64, so a badly conditioned diagonal block costs
+// cond * eps64, not cond * eps32.
+int factor_impl(double* M, int64_t ldm, int64_t np, double* Dinv, double* W, float* A21f, float* Wf, int* info,
+                hipStream_t s) {
   for (int64_t k0 = 0; k0 < np; k0 += NB) {
     double* Di = Dinv + (k0 / NB) * NB * NB;
-    hipLaunchKernelGGL(diag_inv_kernel<T>, dim3(1), dim3(kGT), 0, s, M, ldm, (int)k0, Di,
-                       sizeof(T) == 8 ? (T*)nullptr : Tinv, info);
+    hipLaunchKernelGGL(diag_inv_kernel<double>, dim3(1), dim3(kGT), 0, s, M, ldm, (int)k0, Di, (double*)nullptr,
+                       info);
     HIP_TRY(hipGetLastError());
     const int64_t rest = np - k0 - NB;
     if (rest <= 0) break;
-    T* A12 = M + k0 * ldm + k0 + NB;
-    T* A21 = M + (k0 + NB) * ldm + k0;
-    T* A22 = M + (k0 + NB) * ldm + k0 + NB;
-    if constexpr (sizeof(T) == 8) {
-      GELIM_TRY(dgemm_ex(W, rest, Di, NB, A12, ldm, NB, rest, NB, 1.0, 0, s));        // W = A11^-1 A12
+    double* A12 = M + k0 * ldm + k0 + NB;
+    double* A21 = M + (k0 + NB) * ldm + k0;
+    double* A22 = M + (k0 + NB) * ldm + k0 + NB;
+    GELIM_TRY(dgemm_ex(W, rest, Di, NB, A12, ldm, NB, rest, NB, 1.0, 0, s));  // W = A11^-1 A12
+    if (!A21f) {
       GELIM_TRY(dgemm_ex(A22, ldm, A21, ldm, W, rest, rest, rest, NB, -1.0, 1, s));  // A22 -= A21 W
     } else {
-      GELIM_TRY(matmul_f32(Tinv, NB, A12, ldm, W, rest, NB, rest, NB, 0, GELIM_MM_MFMA, s, 1.0f));
-      GELIM_TRY(matmul_f32(A21, ldm, W, rest, A22, ldm, rest, rest, NB, 1, GELIM_MM_MFMA, s, -1.0f));
+      GELIM_TRY(to_f32(A21, ldm, A21f, NB, rest, NB, s));
+      GELIM_TRY(to_f32(W, rest, Wf, rest, NB, rest, s));
+      GELIM_TRY(matmul_f32(A21f, NB, Wf, rest, nullptr, ldm, rest, rest, NB, 1, GELIM_MM_MFMA, s, -1.0f, A22));
     }
   }
   return GELIM_OK;
@@ -475,10 +499,11 @@ int solve_impl(const T* M, int64_t ldm, int64_t np, const double* Dinv, const do
 struct gelim_mixed_plan {
   int64_t n = 0, np = 0, ldm = 0;
   int fp64 = 0;             // factor precision: 0 fp32 ("hip-mixed"), 1 fp64 ("hip-rbt")
-  void* M = nullptr;        // np x ldm: the transformed matrix, then its block-LDU factor
-  double* Dinv = nullptr;   // nblk x NB x NB: inverse of every (Schur) diagonal block, fp64
-  void* W = nullptr;        // NB x np: A_kk^-1 A_k,rest of the current block
-  void* Tinv = nullptr;     // NB x NB: fp32 copy of the current inverse (fp32 engine)
+  double* M = nullptr;      // np x ldm: the transformed matrix, then its block-LDU factor
+  double* Dinv = nullptr;   // nblk x NB x NB: inverse of every (Schur) diagonal block
+  double* W = nullptr;      // NB x np: A_kk^-1 A_k,rest of the current block
+  float* A21f = nullptr;    // np x NB, NB x np: rounded GEMM operands (fp32 engine only)
+  float* Wf = nullptr;
   double* ud = nullptr;     // U's butterfly diagonals (8 x np/4)
   double* vd = nullptr;     // V's
   unsigned* flags = nullptr;  // solve counters (lower, upper) + error word
@@ -493,7 +518,8 @@ extern "C" int64_t gelim_mixed_max_n(void) { return (int64_t)gelim::kMaxBlocks *
 
 extern "C" void gelim_mixed_plan_destroy(gelim_mixed_plan* p) {
   if (!p) return;
-  for (void* q : {p->M, (void*)p->Dinv, p->W, p->Tinv, (void*)p->ud, (void*)p->vd, (void*)p->flags, (void*)p->c,
+  for (void* q : {(void*)p->M, (void*)p->Dinv, (void*)p->W, (void*)p->A21f, (void*)p->Wf, (void*)p->ud, (void*)p->vd,
+                  (void*)p->flags, (void*)p->c,
                   (void*)p->y, (void*)p->z, (void*)p->info})
     (void)hipFree(q);
   delete p;
@@ -515,8 +541,7 @@ extern "C" gelim_mixed_plan* gelim_mixed_plan_create2(int64_t n, const double* u
   p->n = n;
   p->np = np;
   p->fp64 = fp64 ? 1 : 0;
-  const size_t es = fp64 ? 8 : 4;
-  p->ldm = np + (fp64 ? 2 : 4);  // 16-byte rows, off the power-of-two stride
+  p->ldm = np + 2;  // 16-byte rows, off the power-of-two stride
   auto fail = [&](const char* what) -> gelim_mixed_plan* {
     GELIM_FAIL(GELIM_E_NOMEM, std::string("mixed plan: ") + what);
     gelim_mixed_plan_destroy(p);
@@ -524,10 +549,11 @@ extern "C" gelim_mixed_plan* gelim_mixed_plan_create2(int64_t n, const double* u
   };
   const size_t nd = (size_t)2 * np;  // 8 arrays of np/4
   const int64_t nblk = np / gelim::NB;
-  if (hipMalloc(&p->M, es * (size_t)np * p->ldm) != hipSuccess) return fail("matrix");
+  if (hipMalloc((void**)&p->M, sizeof(double) * (size_t)np * p->ldm) != hipSuccess) return fail("matrix");
   if (hipMalloc((void**)&p->Dinv, sizeof(double) * (size_t)np * gelim::NB) != hipSuccess) return fail("inverses");
-  if (hipMalloc(&p->W, es * (size_t)np * gelim::NB) != hipSuccess) return fail("W buffer");
-  if (!fp64 && hipMalloc(&p->Tinv, es * (size_t)gelim::NB * gelim::NB) != hipSuccess) return fail("fp32 inverse");
+  if (hipMalloc((void**)&p->W, sizeof(double) * (size_t)np * gelim::NB) != hipSuccess) return fail("W buffer");
+  if (!fp64 && hipMalloc((void**)&p->A21f, sizeof(float) * (size_t)np * gelim::NB) != hipSuccess) return fail("A21f");
+  if (!fp64 && hipMalloc((void**)&p->Wf, sizeof(float) * (size_t)np * gelim::NB) != hipSuccess) return fail("Wf");
   if (hipMalloc((void**)&p->ud, sizeof(double) * nd) != hipSuccess) return fail("ud");
   if (hipMalloc((void**)&p->vd, sizeof(double) * nd) != hipSuccess) return fail("vd");
   (void)nblk;
@@ -556,20 +582,11 @@ extern "C" int gelim_mixed_factor(gelim_mixed_plan* p, const double* aug, int64_
   const int64_t np = p->np, h = np / 4, ldm = p->ldm;
   HIP_TRY(hipMemsetAsync(p->info, 0x7f, 4, s));  // INT_MAX-ish: atomicMin keeps the first bad column
   const dim3 grid((unsigned)((h + 255) / 256), (unsigned)h);
-  if (p->fp64) {
-    auto* M = static_cast<double*>(p->M);
-    hipLaunchKernelGGL(rbt_matrix_kernel<double>, grid, dim3(256), 0, s, aug, ld, (int)p->n, (int)np, p->ud, p->vd, M,
-                       ldm);
-    HIP_TRY(hipGetLastError());
-    GELIM_TRY(factor_impl<double>(M, ldm, np, p->Dinv, static_cast<double*>(p->W), nullptr, p->info, s));
-  } else {
-    auto* M = static_cast<float*>(p->M);
-    hipLaunchKernelGGL(rbt_matrix_kernel<float>, grid, dim3(256), 0, s, aug, ld, (int)p->n, (int)np, p->ud, p->vd, M,
-                       ldm);
-    HIP_TRY(hipGetLastError());
-    GELIM_TRY(factor_impl<float>(M, ldm, np, p->Dinv, static_cast<float*>(p->W), static_cast<float*>(p->Tinv),
-                                 p->info, s));
-  }
+  hipLaunchKernelGGL(rbt_matrix_kernel<double>, grid, dim3(256), 0, s, aug, ld, (int)p->n, (int)np, p->ud, p->vd,
+                     p->M, ldm);
+  HIP_TRY(hipGetLastError());
+  GELIM_TRY(factor_impl(p->M, ldm, np, p->Dinv, p->W, p->fp64 ? nullptr : p->A21f, p->fp64 ? nullptr : p->Wf, p->info,
+                        s));
   int h_info = 0;
   HIP_TRY(hipMemcpyAsync(&h_info, p->info, 4, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
@@ -587,12 +604,7 @@ extern "C" int gelim_mixed_apply(gelim_mixed_plan* p, const double* r, int64_t i
   hipLaunchKernelGGL(rbt_vec_kernel, dim3(g), dim3(256), 0, s, r, incr, (int)p->n, (int)np, p->ud, 1, p->c, (int)np);
   HIP_TRY(hipGetLastError());
   // c -> z (scratch), y (block-unit-lower result) -> c (the solution of the transformed system)
-  if (p->fp64)
-    GELIM_TRY(solve_impl<double>(static_cast<const double*>(p->M), p->ldm, np, p->Dinv, p->c, p->z, p->y, p->c,
-                                 p->flags, s));
-  else
-    GELIM_TRY(solve_impl<float>(static_cast<const float*>(p->M), p->ldm, np, p->Dinv, p->c, p->z, p->y, p->c,
-                                p->flags, s));
+  GELIM_TRY(solve_impl<double>(p->M, p->ldm, np, p->Dinv, p->c, p->z, p->y, p->c, p->flags, s));
   // x = V z, only the first n entries are kept (the padding's are zero in exact arithmetic)
   hipLaunchKernelGGL(rbt_vec_kernel, dim3(g), dim3(256), 0, s, p->c, (int64_t)1, (int)np, (int)np, p->vd, 0, d,
                      (int)p->n);

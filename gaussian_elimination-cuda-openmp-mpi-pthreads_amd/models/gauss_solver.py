@@ -202,7 +202,7 @@ class GaussSolver:
         _native.check(lib.gelim_mixed_apply(self._mixed, ptr(b), ld, ptr(x), sh), "mixed_apply")
         # componentwise backward error w = max_i |r_i| / (|b| + |A||x|)_i (one
         # native pass gives r and the denominator): refine until w <= 4 eps64;
-        # once a correction stops halving it, accept w <= sqrt(n) eps64.  A
+        # once a correction stops reducing it by 10 %, accept w <= sqrt(n) eps64.  A
         # norm-wise test (LAPACK dsgesv's ||r|| <= sqrt(n) eps ||A|| ||x||) is
         # too weak for badly row-scaled systems: on sherman3 it accepted an x
         # whose error was ~2e3 (a row of scale 1e10 dominates ||A||).
@@ -218,7 +218,7 @@ class GaussSolver:
             self.last_berr = om
             if om <= strict:
                 return x
-            if not om < 0.5 * prev or it == max_steps:  # NaN, stagnated or out of steps
+            if not om < 0.9 * prev or it == max_steps:  # NaN, stagnated or out of steps
                 if best is not None and best[0] <= loose:
                     self.last_berr = best[0]
                     return best[1]

@@ -4,7 +4,7 @@ set -u
 OUT="${GRAFT_REPO_ROOT:-.}/gpurun_out"
 mkdir -p "$OUT"
 run() { local t=$1; shift; timeout -k 10 "$t" "$@"; local rc=$?; if [ $rc -ne 0 ]; then echo "FAILED rc=$rc: $*"; exit $rc; fi; }
-timeout -k 10 400 python -u -m pytest tests/test_gpu_mixed.py -v --timeout 120 --timeout-method thread -k "rbt or diag" > "$OUT/mixed_d.log" 2>&1; prc=$?; echo "pytest rc=$prc"; [ $prc -gt 1 ] && exit $prc; grep -E "PASS|FAIL|Error|assert" "$OUT/mixed_d.log" | head -60
+timeout -k 10 400 python -u -m pytest tests/test_gpu_mixed.py -v --timeout 120 --timeout-method thread > "$OUT/mixed_d.log" 2>&1; prc=$?; echo "pytest rc=$prc"; [ $prc -gt 1 ] && exit $prc; grep -E "PASS|FAIL|Error|assert" "$OUT/mixed_d.log" | head -60
 tail -3 "$OUT/mixed_d.log"
 run 200 python -u scripts/mixed_breakdown.py --backend hip-rbt 2048 4096 8192 16384
 run 200 python -u scripts/mixed_breakdown.py --backend hip-mixed 2048 4096 8192

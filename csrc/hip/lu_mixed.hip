@@ -192,7 +192,13 @@ template <int KK>
 __device__ __forceinline__ void gj_step(double (&a)[kTl][kTl], GjLds<double>& sh, int kg, int rg, int cg) {
   const int k = kTl * kg + KK;
   constexpr int par = KK & 1;  // kTl is even: k and KK share parity
-  const double pk = 1.0 / sh.row[par][k];
+  // 1 / pivot: v_rcp_f64 + two Newton steps (within an ulp of the IEEE
+  // quotient; the refinement absorbs the rest) -- 3 dependent FMAs instead of
+  // the ~8-deep IEEE division sequence on the critical path of every column
+  const double piv = sh.row[par][k];
+  double pk = __builtin_amdgcn_rcp(piv);
+  pk = fma(pk, fma(-piv, pk, 1.0), pk);
+  pk = fma(pk, fma(-piv, pk, 1.0), pk);
   double u[kTl], g[kTl];
 #pragma unroll
   for (int j = 0; j < kTl; j += 2) {
@@ -208,25 +214,31 @@ __device__ __forceinline__ void gj_step(double (&a)[kTl][kTl], GjLds<double>& sh
   }
   u[KK] = (cg == kg) ? 1.0 + pk : u[KK];
   g[KK] -= (rg == kg) ? 1.0 : 0.0;
+  constexpr int kk1 = (KK + 1) % kTl;
+  const int kg1 = KK + 1 == kTl ? kg + 1 : kg;
+  const bool more = k + 1 < NB;
+  // the next step's pivot row / column first: their LDS stores then drain
+  // under the bulk of the update instead of after it
+#pragma unroll
+  for (int j = 0; j < kTl; ++j) a[kk1][j] = fma(-g[kk1], u[j], a[kk1][j]);
+#pragma unroll
+  for (int i = 0; i < kTl; ++i)
+    if (i != kk1) a[i][kk1] = fma(-g[i], u[kk1], a[i][kk1]);
+  if (more && rg == kg1) {
+#pragma unroll
+    for (int j = 0; j < kTl; j += 2)
+      *reinterpret_cast<double2*>(&sh.row[par ^ 1][kTl * cg + j]) = make_double2(a[kk1][j], a[kk1][j + 1]);
+  }
+  if (more && cg == kg1) {
+#pragma unroll
+    for (int i = 0; i < kTl; i += 2)
+      *reinterpret_cast<double2*>(&sh.col[par ^ 1][kTl * rg + i]) = make_double2(a[i][kk1], a[i + 1][kk1]);
+  }
 #pragma unroll
   for (int i = 0; i < kTl; ++i)
 #pragma unroll
-    for (int j = 0; j < kTl; ++j) a[i][j] = fma(-g[i], u[j], a[i][j]);
-  // publish step k + 1 (raw row / column of the updated block)
-  if (k + 1 < NB) {
-    constexpr int kk1 = (KK + 1) % kTl;
-    const int kg1 = KK + 1 == kTl ? kg + 1 : kg;
-    if (rg == kg1) {
-#pragma unroll
-      for (int j = 0; j < kTl; j += 2)
-        *reinterpret_cast<double2*>(&sh.row[par ^ 1][kTl * cg + j]) = make_double2(a[kk1][j], a[kk1][j + 1]);
-    }
-    if (cg == kg1) {
-#pragma unroll
-      for (int i = 0; i < kTl; i += 2)
-        *reinterpret_cast<double2*>(&sh.col[par ^ 1][kTl * rg + i]) = make_double2(a[i][kk1], a[i + 1][kk1]);
-    }
-  }
+    for (int j = 0; j < kTl; ++j)
+      if (i != kk1 && j != kk1) a[i][j] = fma(-g[i], u[j], a[i][j]);
   __syncthreads();
 }
 

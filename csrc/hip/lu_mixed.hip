@@ -34,7 +34,9 @@
 // chain order (the next block's factor loads in flight under the current
 // block's FMAs), then multiplies by the stored inverse -- a mat-vec, not a
 // 128-step chain -- in fp64 arithmetic over the T factor, and publishes its
-// block (agent-scope stores, drain, barrier, one chain counter).  Spins are
+// block as plain agent-scope stores into a buffer pre-filled with a
+// signalling-NaN sentinel: the consumer polls the values themselves, so a
+// hand-off is one store + one load (no drain, barrier or flag).  Spins are
 // bounded (200 ms) and report through an error word.
 //
 // Depth-2 recursive butterfly: W = L1 L0, L0 = B<n> = 1/sqrt2 [R S; R -S]
@@ -44,13 +46,14 @@
 // i + 3h} (h = n/4) as one 4 x 4 matrix W_i, so M = U^T A V is ONE pass over
 // A: every 4 x 4 group of entries becomes U_i^T A_g V_j.  The system is
 // padded to np = a multiple of 128 with an identity block (b padded with
-// zeros).  Storage: L (unit lower, below the diagonal) and U (on and above it)
-// overwrite the transformed matrix, LAPACK style.
+// zeros).  Storage: the block-LDU factor overwrites the transformed matrix
+// (diagonal blocks unused, their inverses in Dinv).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
 #include <cmath>
 #include <cstdint>
+#include <cstdlib>
 #include <string>
 #include <utility>
 
@@ -62,6 +65,8 @@ int matmul_f32(const float* A, int64_t lda, const float* B, int64_t ldb, float* 
                int64_t K, int accumulate, int kernel, hipStream_t s, float alpha, double* C64);
 int dgemm_ex(double* C, int64_t ldc, const double* A, int64_t lda, const double* B, int64_t ldb, int64_t M,
              int64_t N, int64_t K, double alpha, int accumulate, hipStream_t s);
+int dgemm_capped(double* C, int64_t ldc, const double* A, int64_t lda, const double* B, int64_t ldb, int64_t M,
+                 int64_t N, int64_t K, double alpha, int max_wg, hipStream_t s, int accumulate);
 
 namespace {
 
@@ -307,47 +312,70 @@ __device__ __forceinline__ double bcast_lane(double v, int l) {
                                         (unsigned)__builtin_amdgcn_readlane((int)b, l));
 }
 
-// x = F^-1 c for the unit-lower (UPPER = false) or upper (UPPER = true)
-// triangle of the factor F (np x np, ldf), with the diagonal blocks' inverses
-// Dinv (nblk x NB x NB fp64, row-major).  Workgroup w handles block row b = w
-// (lower) or nblk - 1 - w (upper): chain position w, so the first block of the
-// chain is the first workgroup dispatched.  Blocks are solved strictly in
-// chain order, so ONE counter (`done` = blocks solved) replaces per-block
-// flags: a workgroup polls only when it has consumed every block the counter
-// promised, and otherwise streams through the solved blocks with the next
-// block's factor loads in flight under the current block's FMAs (a poll is an
-// atomic load, whose wait would drain every outstanding load).  Thread (r, q):
+// x = F^-1 c for the block-unit-lower (UPPER = false) or block-upper (UPPER =
+// true) part of the block-LDU factor F (np x np, ldf), with the diagonal
+// blocks' inverses Dinv (nblk x NB x NB fp64, row-major).  Workgroup w handles
+// block row b = w (lower) or nblk - 1 - w (upper): chain position w, so the
+// first block of the chain is the first workgroup dispatched.  Thread (r, q):
 // equation 128 b + r, columns 32 q .. 32 q + 31 of every 128-column block.
+//
+// Hand-off: x is pre-filled with kSentinel (a signalling NaN no arithmetic
+// produces); a producer stores its 128 values with agent-scope stores and is
+// done, a consumer's lanes load the 32 values of their quarter and spin until
+// none is the sentinel -- one store + one load per hand-off, where a flag
+// needed store + drain + barrier + flag store + flag poll + value load.
+constexpr uint64_t kSentinel = 0x7ff4dead0badf00dull;
+
 template <typename T>
 __device__ __forceinline__ void load_blk(T (&u)[kQW], const T* __restrict__ p) {
 #pragma unroll
   for (int j = 0; j < kQW; ++j) u[j] = p[j];
 }
 
-__device__ __forceinline__ int poll_done(const unsigned* done, int need, int* err) {
-  int got = 0;
-  if (__lane_id() == 0) {
-    unsigned v = __hip_atomic_load(done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if ((int)v < need) {
-      const unsigned long long t0 = rtc();
-      while ((int)(v = __hip_atomic_load(done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) < need) {
-        if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0 || rtc() - t0 > kSpinTicks) {
-          __hip_atomic_store(err, 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          v = 0;
-          break;
-        }
+// Lanes 0..31 of the calling wave poll the published values x[idx + lane]
+// in two parts: issue_x sends the first load, settle_x spins until none is
+// the sentinel (lanes 32..63 return 0).  The next block's factor loads are
+// issued BETWEEN the two, so the first wait is vmcnt(#factor loads): VMEM
+// loads return in order, and a value load issued after the prefetch would
+// drain it (one HBM latency per block for a workgroup catching up on many
+// already-solved blocks).  settle_x returns false (wave-uniform) when the
+// bounded spin expired or another workgroup reported an error.
+__device__ __forceinline__ unsigned long long issue_x(const double* __restrict__ x, int idx) {
+  const int lane = __lane_id();
+  const unsigned long long* p = reinterpret_cast<const unsigned long long*>(x + idx + (lane & (kQW - 1)));
+  const unsigned long long v = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __builtin_amdgcn_sched_barrier(0);  // keep the prefetch that follows after this load
+  return v;
+}
+
+__device__ __forceinline__ bool settle_x(const double* __restrict__ x, int idx, unsigned long long v, int* err,
+                                         double& out, bool nap) {
+  const int lane = __lane_id();
+  bool ok = true;
+  if (__ballot(lane < kQW && v == kSentinel) != 0) {
+    const unsigned long long* p = reinterpret_cast<const unsigned long long*>(x + idx + (lane & (kQW - 1)));
+    const unsigned long long t0 = rtc();
+    while (__ballot(lane < kQW && v == kSentinel) != 0) {
+      // workgroups further down the chain back off: every waiting wave polls
+      // the same two cache lines, and only the next block's owner is urgent
+      if (nap) __builtin_amdgcn_s_sleep(2);
+      if (lane < kQW && v == kSentinel) v = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (rtc() - t0 > kSpinTicks || __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) {
+        if (lane == 0) __hip_atomic_store(err, 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ok = false;
+        break;
       }
     }
-    got = (int)v;
   }
-  return __shfl(got, 0);
+  out = lane < kQW ? __builtin_bit_cast(double, v) : 0.0;
+  return ok;
 }
 
 template <typename T, bool UPPER>
 __global__ __launch_bounds__(kDT) void blk_trsv_kernel(const T* __restrict__ F, int64_t ldf,
                                                       const double* __restrict__ Dinv, const double* __restrict__ c,
                                                       double* __restrict__ x, double* __restrict__ ysave, int nblk,
-                                                      unsigned* __restrict__ done, int* __restrict__ err) {
+                                                      int* __restrict__ err) {
   __shared__ double part[4][NB];
   __shared__ double rb[NB];
   __shared__ int bad;
@@ -366,45 +394,29 @@ __global__ __launch_bounds__(kDT) void blk_trsv_kernel(const T* __restrict__ F, 
   }
   const double cv = c[row];
   double acc = 0.0;
-  int avail = 0;
   const T* frow = F + (int64_t)row * ldf + kQW * q;
   auto blk = [&](int i) { return frow + (int64_t)NB * (UPPER ? nblk - 1 - i : i); };
+  auto xidx = [&](int i) { return NB * (UPPER ? nblk - 1 - i : i) + kQW * q; };
   bool ok = true;
   T ua[kQW], ub[kQW];
   if (w > 0) load_blk(ua, blk(0));
   for (int i = 0; i < w; i += 2) {
-    // block i (in ua); block i + 1's loads go out after block i's x
-    if (i >= avail) {
-      avail = poll_done(done, i + 1, err);
-      if (avail <= i) { ok = false; break; }
-    }
-    {
-      const int jb = UPPER ? nblk - 1 - i : i;
-      const double xl = lane < kQW ? __builtin_bit_cast(double, __hip_atomic_load(
-                                                                    reinterpret_cast<const unsigned long long*>(
-                                                                        x + NB * jb + kQW * q + lane),
-                                                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
-                                   : 0.0;
-      if (i + 1 < w) load_blk(ub, blk(i + 1));
+    // block i (in ua): its values' first load, then block i + 1's factor
+    // loads, then the wait on the values
+    // (the prefetch is unconditional -- the last block is re-read -- so the
+    // code is straight-line and the value wait can count the loads after it)
+    double xl;
+    unsigned long long v = issue_x(x, xidx(i));
+    load_blk(ub, blk(min(i + 1, w - 1)));
+    if (!settle_x(x, xidx(i), v, err, xl, i + 1 < w)) { ok = false; break; }
 #pragma unroll
-      for (int j = 0; j < kQW; ++j) acc = fma(-(double)ua[j], bcast_lane(xl, j), acc);
-    }
+    for (int j = 0; j < kQW; ++j) acc = fma(-(double)ua[j], bcast_lane(xl, j), acc);
     if (i + 1 >= w) break;
-    if (i + 1 >= avail) {
-      avail = poll_done(done, i + 2, err);
-      if (avail <= i + 1) { ok = false; break; }
-    }
-    {
-      const int jb = UPPER ? nblk - 2 - i : i + 1;
-      const double xl = lane < kQW ? __builtin_bit_cast(double, __hip_atomic_load(
-                                                                    reinterpret_cast<const unsigned long long*>(
-                                                                        x + NB * jb + kQW * q + lane),
-                                                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
-                                   : 0.0;
-      if (i + 2 < w) load_blk(ua, blk(i + 2));
+    v = issue_x(x, xidx(i + 1));
+    load_blk(ua, blk(min(i + 2, w - 1)));
+    if (!settle_x(x, xidx(i + 1), v, err, xl, i + 2 < w)) { ok = false; break; }
 #pragma unroll
-      for (int j = 0; j < kQW; ++j) acc = fma(-(double)ub[j], bcast_lane(xl, j), acc);
-    }
+    for (int j = 0; j < kQW; ++j) acc = fma(-(double)ub[j], bcast_lane(xl, j), acc);
   }
   part[q][r] = acc;
   if (!ok && lane == 0) bad = 1;
@@ -423,13 +435,16 @@ __global__ __launch_bounds__(kDT) void blk_trsv_kernel(const T* __restrict__ F, 
   part[q][r] = xs;
   __syncthreads();
   if (q == 0) {
-    const double xv = part[0][r] + part[1][r] + part[2][r] + part[3][r];
+    double xv = part[0][r] + part[1][r] + part[2][r] + part[3][r];
+    if (__builtin_bit_cast(unsigned long long, xv) == kSentinel) xv = __builtin_nan("");  // never publish the sentinel
     __hip_atomic_store(reinterpret_cast<unsigned long long*>(x + row), __builtin_bit_cast(unsigned long long, xv),
                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
-  __syncthreads();
-  if (t == 0) __hip_atomic_store(done, (unsigned)(w + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__global__ __launch_bounds__(256) void fill_sentinel_kernel(unsigned long long* __restrict__ p, int n) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i < n) p[i] = kSentinel;
 }
 
 // Rounded fp32 copy of a rows x cols fp64 block (the fp32 engine's GEMM operands).
@@ -478,9 +493,49 @@ int factor_impl(double* M, int64_t ldm, int64_t np, double* Dinv, double* W, flo
   return GELIM_OK;
 }
 
+// The same factorisation with a one-block lookahead on two streams (fp64):
+// after W_k, the main stream updates only block column k+1 and block row k+1
+// (two thin GEMMs) and inverts the next diagonal block at once, while the
+// side stream runs the big trailing update of step k (rows / columns >= k+2)
+// (optionally on a grid capped below the CU count, GELIM_RBT_RESERVE).  Main waits for side step k-1 before touching block row / column
+// k+1 (the side's step k-1 region); W is double-buffered (side step k reads
+// W_k while main computes W_{k+1}).
+int factor_la(double* M, int64_t ldm, int64_t np, double* Dinv, double* W2, int* info, hipStream_t s,
+              hipStream_t side, hipEvent_t e0, hipEvent_t e1, int cap) {
+  const int64_t nblk = np / NB;
+  hipLaunchKernelGGL(diag_inv_kernel<double>, dim3(1), dim3(kGT), 0, s, M, ldm, 0, Dinv, (double*)nullptr, info);
+  HIP_TRY(hipGetLastError());
+  bool side_used = false;
+  for (int64_t k = 0; k + 1 < nblk; ++k) {
+    const int64_t k0 = k * NB, rest = np - k0 - NB, rest2 = rest - NB;
+    double* Di = Dinv + k * NB * NB;
+    double* Wk = W2 + (k & 1) * NB * np;
+    double* A21 = M + (k0 + NB) * ldm + k0;
+    GELIM_TRY(dgemm_ex(Wk, rest, Di, NB, M + k0 * ldm + k0 + NB, ldm, NB, rest, NB, 1.0, 0, s));  // W_k
+    if (side_used) HIP_TRY(hipStreamWaitEvent(s, e1, 0));  // side step k-1 done
+    // block column k+1 (all rows below k), then block row k+1 (columns past k+1)
+    GELIM_TRY(dgemm_ex(M + (k0 + NB) * ldm + k0 + NB, ldm, A21, ldm, Wk, rest, rest, NB, NB, -1.0, 1, s));
+    if (rest2 > 0) {
+      GELIM_TRY(dgemm_ex(M + (k0 + NB) * ldm + k0 + 2 * NB, ldm, A21, ldm, Wk + NB, rest, NB, rest2, NB, -1.0, 1, s));
+      HIP_TRY(hipEventRecord(e0, s));
+      HIP_TRY(hipStreamWaitEvent(side, e0, 0));
+      GELIM_TRY(dgemm_capped(M + (k0 + 2 * NB) * ldm + k0 + 2 * NB, ldm, M + (k0 + 2 * NB) * ldm + k0, ldm, Wk + NB,
+                             rest, rest2, rest2, NB, -1.0, cap, side, 1));
+      HIP_TRY(hipEventRecord(e1, side));
+      side_used = true;
+    }
+    hipLaunchKernelGGL(diag_inv_kernel<double>, dim3(1), dim3(kGT), 0, s, M, ldm, (int)(k0 + NB),
+                       Dinv + (k + 1) * NB * NB, (double*)nullptr, info);
+    HIP_TRY(hipGetLastError());
+  }
+  if (side_used) HIP_TRY(hipStreamWaitEvent(s, e1, 0));
+  return GELIM_OK;
+}
+
 // Block-LDU solve: forward z_k = D_k^-1 (c_k - sum_{j<k} A_kj z_j) keeping
 // y_k = c_k - sum (the block-unit-lower solve's result), then backward
-// x_k = D_k^-1 (y_k - sum_{j>k} A_kj x_j).  c -> (z, y) -> x (x may alias c).
+// x_k = D_k^-1 (y_k - sum_{j>k} A_kj x_j).  c -> (z, y) -> x (x may alias c:
+// it is sentinel-filled only after the forward solve has read c).
 template <typename T>
 int solve_impl(const T* M, int64_t ldm, int64_t np, const double* Dinv, const double* c, double* z, double* y,
                double* x, unsigned* flags, hipStream_t s) {
@@ -493,14 +548,19 @@ int solve_impl(const T* M, int64_t ldm, int64_t np, const double* Dinv, const do
   }();
   if (!fits || nblk > kMaxBlocks || !coresident(1, nblk))
     return GELIM_FAIL(GELIM_E_ARG, "mixed solve: the block rows of this order cannot all be resident");
-  // flags[0]: lower-solve counter, flags[1]: upper-solve counter, flags[2]: error word
-  int* err = reinterpret_cast<int*>(flags + 2);
+  int* err = reinterpret_cast<int*>(flags);  // flags[0]: error word
   GELIM_TRY(zero_async(flags, 16, s));
-  hipLaunchKernelGGL((blk_trsv_kernel<T, false>), dim3(nblk), dim3(kDT), 0, s, M, ldm, Dinv, c, z, y, nblk, flags,
-                     err);
+  const unsigned g = (unsigned)((np + 255) / 256);
+  hipLaunchKernelGGL(fill_sentinel_kernel, dim3(g), dim3(256), 0, s, reinterpret_cast<unsigned long long*>(z),
+                     (int)np);
+  HIP_TRY(hipGetLastError());
+  hipLaunchKernelGGL((blk_trsv_kernel<T, false>), dim3(nblk), dim3(kDT), 0, s, M, ldm, Dinv, c, z, y, nblk, err);
+  HIP_TRY(hipGetLastError());
+  hipLaunchKernelGGL(fill_sentinel_kernel, dim3(g), dim3(256), 0, s, reinterpret_cast<unsigned long long*>(x),
+                     (int)np);
   HIP_TRY(hipGetLastError());
   hipLaunchKernelGGL((blk_trsv_kernel<T, true>), dim3(nblk), dim3(kDT), 0, s, M, ldm, Dinv, y, x, (double*)nullptr,
-                     nblk, flags + 1, err);
+                     nblk, err);
   HIP_TRY(hipGetLastError());
   return GELIM_OK;
 }
@@ -513,17 +573,21 @@ struct gelim_mixed_plan {
   int fp64 = 0;             // factor precision: 0 fp32 ("hip-mixed"), 1 fp64 ("hip-rbt")
   double* M = nullptr;      // np x ldm: the transformed matrix, then its block-LDU factor
   double* Dinv = nullptr;   // nblk x NB x NB: inverse of every (Schur) diagonal block
-  double* W = nullptr;      // NB x np: A_kk^-1 A_k,rest of the current block
+  double* W = nullptr;      // 2 x NB x np: A_kk^-1 A_k,rest (double-buffered under lookahead)
   float* A21f = nullptr;    // np x NB, NB x np: rounded GEMM operands (fp32 engine only)
   float* Wf = nullptr;
   double* ud = nullptr;     // U's butterfly diagonals (8 x np/4)
   double* vd = nullptr;     // V's
-  unsigned* flags = nullptr;  // solve counters (lower, upper) + error word
+  unsigned* flags = nullptr;  // [0]: the solves' error word
   double* c = nullptr;      // U^T r (np)
   double* y = nullptr;      // L^-1 c (np)
   double* z = nullptr;      // U^-1 y (np)
   int* info = nullptr;
   int err_host = 0;
+  int lookahead = 0;        // fp64 engine: one-block lookahead on a side stream
+  int cap = 0;              // side-stream GEMM grid cap (CUs)
+  hipStream_t side = nullptr;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
 };
 
 extern "C" int64_t gelim_mixed_max_n(void) { return (int64_t)gelim::kMaxBlocks * gelim::NB; }
@@ -534,6 +598,9 @@ extern "C" void gelim_mixed_plan_destroy(gelim_mixed_plan* p) {
                   (void*)p->flags, (void*)p->c,
                   (void*)p->y, (void*)p->z, (void*)p->info})
     (void)hipFree(q);
+  if (p->e0) (void)hipEventDestroy(p->e0);
+  if (p->e1) (void)hipEventDestroy(p->e1);
+  if (p->side) (void)hipStreamDestroy(p->side);
   delete p;
 }
 
@@ -563,7 +630,27 @@ extern "C" gelim_mixed_plan* gelim_mixed_plan_create2(int64_t n, const double* u
   const int64_t nblk = np / gelim::NB;
   if (hipMalloc((void**)&p->M, sizeof(double) * (size_t)np * p->ldm) != hipSuccess) return fail("matrix");
   if (hipMalloc((void**)&p->Dinv, sizeof(double) * (size_t)np * gelim::NB) != hipSuccess) return fail("inverses");
-  if (hipMalloc((void**)&p->W, sizeof(double) * (size_t)np * gelim::NB) != hipSuccess) return fail("W buffer");
+  if (hipMalloc((void**)&p->W, 2 * sizeof(double) * (size_t)np * gelim::NB) != hipSuccess) return fail("W buffer");
+  // lookahead (fp64): from 32 blocks (n = 4096) unless GELIM_RBT_LOOKAHEAD says otherwise
+  {
+    const char* e = std::getenv("GELIM_RBT_LOOKAHEAD");
+    p->lookahead = fp64 && (e ? std::atoi(e) != 0 : np >= 4096);
+  }
+  if (p->lookahead) {
+    int dev = 0, ncu = 256;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    // side grid: uncapped by default (the regular dgemm kernel; the one-CU
+    // inverse still gets a CU as the GEMM's short-lived workgroups retire):
+    // 8192 15.0 ms, 16384 87.6 ms vs 18.7 / 122.7 ms with the persistent
+    // kernel capped 64 CUs short, and 16.0 / 91.3 ms without lookahead
+    int reserve = 0;
+    if (const char* e = std::getenv("GELIM_RBT_RESERVE")) reserve = std::max(0, std::atoi(e));
+    p->cap = reserve == 0 ? 0 : ncu > reserve + 8 ? ncu - reserve : std::max(8, ncu / 2);
+    if (hipStreamCreateWithFlags(&p->side, hipStreamNonBlocking) != hipSuccess) return fail("side stream");
+    if (hipEventCreateWithFlags(&p->e0, hipEventDisableTiming) != hipSuccess) return fail("event");
+    if (hipEventCreateWithFlags(&p->e1, hipEventDisableTiming) != hipSuccess) return fail("event");
+  }
   if (!fp64 && hipMalloc((void**)&p->A21f, sizeof(float) * (size_t)np * gelim::NB) != hipSuccess) return fail("A21f");
   if (!fp64 && hipMalloc((void**)&p->Wf, sizeof(float) * (size_t)np * gelim::NB) != hipSuccess) return fail("Wf");
   if (hipMalloc((void**)&p->ud, sizeof(double) * nd) != hipSuccess) return fail("ud");
@@ -597,8 +684,11 @@ extern "C" int gelim_mixed_factor(gelim_mixed_plan* p, const double* aug, int64_
   hipLaunchKernelGGL(rbt_matrix_kernel<double>, grid, dim3(256), 0, s, aug, ld, (int)p->n, (int)np, p->ud, p->vd,
                      p->M, ldm);
   HIP_TRY(hipGetLastError());
-  GELIM_TRY(factor_impl(p->M, ldm, np, p->Dinv, p->W, p->fp64 ? nullptr : p->A21f, p->fp64 ? nullptr : p->Wf, p->info,
-                        s));
+  if (p->lookahead)
+    GELIM_TRY(factor_la(p->M, ldm, np, p->Dinv, p->W, p->info, s, p->side, p->e0, p->e1, p->cap));
+  else
+    GELIM_TRY(factor_impl(p->M, ldm, np, p->Dinv, p->W, p->fp64 ? nullptr : p->A21f, p->fp64 ? nullptr : p->Wf,
+                          p->info, s));
   int h_info = 0;
   HIP_TRY(hipMemcpyAsync(&h_info, p->info, 4, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
@@ -630,7 +720,7 @@ extern "C" int gelim_mixed_solve_error(gelim_mixed_plan* p, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   const int64_t nblk = p->np / gelim::NB;
   (void)nblk;
-  HIP_TRY(hipMemcpyAsync(&p->err_host, p->flags + 2, 4, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemcpyAsync(&p->err_host, p->flags, 4, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
   return p->err_host;
 }

@@ -375,7 +375,7 @@ template <typename T, bool UPPER>
 __global__ __launch_bounds__(kDT) void blk_trsv_kernel(const T* __restrict__ F, int64_t ldf,
                                                       const double* __restrict__ Dinv, const double* __restrict__ c,
                                                       double* __restrict__ x, double* __restrict__ ysave, int nblk,
-                                                      int* __restrict__ err) {
+                                                      int* __restrict__ err, unsigned long long* __restrict__ stamps) {
   __shared__ double part[4][NB];
   __shared__ double rb[NB];
   __shared__ int bad;
@@ -392,6 +392,7 @@ __global__ __launch_bounds__(kDT) void blk_trsv_kernel(const T* __restrict__ F, 
 #pragma unroll
     for (int j = 0; j < kQW; ++j) dv[j] = d[j];
   }
+  if (stamps && t == 0) stamps[3 * w] = rtc();
   const double cv = c[row];
   double acc = 0.0;
   const T* frow = F + (int64_t)row * ldf + kQW * q;
@@ -418,6 +419,7 @@ __global__ __launch_bounds__(kDT) void blk_trsv_kernel(const T* __restrict__ F, 
 #pragma unroll
     for (int j = 0; j < kQW; ++j) acc = fma(-(double)ub[j], bcast_lane(xl, j), acc);
   }
+  if (stamps && t == 0) stamps[3 * w + 1] = rtc();  // wave 0 has its last block's values
   part[q][r] = acc;
   if (!ok && lane == 0) bad = 1;
   __syncthreads();
@@ -439,6 +441,7 @@ __global__ __launch_bounds__(kDT) void blk_trsv_kernel(const T* __restrict__ F, 
     if (__builtin_bit_cast(unsigned long long, xv) == kSentinel) xv = __builtin_nan("");  // never publish the sentinel
     __hip_atomic_store(reinterpret_cast<unsigned long long*>(x + row), __builtin_bit_cast(unsigned long long, xv),
                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (stamps && t == 0) stamps[3 * w + 2] = rtc();
   }
 }
 
@@ -536,6 +539,8 @@ int factor_la(double* M, int64_t ldm, int64_t np, double* Dinv, double* W2, int*
 // y_k = c_k - sum (the block-unit-lower solve's result), then backward
 // x_k = D_k^-1 (y_k - sum_{j>k} A_kj x_j).  c -> (z, y) -> x (x may alias c:
 // it is sentinel-filled only after the forward solve has read c).
+unsigned long long* g_trsv_stamps = nullptr;  // diagnostics: 3 realtime stamps per workgroup (lower solve)
+
 template <typename T>
 int solve_impl(const T* M, int64_t ldm, int64_t np, const double* Dinv, const double* c, double* z, double* y,
                double* x, unsigned* flags, hipStream_t s) {
@@ -554,13 +559,14 @@ int solve_impl(const T* M, int64_t ldm, int64_t np, const double* Dinv, const do
   hipLaunchKernelGGL(fill_sentinel_kernel, dim3(g), dim3(256), 0, s, reinterpret_cast<unsigned long long*>(z),
                      (int)np);
   HIP_TRY(hipGetLastError());
-  hipLaunchKernelGGL((blk_trsv_kernel<T, false>), dim3(nblk), dim3(kDT), 0, s, M, ldm, Dinv, c, z, y, nblk, err);
+  hipLaunchKernelGGL((blk_trsv_kernel<T, false>), dim3(nblk), dim3(kDT), 0, s, M, ldm, Dinv, c, z, y, nblk, err,
+                     g_trsv_stamps);
   HIP_TRY(hipGetLastError());
   hipLaunchKernelGGL(fill_sentinel_kernel, dim3(g), dim3(256), 0, s, reinterpret_cast<unsigned long long*>(x),
                      (int)np);
   HIP_TRY(hipGetLastError());
   hipLaunchKernelGGL((blk_trsv_kernel<T, true>), dim3(nblk), dim3(kDT), 0, s, M, ldm, Dinv, y, x, (double*)nullptr,
-                     nblk, err);
+                     nblk, err, (unsigned long long*)nullptr);
   HIP_TRY(hipGetLastError());
   return GELIM_OK;
 }
@@ -726,6 +732,11 @@ extern "C" int gelim_mixed_solve_error(gelim_mixed_plan* p, void* stream) {
 }
 
 extern "C" int64_t gelim_mixed_plan_np(const gelim_mixed_plan* p) { return p ? p->np : 0; }
+
+// Diagnostics: realtime stamps (100 MHz) of the NEXT lower block solves, 3 per
+// workgroup (start, last block's values in hand, published) into the device
+// buffer `stamps` (null: off).
+extern "C" void gelim_debug_trsv_stamps(unsigned long long* stamps) { gelim::g_trsv_stamps = stamps; }
 
 // Device pointers of the plan's buffers (tests / debugging): out[0] = factor
 // (np x ldm), out[1] = diagonal-block inverses (nblk x 128 x 128 fp64),

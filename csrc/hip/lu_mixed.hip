@@ -325,6 +325,7 @@ __device__ __forceinline__ double bcast_lane(double v, int l) {
 // none is the sentinel -- one store + one load per hand-off, where a flag
 // needed store + drain + barrier + flag store + flag poll + value load.
 constexpr uint64_t kSentinel = 0x7ff4dead0badf00dull;
+constexpr int kXcdSlots = 32;  // packed chain: positions per XCD (one workgroup per CU)
 
 template <typename T>
 __device__ __forceinline__ void load_blk(T (&u)[kQW], const T* __restrict__ p) {
@@ -375,73 +376,112 @@ template <typename T, bool UPPER>
 __global__ __launch_bounds__(kDT) void blk_trsv_kernel(const T* __restrict__ F, int64_t ldf,
                                                       const double* __restrict__ Dinv, const double* __restrict__ c,
                                                       double* __restrict__ x, double* __restrict__ ysave, int nblk,
-                                                      int* __restrict__ err, unsigned long long* __restrict__ stamps) {
+                                                      int* __restrict__ err, unsigned long long* __restrict__ stamps,
+                                                      int packed) {
   __shared__ double part[4][NB];
   __shared__ double rb[NB];
   __shared__ int bad;
   const int t = threadIdx.x, r = t & (NB - 1), lane = t & 63;
   const int q = __builtin_amdgcn_readfirstlane(t >> 7);
-  const int w = blockIdx.x;
+  // chain position: packed = consecutive positions on one XCD (workgroup ids
+  // are dealt to the 8 XCDs round-robin, so id = 8 slot + xcd; position =
+  // 32 xcd + slot), keeping most hand-offs inside one XCD's L2; the grid then
+  // has 8 * 32 workgroups and the unused ones return at once
+  int w = blockIdx.x;
+  if (packed) {
+    const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;
+    if (slot >= kXcdSlots) return;
+    w = xcd * kXcdSlots + slot;
+  }
+  if (w >= nblk) return;
   const int b = UPPER ? nblk - 1 - w : w;
   const int row = NB * b + r;
   if (t == 0) bad = 0;
-  // this block's inverse row (independent of everything: loaded first)
+  // this block's inverse row and right-hand side (independent of
+  // everything): loaded first and pinned in registers here -- left to the
+  // scheduler, the loads sank past the block loop and their HBM latency
+  // (2-5 us at 8192) landed on the chain, between the last hand-off and the
+  // publish (scripts/trsv_stamps.py)
   double dv[kQW];
   {
     const double* d = Dinv + ((int64_t)b * NB + r) * NB + kQW * q;
 #pragma unroll
     for (int j = 0; j < kQW; ++j) dv[j] = d[j];
   }
+  double cv = c[row];
+#pragma unroll
+  for (int j = 0; j < kQW; ++j) asm volatile("" : "+v"(dv[j]));
+  asm volatile("" : "+v"(cv));
   if (stamps && t == 0) stamps[3 * w] = rtc();
-  const double cv = c[row];
   double acc = 0.0;
   const T* frow = F + (int64_t)row * ldf + kQW * q;
   auto blk = [&](int i) { return frow + (int64_t)NB * (UPPER ? nblk - 1 - i : i); };
   auto xidx = [&](int i) { return NB * (UPPER ? nblk - 1 - i : i) + kQW * q; };
   bool ok = true;
   T ua[kQW], ub[kQW];
-  if (w > 0) load_blk(ua, blk(0));
-  for (int i = 0; i < w; i += 2) {
-    // block i (in ua): its values' first load, then block i + 1's factor
-    // loads, then the wait on the values
-    // (the prefetch is unconditional -- the last block is re-read -- so the
-    // code is straight-line and the value wait can count the loads after it)
+  auto step = [&](const T(&u)[kQW], unsigned long long v, int i) -> bool {
     double xl;
-    unsigned long long v = issue_x(x, xidx(i));
-    load_blk(ub, blk(min(i + 1, w - 1)));
-    if (!settle_x(x, xidx(i), v, err, xl, i + 1 < w)) { ok = false; break; }
+    if (!settle_x(x, xidx(i), v, err, xl, i + 1 < w)) return false;
 #pragma unroll
-    for (int j = 0; j < kQW; ++j) acc = fma(-(double)ua[j], bcast_lane(xl, j), acc);
-    if (i + 1 >= w) break;
-    v = issue_x(x, xidx(i + 1));
-    load_blk(ua, blk(min(i + 2, w - 1)));
-    if (!settle_x(x, xidx(i + 1), v, err, xl, i + 2 < w)) { ok = false; break; }
+    for (int j = 0; j < kQW; ++j) acc = fma(-(double)u[j], bcast_lane(xl, j), acc);
+    return true;
+  };
+  // Two passes over ONE copy of the finish code: pass 0 runs it on zeros
+  // before the block loop (no stores), so its instructions are in the
+  // instruction cache when the real finish -- the chain's critical section,
+  // executed once per workgroup -- runs in pass 1 (cold, it took 3 us even
+  // for block 0, which has no predecessor: scripts/trsv_stamps.py).
+  for (int pass = 0; pass < 2; ++pass) {
+    if (pass == 1) {
+      if (w > 0) load_blk(ua, blk(0));
+      int i = 0;
+      // pairs of blocks with the next block's factor loads issued between the
+      // values' first load and their wait (straight-line: the wait counts
+      // them); no prefetch past the last block -- a load still in flight at
+      // the end would hold its registers, and the finish would wait for it
+      for (; i + 2 < w; i += 2) {
+        unsigned long long v = issue_x(x, xidx(i));
+        load_blk(ub, blk(i + 1));
+        if (!step(ua, v, i)) { ok = false; break; }
+        v = issue_x(x, xidx(i + 1));
+        load_blk(ua, blk(i + 2));
+        if (!step(ub, v, i + 1)) { ok = false; break; }
+      }
+      if (ok && i + 1 < w) {  // two blocks left
+        unsigned long long v = issue_x(x, xidx(i));
+        load_blk(ub, blk(i + 1));
+        ok = step(ua, v, i);
+        if (ok) ok = step(ub, issue_x(x, xidx(i + 1)), i + 1);
+      } else if (ok && i < w) {  // one block left
+        ok = step(ua, issue_x(x, xidx(i)), i);
+      }
+      if (stamps && t == 0) stamps[3 * w + 1] = rtc();  // wave 0 has its last block's values
+    }
+    const bool real = pass == 1;
+    part[q][r] = acc;
+    if (!ok && lane == 0) bad = 1;
+    __syncthreads();
+    if (bad) return;  // uniform: a timed-out wave makes the whole workgroup stop
+    if (q == 0) {
+      const double y = cv + part[0][r] + part[1][r] + part[2][r] + part[3][r];
+      rb[r] = y;
+      if (real && ysave) ysave[row] = y;
+    }
+    __syncthreads();
+    double xs = 0.0;
 #pragma unroll
-    for (int j = 0; j < kQW; ++j) acc = fma(-(double)ub[j], bcast_lane(xl, j), acc);
-  }
-  if (stamps && t == 0) stamps[3 * w + 1] = rtc();  // wave 0 has its last block's values
-  part[q][r] = acc;
-  if (!ok && lane == 0) bad = 1;
-  __syncthreads();
-  if (bad) return;  // uniform: a timed-out wave makes the whole workgroup stop
-  if (q == 0) {
-    const double y = cv + part[0][r] + part[1][r] + part[2][r] + part[3][r];
-    rb[r] = y;
-    if (ysave) ysave[row] = y;
-  }
-  __syncthreads();
-  double xs = 0.0;
-#pragma unroll
-  for (int j = 0; j < kQW; ++j) xs = fma(dv[j], rb[kQW * q + j], xs);
-  __syncthreads();  // everyone has read rb / part
-  part[q][r] = xs;
-  __syncthreads();
-  if (q == 0) {
-    double xv = part[0][r] + part[1][r] + part[2][r] + part[3][r];
-    if (__builtin_bit_cast(unsigned long long, xv) == kSentinel) xv = __builtin_nan("");  // never publish the sentinel
-    __hip_atomic_store(reinterpret_cast<unsigned long long*>(x + row), __builtin_bit_cast(unsigned long long, xv),
-                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (stamps && t == 0) stamps[3 * w + 2] = rtc();
+    for (int j = 0; j < kQW; ++j) xs = fma(dv[j], rb[kQW * q + j], xs);
+    __syncthreads();  // everyone has read rb / part
+    part[q][r] = xs;
+    __syncthreads();
+    if (q == 0 && real) {
+      double xv = part[0][r] + part[1][r] + part[2][r] + part[3][r];
+      if (__builtin_bit_cast(unsigned long long, xv) == kSentinel) xv = __builtin_nan("");  // never publish the sentinel
+      __hip_atomic_store(reinterpret_cast<unsigned long long*>(x + row), __builtin_bit_cast(unsigned long long, xv),
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (stamps && t == 0) stamps[3 * w + 2] = rtc();
+    }
+    __syncthreads();  // pass 0's reads of part are done before pass 1 writes it
   }
 }
 
@@ -551,7 +591,7 @@ int solve_impl(const T* M, int64_t ldm, int64_t np, const double* Dinv, const do
            hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, blk_trsv_kernel<T, true>, kDT, 0) == hipSuccess &&
            a >= 1 && b >= 1;
   }();
-  if (!fits || nblk > kMaxBlocks || !coresident(1, nblk))
+  if (!fits || nblk > kMaxBlocks || !coresident(1, 8 * kXcdSlots))
     return GELIM_FAIL(GELIM_E_ARG, "mixed solve: the block rows of this order cannot all be resident");
   int* err = reinterpret_cast<int*>(flags);  // flags[0]: error word
   GELIM_TRY(zero_async(flags, 16, s));
@@ -559,14 +599,19 @@ int solve_impl(const T* M, int64_t ldm, int64_t np, const double* Dinv, const do
   hipLaunchKernelGGL(fill_sentinel_kernel, dim3(g), dim3(256), 0, s, reinterpret_cast<unsigned long long*>(z),
                      (int)np);
   HIP_TRY(hipGetLastError());
-  hipLaunchKernelGGL((blk_trsv_kernel<T, false>), dim3(nblk), dim3(kDT), 0, s, M, ldm, Dinv, c, z, y, nblk, err,
-                     g_trsv_stamps);
+  static const int pack = [] {
+    const char* e = std::getenv("GELIM_TRSV_PACK");
+    return e ? std::atoi(e) : 1;
+  }();
+  const unsigned grid = pack ? 8u * kXcdSlots : (unsigned)nblk;
+  hipLaunchKernelGGL((blk_trsv_kernel<T, false>), dim3(grid), dim3(kDT), 0, s, M, ldm, Dinv, c, z, y, nblk, err,
+                     g_trsv_stamps, pack);
   HIP_TRY(hipGetLastError());
   hipLaunchKernelGGL(fill_sentinel_kernel, dim3(g), dim3(256), 0, s, reinterpret_cast<unsigned long long*>(x),
                      (int)np);
   HIP_TRY(hipGetLastError());
-  hipLaunchKernelGGL((blk_trsv_kernel<T, true>), dim3(nblk), dim3(kDT), 0, s, M, ldm, Dinv, y, x, (double*)nullptr,
-                     nblk, err, (unsigned long long*)nullptr);
+  hipLaunchKernelGGL((blk_trsv_kernel<T, true>), dim3(grid), dim3(kDT), 0, s, M, ldm, Dinv, y, x, (double*)nullptr,
+                     nblk, err, (unsigned long long*)nullptr, pack);
   HIP_TRY(hipGetLastError());
   return GELIM_OK;
 }

@@ -67,6 +67,8 @@ int dgemm_ex(double* C, int64_t ldc, const double* A, int64_t lda, const double*
              int64_t N, int64_t K, double alpha, int accumulate, hipStream_t s);
 int dgemm_capped(double* C, int64_t ldc, const double* A, int64_t lda, const double* B, int64_t ldb, int64_t M,
                  int64_t N, int64_t K, double alpha, int max_wg, hipStream_t s, int accumulate);
+int residual_f64(const double* aug, int64_t ld, int64_t n, const double* x, double* r, hipStream_t s, int matvec,
+                 double* w);
 
 namespace {
 
@@ -490,6 +492,32 @@ __global__ __launch_bounds__(256) void fill_sentinel_kernel(unsigned long long* 
   if (i < n) p[i] = kSentinel;
 }
 
+// omega = max_i |r_i| / w_i (componentwise backward error; w_i = 0 counts as
+// 0), one workgroup, written to *out.
+__global__ __launch_bounds__(1024) void berr_kernel(const double* __restrict__ r, const double* __restrict__ w, int n,
+                                                   double* __restrict__ out) {
+  __shared__ double red[16];
+  double m = 0.0;
+  for (int i = threadIdx.x; i < n; i += 1024) {
+    const double wi = w[i], ri = fabs(r[i]);
+    const double v = wi > 0.0 ? ri / wi : (ri > 0.0 ? INFINITY : 0.0);
+    m = (v > m || v != v) ? v : m;  // NaN propagates
+  }
+  m = dev::wave_max(m);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    double v = threadIdx.x < 16 ? red[threadIdx.x] : 0.0;
+    v = dev::wave_max(v);
+    if (threadIdx.x == 0) *out = v;
+  }
+}
+
+__global__ __launch_bounds__(256) void axpy_kernel(double* __restrict__ x, const double* __restrict__ d, int n) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i < n) x[i] += d[i];
+}
+
 // Rounded fp32 copy of a rows x cols fp64 block (the fp32 engine's GEMM operands).
 __global__ __launch_bounds__(256) void to_f32_kernel(const double* __restrict__ src, int64_t sld,
                                                     float* __restrict__ dst, int64_t dld, int cols) {
@@ -635,6 +663,11 @@ struct gelim_mixed_plan {
   double* z = nullptr;      // U^-1 y (np)
   int* info = nullptr;
   int err_host = 0;
+  double* rv = nullptr;     // refinement (gelim_mixed_solve): r, |b| + |A||x|, correction, best x (n each)
+  double* wv = nullptr;
+  double* dv = nullptr;
+  double* xb = nullptr;
+  double* om = nullptr;     // device scalar: the backward error
   int lookahead = 0;        // fp64 engine: one-block lookahead on a side stream
   int cap = 0;              // side-stream GEMM grid cap (CUs)
   hipStream_t side = nullptr;
@@ -646,7 +679,7 @@ extern "C" int64_t gelim_mixed_max_n(void) { return (int64_t)gelim::kMaxBlocks *
 extern "C" void gelim_mixed_plan_destroy(gelim_mixed_plan* p) {
   if (!p) return;
   for (void* q : {(void*)p->M, (void*)p->Dinv, (void*)p->W, (void*)p->A21f, (void*)p->Wf, (void*)p->ud, (void*)p->vd,
-                  (void*)p->flags, (void*)p->c,
+                  (void*)p->rv, (void*)p->wv, (void*)p->dv, (void*)p->xb, (void*)p->om, (void*)p->flags, (void*)p->c,
                   (void*)p->y, (void*)p->z, (void*)p->info})
     (void)hipFree(q);
   if (p->e0) (void)hipEventDestroy(p->e0);
@@ -712,6 +745,9 @@ extern "C" gelim_mixed_plan* gelim_mixed_plan_create2(int64_t n, const double* u
   if (hipMalloc((void**)&p->y, sizeof(double) * np) != hipSuccess) return fail("y");
   if (hipMalloc((void**)&p->z, sizeof(double) * np) != hipSuccess) return fail("z");
   if (hipMalloc((void**)&p->info, 16) != hipSuccess) return fail("info");
+  for (double** b : {&p->rv, &p->wv, &p->dv, &p->xb})
+    if (hipMalloc((void**)b, sizeof(double) * (size_t)n) != hipSuccess) return fail("refinement vectors");
+  if (hipMalloc((void**)&p->om, 16) != hipSuccess) return fail("omega");
   if (hipMemcpy(p->ud, ud, sizeof(double) * nd, hipMemcpyHostToDevice) != hipSuccess) return fail("ud copy");
   if (hipMemcpy(p->vd, vd, sizeof(double) * nd, hipMemcpyHostToDevice) != hipSuccess) return fail("vd copy");
   return p;
@@ -763,6 +799,66 @@ extern "C" int gelim_mixed_apply(gelim_mixed_plan* p, const double* r, int64_t i
                      (int)p->n);
   HIP_TRY(hipGetLastError());
   return GELIM_OK;
+}
+
+extern "C" int gelim_mixed_solve_error(gelim_mixed_plan* p, void* stream);
+
+// The whole randomised solve of an augmented fp64 system (n x >= n+1 at aug,
+// leading dimension ld) into x (n fp64, device): factorisation, x = (LU)^-1 b,
+// then classic fp64 refinement x += (LU)^-1 (b - A x) until the componentwise
+// backward error max_i |r_i| / (|b| + |A||x|)_i is <= 4 eps64; once a
+// correction stops reducing it by 10 %, or after max_steps corrections, x is
+// accepted if it is <= max(sqrt(n), 8) eps64.  Returns 0 (x written; *steps =
+// corrections, *berr = final backward error), 1 when the caller must fall
+// back to partial pivoting (zero / non-finite pivot or stalled refinement;
+// *berr says how far it got), < 0 on errors.  One 8-byte device-to-host read
+// per correction (the convergence test); the Python GMRES-IR of the fp32
+// engine does not use this.
+extern "C" int gelim_mixed_solve(gelim_mixed_plan* p, const double* aug, int64_t ld, double* x, int max_steps,
+                                 int* steps, double* berr, void* stream) {
+  using namespace gelim;
+  if (!p || !aug || !x) return GELIM_FAIL(GELIM_E_ARG, "mixed_solve: null argument");
+  hipStream_t s = (hipStream_t)stream;
+  const int n = (int)p->n;
+  if (steps) *steps = 0;
+  if (berr) *berr = INFINITY;
+  const int rc = gelim_mixed_factor(p, aug, ld, stream);
+  if (rc < 0) return rc;
+  if (rc > 0) return 1;
+  GELIM_TRY(gelim_mixed_apply(p, aug + n, ld, x, stream));
+  const double eps = 2.220446049250313e-16;
+  const double strict = 4.0 * eps, loose = std::max(std::sqrt((double)n), 8.0) * eps;
+  double prev = INFINITY, best = INFINITY;
+  const unsigned g = (unsigned)((n + 255) / 256);
+  for (int it = 0;; ++it) {
+    GELIM_TRY(residual_f64(aug, ld, n, x, p->rv, s, 0, p->wv));
+    hipLaunchKernelGGL(berr_kernel, dim3(1), dim3(1024), 0, s, p->rv, p->wv, n, p->om);
+    HIP_TRY(hipGetLastError());
+    double om = 0.0;
+    HIP_TRY(hipMemcpyAsync(&om, p->om, 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    if (steps) *steps = it;
+    if (berr) *berr = om;
+    if (om <= strict) return 0;
+    if (!(om < 0.9 * prev) || it == max_steps) {  // NaN, stagnated or out of steps
+      if (best <= loose) {
+        HIP_TRY(hipMemcpyAsync(x, p->xb, sizeof(double) * n, hipMemcpyDeviceToDevice, s));
+        if (berr) *berr = best;
+        return 0;
+      }
+      return om <= loose ? 0 : 1;
+    }
+    if (om < best) {
+      best = om;
+      HIP_TRY(hipMemcpyAsync(p->xb, x, sizeof(double) * n, hipMemcpyDeviceToDevice, s));
+    }
+    prev = om;
+    GELIM_TRY(gelim_mixed_apply(p, p->rv, 1, p->dv, stream));
+    hipLaunchKernelGGL(axpy_kernel, dim3(g), dim3(256), 0, s, x, p->dv, n);
+    HIP_TRY(hipGetLastError());
+    if (gelim_mixed_solve_error(p, stream) != 0)
+      return GELIM_FAIL(GELIM_E_HIP, "mixed_solve: a triangular-solve hand-off timed out");
+  }
 }
 
 // Hand-off error word of the last solve (0: fine, 3: a bounded spin expired).

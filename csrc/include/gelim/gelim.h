@@ -235,6 +235,20 @@ int gelim_gauss_plan_resolve(gelim_gauss_plan* p, const double* d_c, double* d_x
 /* r = b - A x of an augmented fp64 system (b in column n) */
 int gelim_gpu_residual(const double* d_aug, int64_t ld, int64_t n, const double* d_x, double* d_r, void* stream);
 
+/* ---- randomised no-pivoting engine (hip-rbt / hip-mixed) ----------------
+ * Random butterfly transform + block LDU without pivoting (lu_mixed.hip).
+ * ud / vd: host arrays of 2 * gelim_mixed_padded(n) butterfly entries each
+ * (exp(r / 10), r uniform in [-1/2, 1/2]); fp64 = 1: fp64 factors (hip-rbt). */
+typedef struct gelim_mixed_plan gelim_mixed_plan;
+int64_t gelim_mixed_max_n(void);
+int64_t gelim_mixed_padded(int64_t n);
+gelim_mixed_plan* gelim_mixed_plan_create2(int64_t n, const double* ud, const double* vd, int fp64);
+void gelim_mixed_plan_destroy(gelim_mixed_plan* p);
+/* Whole solve with fp64 refinement to a componentwise backward error <= 4 eps:
+ * 0 = x written, 1 = fall back to partial pivoting, < 0 = error. */
+int gelim_mixed_solve(gelim_mixed_plan* p, const double* d_aug, int64_t ld, double* d_x, int max_steps, int* steps,
+                      double* berr, void* stream);
+
 /* ---- GPU fp32 matmul --------------------------------------------------- */
 /* C (M x N) = A (M x K) * B (K x N), row-major, ld = cols. */
 int gelim_gpu_matmul_f32(const float* dA, const float* dB, float* dC,

@@ -113,6 +113,37 @@ int main(int argc, char* argv[]) {
     gelim_cpu_backsub_unit(A.data(), lda, R.data(), X.data(), n);
   } else {
     for (int64_t i = 0; i < n; ++i) A[i * lda + n] = R[i];
+    if (backend == cli::HIP_RBT) {
+      double *dA = nullptr, *dx = nullptr;
+      CLI_HIP(hipMalloc((void**)&dA, A.size() * sizeof(double)));
+      CLI_HIP(hipMalloc((void**)&dx, n * sizeof(double)));
+      CLI_HIP(hipMemcpy(dA, A.data(), A.size() * sizeof(double), hipMemcpyHostToDevice));
+      hipStream_t s;
+      CLI_HIP(hipStreamCreate(&s));
+      {
+        cli::RbtSolver rbt(n, GELIM_PIVOT_PARTIAL, use_graph);
+        auto run = [&]() {
+          rbt.solve(dA, lda, dx, s);
+          CLI_HIP(hipStreamSynchronize(s));
+        };
+        for (int w = 0; w < warmup; ++w) run();
+        const double t0 = cli::wall();
+        run();
+        elapsed = cli::wall() - t0;
+        const int info = rbt.info(s);
+        if (info > 0) {
+          fprintf(stderr, "The matrix is singular\n");
+          exit(-1);
+        }
+        if (info < 0) cli::die("plan_info");
+        CLI_HIP(hipMemcpy(X.data(), dx, n * sizeof(double), hipMemcpyDeviceToHost));
+        printf("Device: %s ; Backend: %s ; dtype: f64\n", cli::device_name().c_str(), cli::backend_name(backend));
+        rbt.note();
+      }
+      (void)hipFree(dA);
+      (void)hipFree(dx);
+      (void)hipStreamDestroy(s);
+    } else {
     int algo = backend == cli::HIP_BLOCKED ? GELIM_GPU_BLOCKED : GELIM_GPU_PIVOT;
     // the blocked LU takes any order up to gelim_gpu_leaf_max_rows() (262144,
     // beyond one GPU's 288 GB at fp64): no silent fallback to hip-pivot
@@ -146,6 +177,7 @@ int main(int argc, char* argv[]) {
     (void)hipFree(dA);
     (void)hipFree(dx);
     (void)hipStreamDestroy(s);
+    }
   }
 
   fprintf(stdout, "Time:  %f seconds\n", elapsed);

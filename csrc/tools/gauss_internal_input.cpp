@@ -11,6 +11,9 @@
 // New: --backend selects the parallel strategy; the default runs on the GPU.
 //   --backend=hip|hip-blocked  blocked LU, fp64 MFMA trailing updates (default)
 //   --backend=hip-pivot        reference per-pivot algorithm on the GPU
+//   --backend=hip-rbt          randomised no-pivoting fp64 engine (butterfly
+//                              transform + block LDU + fp64 refinement; falls
+//                              back to the blocked LU by itself)
 //   --backend=seq|omp|pthreads-v1|pthreads-v2|pthreads-v3   CPU strategies
 //   --dtype=f64|f32 (f32: hip-pivot only)  --pivot=zero|partial (default zero,
 //   the reference internal rule)  --verify (print B/C pairs as VERIFY=1 did)
@@ -65,7 +68,7 @@ int main(int argc, char* argv[]) {
       }
       case 'h':
         printf("Usage: ./program -t <num threads> -s <matrix size>"
-               " [--backend=hip|hip-pivot|seq|omp|pthreads-v1|pthreads-v2|pthreads-v3]"
+               " [--backend=hip|hip-pivot|hip-rbt|seq|omp|pthreads-v1|pthreads-v2|pthreads-v3]"
                " [--dtype=f64|f32] [--pivot=zero|partial] [--verify] [--json]\n");
         return 0;
       case 'b':
@@ -94,6 +97,10 @@ int main(int argc, char* argv[]) {
     num_threads = gelim_cpu_max_threads();
   }
   if (dtype == 4 && backend == cli::HIP_BLOCKED) backend = cli::HIP_PIVOT;
+  if (backend == cli::HIP_RBT && (verify || dtype != 8)) {
+    fprintf(stderr, "hip-rbt solves a transformed fp64 system: no --verify (reference-style B), no --dtype=f32\n");
+    return -1;
+  }
 
   const int64_t n = nsize;
   if (backend == cli::PTH_V2)
@@ -124,6 +131,37 @@ int main(int argc, char* argv[]) {
     if (rc != 0) cli::die("gauss");
     gelim_cpu_backsub_unit(A.data(), n, B.data(), C.data(), n);
     elapsed = cli::wall() - t0;
+  } else if (backend == cli::HIP_RBT) {
+    const int64_t lda = n + 1;
+    double *dA = nullptr, *dx = nullptr;
+    CLI_HIP(hipMalloc((void**)&dA, (size_t)(n * lda) * sizeof(double)));
+    CLI_HIP(hipMalloc((void**)&dx, n * sizeof(double)));
+    hipStream_t s;
+    CLI_HIP(hipStreamCreate(&s));
+    {
+      cli::RbtSolver rbt(n, pivot, use_graph);
+      auto run = [&]() {
+        CLI_CHECK(gelim_gpu_init_synthetic(dA, lda, n, s));
+        rbt.solve(dA, lda, dx, s);
+        CLI_HIP(hipStreamSynchronize(s));
+      };
+      for (int w = 0; w < warmup; ++w) run();
+      const double t0 = cli::wall();
+      run();
+      elapsed = cli::wall() - t0;
+      const int info = rbt.info(s);
+      if (info > 0) {
+        printf("The matrix is singular\n");
+        exit(-1);
+      }
+      if (info < 0) cli::die("plan_info");
+      CLI_HIP(hipMemcpy(C.data(), dx, n * sizeof(double), hipMemcpyDeviceToHost));
+      printf("Device: %s ; Backend: %s ; dtype: f64\n", cli::device_name().c_str(), cli::backend_name(backend));
+      rbt.note();
+    }
+    (void)hipFree(dA);
+    (void)hipFree(dx);
+    (void)hipStreamDestroy(s);
   } else {
     const int algo = backend == cli::HIP_BLOCKED ? GELIM_GPU_BLOCKED : GELIM_GPU_PIVOT;
     gelim_gauss_plan* plan = gelim_gauss_plan_create(n, algo, pivot, dtype, use_graph);

@@ -82,6 +82,7 @@ _PROTOS = {
     "gelim_mixed_debug_ptrs": (_i64, [_vp, _vp]),
     "gelim_mixed_debug_copy": (_int, [_vp, _vp, _i64]),
     "gelim_mixed_plan_np": (_i64, [_vp]),
+    "gelim_mixed_solve": (_int, [_vp, _vp, _i64, _vp, _int, _vp, _vp, _vp]),
     "gelim_gpu_residual_cw": (_int, [_vp, _i64, _i64, _vp, _vp, _vp, _vp]),
     "gelim_mixed_plan_destroy": (None, [_vp]),
     "gelim_mixed_factor": (_int, [_vp, _vp, _i64, _vp]),

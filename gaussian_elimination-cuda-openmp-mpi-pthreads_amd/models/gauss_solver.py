@@ -193,6 +193,22 @@ class GaussSolver:
             return self._fallback(aug64, self._mixed_unavailable or "no mixed plan", check)
         ld = aug64.stride(0)
         sh = stream_handle(dev)
+        if self.dtype == torch.float64:
+            # hip-rbt: the whole solve + classic refinement in native code
+            # (csrc/hip/lu_mixed.hip gelim_mixed_solve: one 8-byte read-back
+            # per correction)
+            import ctypes
+
+            x = torch.empty(n, dtype=torch.float64, device=dev)
+            st, be = ctypes.c_int(0), ctypes.c_double(0.0)
+            rc = lib.gelim_mixed_solve(self._mixed, ptr(aug64), ld, ptr(x), max_steps, ctypes.byref(st),
+                                       ctypes.byref(be), sh)
+            _native.check(rc, "mixed_solve")
+            self.last_steps, self.last_berr = st.value, be.value
+            if rc == 1:
+                return self._fallback(aug64, f"no-pivot LU: zero pivot or refinement stalled after {st.value} "
+                                             f"corrections (componentwise backward error {be.value:.3e})", check)
+            return x
         rc = lib.gelim_mixed_factor(self._mixed, ptr(aug64), ld, sh)
         _native.check(rc, "mixed_factor")
         if rc > 0:

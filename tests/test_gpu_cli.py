@@ -35,6 +35,33 @@ def test_external_gpu(tmp_path, gelim, cuda):
     assert m and float(m.group(1)) < 1e-11
 
 
+@pytest.mark.parametrize("name", ["jpwh_991", "sherman3"])
+def test_external_rbt_gpu(tmp_path, gelim, cuda, name):
+    """hip-rbt on the reference's .dat files: the randomised engine's answer
+    (or its automatic partial-pivoting fallback) within 20x of the
+    reference's golden fp64 error."""
+    from conftest import GOLDEN_ERROR
+
+    n, rr, cc, vv = gelim.utils.io.load_coo_npz(gelim.utils.io.fixture_path(name))
+    p = tmp_path / f"{name}.dat"
+    gelim.utils.io.write_dat(p, rr, cc, vv, n)
+    r = run_cli(BIN / "gauss_external_input", p, "--backend=hip-rbt")
+    assert r.returncode == 0, r.stderr
+    assert "Backend: hip-rbt" in r.stdout and "hip-rbt: " in r.stdout
+    m = re.search(r"Error: (\S+)", r.stdout)
+    assert m and float(m.group(1)) <= max(20 * GOLDEN_ERROR[name], 1e-13), r.stdout
+
+
+def test_internal_rbt_gpu(cuda):
+    """The synthetic internal system (exact x = (-0.5, 0, ..., 0, 0.5))."""
+    r = run_cli(BIN / "gauss_internal_input", "-s", "1000", "--backend=hip-rbt", "--json")
+    assert r.returncode == 0, r.stderr
+    m = re.search(r'"max_abs_err": (\S+?)[,}]', r.stdout)
+    assert m and float(m.group(1)) < 1e-9, r.stdout
+    bad = run_cli(BIN / "gauss_internal_input", "-s", "64", "--backend=hip-rbt", "--verify")
+    assert bad.returncode != 0
+
+
 def test_hip_matmul_cli(cuda):
     r = run_cli(BIN / "hip_matmul", "1024", "--no-seq", "--no-omp", "--verify")
     assert r.returncode == 0, r.stderr

@@ -186,8 +186,7 @@ __global__ __launch_bounds__(256) void rbt_vec_kernel(const double* __restrict__
 // a 4-column blocked Gauss-Jordan step -- explicit 4 x 4 pivot-block inverse,
 // rank-4 update -- was slower, 81 us, and lost accuracy: refinement needed
 // more corrections and fell back at n >= 4096).
-constexpr int kGT = 256;  // threads
-constexpr int kTl = 8;    // tile edge
+constexpr int kTl = 8;    // tile columns (and rows, TR = 8)
 
 template <typename TI>
 struct alignas(16) GjLds {
@@ -195,10 +194,13 @@ struct alignas(16) GjLds {
   TI col[2][NB];
 };
 
-template <int KK>
-__device__ __forceinline__ void gj_step(double (&a)[kTl][kTl], GjLds<double>& sh, int kg, int rg, int cg) {
+// Step k = 8 kg + KK of the Gauss-Jordan inverse on TR x 8 tiles (TR = 8:
+// 256 threads, one wave per SIMD; TR = 4: 512 threads, two waves per SIMD).
+template <int TR, int KK>
+__device__ __forceinline__ void gj_step(double (&a)[TR][kTl], GjLds<double>& sh, int kg, int rg, int cg) {
   const int k = kTl * kg + KK;
   constexpr int par = KK & 1;  // kTl is even: k and KK share parity
+  constexpr int RPG = kTl / TR;  // row groups per column group
   // 1 / pivot: v_rcp_f64 + two Newton steps (within an ulp of the IEEE
   // quotient; the refinement absorbs the rest) -- 3 dependent FMAs instead of
   // the ~8-deep IEEE division sequence on the critical path of every column
@@ -206,7 +208,7 @@ __device__ __forceinline__ void gj_step(double (&a)[kTl][kTl], GjLds<double>& sh
   double pk = __builtin_amdgcn_rcp(piv);
   pk = fma(pk, fma(-piv, pk, 1.0), pk);
   pk = fma(pk, fma(-piv, pk, 1.0), pk);
-  double u[kTl], g[kTl];
+  double u[kTl], g[TR];
 #pragma unroll
   for (int j = 0; j < kTl; j += 2) {
     const double2 v = *reinterpret_cast<const double2*>(&sh.row[par][kTl * cg + j]);
@@ -214,61 +216,64 @@ __device__ __forceinline__ void gj_step(double (&a)[kTl][kTl], GjLds<double>& sh
     u[j + 1] = v.y * pk;
   }
 #pragma unroll
-  for (int i = 0; i < kTl; i += 2) {
-    const double2 v = *reinterpret_cast<const double2*>(&sh.col[par][kTl * rg + i]);
+  for (int i = 0; i < TR; i += 2) {
+    const double2 v = *reinterpret_cast<const double2*>(&sh.col[par][TR * rg + i]);
     g[i] = v.x;
     g[i + 1] = v.y;
   }
   u[KK] = (cg == kg) ? 1.0 + pk : u[KK];
-  g[KK] -= (rg == kg) ? 1.0 : 0.0;
+  g[KK % TR] -= (rg == RPG * kg + KK / TR) ? 1.0 : 0.0;
+  // next step's pivot row (in-tile row r1 of row group rg1) and column
   constexpr int kk1 = (KK + 1) % kTl;
+  constexpr int r1 = (KK + 1) % TR;
   const int kg1 = KK + 1 == kTl ? kg + 1 : kg;
+  const int rg1 = (k + 1) / TR;
   const bool more = k + 1 < NB;
   // the next step's pivot row / column first: their LDS stores then drain
   // under the bulk of the update instead of after it
 #pragma unroll
-  for (int j = 0; j < kTl; ++j) a[kk1][j] = fma(-g[kk1], u[j], a[kk1][j]);
+  for (int j = 0; j < kTl; ++j) a[r1][j] = fma(-g[r1], u[j], a[r1][j]);
 #pragma unroll
-  for (int i = 0; i < kTl; ++i)
-    if (i != kk1) a[i][kk1] = fma(-g[i], u[kk1], a[i][kk1]);
-  if (more && rg == kg1) {
+  for (int i = 0; i < TR; ++i)
+    if (i != r1) a[i][kk1] = fma(-g[i], u[kk1], a[i][kk1]);
+  if (more && rg == rg1) {
 #pragma unroll
     for (int j = 0; j < kTl; j += 2)
-      *reinterpret_cast<double2*>(&sh.row[par ^ 1][kTl * cg + j]) = make_double2(a[kk1][j], a[kk1][j + 1]);
+      *reinterpret_cast<double2*>(&sh.row[par ^ 1][kTl * cg + j]) = make_double2(a[r1][j], a[r1][j + 1]);
   }
   if (more && cg == kg1) {
 #pragma unroll
-    for (int i = 0; i < kTl; i += 2)
-      *reinterpret_cast<double2*>(&sh.col[par ^ 1][kTl * rg + i]) = make_double2(a[i][kk1], a[i + 1][kk1]);
+    for (int i = 0; i < TR; i += 2)
+      *reinterpret_cast<double2*>(&sh.col[par ^ 1][TR * rg + i]) = make_double2(a[i][kk1], a[i + 1][kk1]);
   }
 #pragma unroll
-  for (int i = 0; i < kTl; ++i)
+  for (int i = 0; i < TR; ++i)
 #pragma unroll
     for (int j = 0; j < kTl; ++j)
-      if (i != kk1 && j != kk1) a[i][j] = fma(-g[i], u[j], a[i][j]);
+      if (i != r1 && j != kk1) a[i][j] = fma(-g[i], u[j], a[i][j]);
   __syncthreads();
 }
 
-template <int... KK>
-__device__ __forceinline__ void gj_steps(double (&a)[kTl][kTl], GjLds<double>& sh, int kg, int rg, int cg,
+template <int TR, int... KK>
+__device__ __forceinline__ void gj_steps(double (&a)[TR][kTl], GjLds<double>& sh, int kg, int rg, int cg,
                                          std::integer_sequence<int, KK...>) {
-  (gj_step<KK>(a, sh, kg, rg, cg), ...);
+  (gj_step<TR, KK>(a, sh, kg, rg, cg), ...);
 }
 
 // Dinv = A[k0.., k0..]^-1 (fp64, row-major NB x NB) of the T block of A; with
 // Tinv, also a T copy (the fp32 engine's GEMM operand).  The block is read,
 // not modified.  info: atomicMin of 1 + k0 when the inverse is not finite (a
 // zero / tiny pivot).
-template <typename T>
-__global__ __launch_bounds__(kGT) void diag_inv_kernel(const T* __restrict__ A, int64_t lda, int k0,
-                                                      double* __restrict__ Dinv, T* __restrict__ Tinv,
-                                                      int* __restrict__ info) {
+template <typename T, int TR>
+__global__ __launch_bounds__(16 * NB / TR) void diag_inv_kernel(const T* __restrict__ A, int64_t lda, int k0,
+                                                               double* __restrict__ Dinv, T* __restrict__ Tinv,
+                                                               int* __restrict__ info) {
   __shared__ GjLds<double> sh;
   const int t = threadIdx.x, rg = t >> 4, cg = t & 15;
-  double a[kTl][kTl];
+  double a[TR][kTl];
 #pragma unroll
-  for (int i = 0; i < kTl; ++i) {
-    const T* src = A + (int64_t)(k0 + kTl * rg + i) * lda + k0 + kTl * cg;
+  for (int i = 0; i < TR; ++i) {
+    const T* src = A + (int64_t)(k0 + TR * rg + i) * lda + k0 + kTl * cg;
 #pragma unroll
     for (int j = 0; j < kTl; ++j) a[i][j] = (double)src[j];
   }
@@ -278,26 +283,42 @@ __global__ __launch_bounds__(kGT) void diag_inv_kernel(const T* __restrict__ A, 
   }
   if (cg == 0) {
 #pragma unroll
-    for (int i = 0; i < kTl; ++i) sh.col[0][kTl * rg + i] = a[i][0];
+    for (int i = 0; i < TR; ++i) sh.col[0][TR * rg + i] = a[i][0];
   }
   __syncthreads();
-  for (int kg = 0; kg < NB / kTl; ++kg) gj_steps(a, sh, kg, rg, cg, std::make_integer_sequence<int, kTl>{});
+  for (int kg = 0; kg < NB / kTl; ++kg) gj_steps<TR>(a, sh, kg, rg, cg, std::make_integer_sequence<int, kTl>{});
   bool fin = true;
 #pragma unroll
-  for (int i = 0; i < kTl; ++i) {
-    double* dst = Dinv + (int64_t)(kTl * rg + i) * NB + kTl * cg;
+  for (int i = 0; i < TR; ++i) {
+    double* dst = Dinv + (int64_t)(TR * rg + i) * NB + kTl * cg;
 #pragma unroll
     for (int j = 0; j < kTl; ++j) {
       fin = fin && isfinite(a[i][j]);
       dst[j] = a[i][j];
     }
     if (Tinv) {
-      T* tdst = Tinv + (int64_t)(kTl * rg + i) * NB + kTl * cg;
+      T* tdst = Tinv + (int64_t)(TR * rg + i) * NB + kTl * cg;
 #pragma unroll
       for (int j = 0; j < kTl; ++j) tdst[j] = (T)a[i][j];
     }
   }
   if (!fin) atomicMin(info, k0 + 1);
+}
+
+// Launch of the diagonal inverse: GELIM_GJ_TR = 8 (256 threads) or 4 (512).
+int diag_inv(double* M, int64_t ldm, int64_t k0, double* Di, int* info, hipStream_t s) {
+  static const int tr = [] {
+    const char* e = std::getenv("GELIM_GJ_TR");
+    return e && std::atoi(e) == 4 ? 4 : 8;
+  }();
+  if (tr == 4)
+    hipLaunchKernelGGL((diag_inv_kernel<double, 4>), dim3(1), dim3(16 * NB / 4), 0, s, M, ldm, (int)k0, Di,
+                       (double*)nullptr, info);
+  else
+    hipLaunchKernelGGL((diag_inv_kernel<double, 8>), dim3(1), dim3(16 * NB / 8), 0, s, M, ldm, (int)k0, Di,
+                       (double*)nullptr, info);
+  HIP_TRY(hipGetLastError());
+  return GELIM_OK;
 }
 
 // ---- persistent block triangular solves ----------------------------------------
@@ -544,9 +565,7 @@ int factor_impl(double* M, int64_t ldm, int64_t np, double* Dinv, double* W, flo
                 hipStream_t s) {
   for (int64_t k0 = 0; k0 < np; k0 += NB) {
     double* Di = Dinv + (k0 / NB) * NB * NB;
-    hipLaunchKernelGGL(diag_inv_kernel<double>, dim3(1), dim3(kGT), 0, s, M, ldm, (int)k0, Di, (double*)nullptr,
-                       info);
-    HIP_TRY(hipGetLastError());
+    GELIM_TRY(diag_inv(M, ldm, k0, Di, info, s));
     const int64_t rest = np - k0 - NB;
     if (rest <= 0) break;
     double* A12 = M + k0 * ldm + k0 + NB;
@@ -574,8 +593,7 @@ int factor_impl(double* M, int64_t ldm, int64_t np, double* Dinv, double* W, flo
 int factor_la(double* M, int64_t ldm, int64_t np, double* Dinv, double* W2, int* info, hipStream_t s,
               hipStream_t side, hipEvent_t e0, hipEvent_t e1, int cap) {
   const int64_t nblk = np / NB;
-  hipLaunchKernelGGL(diag_inv_kernel<double>, dim3(1), dim3(kGT), 0, s, M, ldm, 0, Dinv, (double*)nullptr, info);
-  HIP_TRY(hipGetLastError());
+  GELIM_TRY(diag_inv(M, ldm, 0, Dinv, info, s));
   bool side_used = false;
   for (int64_t k = 0; k + 1 < nblk; ++k) {
     const int64_t k0 = k * NB, rest = np - k0 - NB, rest2 = rest - NB;
@@ -595,9 +613,7 @@ int factor_la(double* M, int64_t ldm, int64_t np, double* Dinv, double* W2, int*
       HIP_TRY(hipEventRecord(e1, side));
       side_used = true;
     }
-    hipLaunchKernelGGL(diag_inv_kernel<double>, dim3(1), dim3(kGT), 0, s, M, ldm, (int)(k0 + NB),
-                       Dinv + (k + 1) * NB * NB, (double*)nullptr, info);
-    HIP_TRY(hipGetLastError());
+    GELIM_TRY(diag_inv(M, ldm, k0 + NB, Dinv + (k + 1) * NB * NB, info, s));
   }
   if (side_used) HIP_TRY(hipStreamWaitEvent(s, e1, 0));
   return GELIM_OK;

@@ -619,6 +619,62 @@ int factor_la(double* M, int64_t ldm, int64_t np, double* Dinv, double* W2, int*
   return GELIM_OK;
 }
 
+// Lookahead with PAIRS of blocks per trailing update (fp64): the big update
+// runs once per two blocks with K = 256 (dgemm 41-43 TF/s at K = 256 vs ~32
+// at K = 128, and half the C traffic), and the main stream works one pair
+// ahead of it.  Pair p = blocks (k, k+1), whose block rows / columns are up
+// to date when it starts; main stream:
+//   W1 = D_k A[k, k+1:]  (rows 0..127 of the pair's W)
+//   A[k+1:, k+1] -= A[k+1:, k] W1[:, k+1];  A[k+1, k+2:] -= A[k+1, k] W1[:, k+2:]
+//   D_{k+1};  W2 = D_{k+1} A[k+1, k+2:]  (rows 128..255, column offset 128)
+//   [wait: side's update of pair p-1]
+//   next pair's panel (block columns k+2, k+3, all rows below; then their block
+//   rows right of them): -= A[., k:k+2] [W1; W2] (K = 256)
+//   D_{k+2}, and on to pair p+1 -- while the side stream runs
+//   A[k+4:, k+4:] -= A[k+4:, k:k+2] [W1; W2][:, k+4:]  (K = 256).
+// The pair's W is double-buffered (side reads pair p while main builds p+1).
+int factor_la2(double* M, int64_t ldm, int64_t np, double* Dinv, double* W4, int* info, hipStream_t s,
+               hipStream_t side, hipEvent_t e0, hipEvent_t e1, int cap) {
+  const int64_t nblk = np / NB;
+  GELIM_TRY(diag_inv(M, ldm, 0, Dinv, info, s));
+  bool side_used = false;
+  for (int64_t k = 0, pair = 0; k + 1 < nblk; k += 2, ++pair) {
+    const int64_t k0 = k * NB, r1 = np - k0 - NB;  // columns right of block k
+    double* Wp = W4 + (pair & 1) * 2 * NB * np;    // 2 NB rows, ld r1
+    double* Ak = M + (k0 + NB) * ldm + k0;         // A[k+1:, k]
+    GELIM_TRY(dgemm_ex(Wp, r1, Dinv + k * NB * NB, NB, M + k0 * ldm + k0 + NB, ldm, NB, r1, NB, 1.0, 0, s));
+    // step k on block k+1: its column (rows k+1..), its row (columns k+2..)
+    GELIM_TRY(dgemm_ex(M + (k0 + NB) * ldm + k0 + NB, ldm, Ak, ldm, Wp, r1, r1, NB, NB, -1.0, 1, s));
+    const int64_t r2 = r1 - NB;  // columns right of block k+1
+    if (r2 > 0)
+      GELIM_TRY(dgemm_ex(M + (k0 + NB) * ldm + k0 + 2 * NB, ldm, Ak, ldm, Wp + NB, r1, NB, r2, NB, -1.0, 1, s));
+    GELIM_TRY(diag_inv(M, ldm, k0 + NB, Dinv + (k + 1) * NB * NB, info, s));
+    if (r2 <= 0) break;  // block k+1 was the last
+    GELIM_TRY(dgemm_ex(Wp + NB * r1 + NB, r1, Dinv + (k + 1) * NB * NB, NB, M + (k0 + NB) * ldm + k0 + 2 * NB, ldm,
+                       NB, r2, NB, 1.0, 0, s));
+    if (side_used) HIP_TRY(hipStreamWaitEvent(s, e1, 0));  // side's pair p-1 update (rows / columns >= k+2)
+    // the next pair's panel: block columns k+2 .. k+2+pw (all rows >= k+2),
+    // then its block rows right of it
+    const int64_t pw = std::min<int64_t>(2 * NB, r2);   // panel width
+    const int64_t r4 = r2 - pw;                        // columns right of the panel
+    double* A2 = M + (k0 + 2 * NB) * ldm + k0;         // A[k+2:, k:k+2]
+    GELIM_TRY(dgemm_ex(M + (k0 + 2 * NB) * ldm + k0 + 2 * NB, ldm, A2, ldm, Wp + NB, r1, r2, pw, 2 * NB, -1.0, 1, s));
+    if (r4 > 0) {
+      GELIM_TRY(dgemm_ex(M + (k0 + 2 * NB) * ldm + k0 + 2 * NB + pw, ldm, A2, ldm, Wp + NB + pw, r1, pw, r4, 2 * NB,
+                         -1.0, 1, s));
+      HIP_TRY(hipEventRecord(e0, s));
+      HIP_TRY(hipStreamWaitEvent(side, e0, 0));
+      GELIM_TRY(dgemm_capped(M + (k0 + 2 * NB + pw) * ldm + k0 + 2 * NB + pw, ldm, M + (k0 + 2 * NB + pw) * ldm + k0,
+                             ldm, Wp + NB + pw, r1, r4, r4, 2 * NB, -1.0, cap, side, 1));
+      HIP_TRY(hipEventRecord(e1, side));
+      side_used = true;
+    }
+    GELIM_TRY(diag_inv(M, ldm, k0 + 2 * NB, Dinv + (k + 2) * NB * NB, info, s));
+  }
+  if (side_used) HIP_TRY(hipStreamWaitEvent(s, e1, 0));
+  return GELIM_OK;
+}
+
 // Block-LDU solve: forward z_k = D_k^-1 (c_k - sum_{j<k} A_kj z_j) keeping
 // y_k = c_k - sum (the block-unit-lower solve's result), then backward
 // x_k = D_k^-1 (y_k - sum_{j>k} A_kj x_j).  c -> (z, y) -> x (x may alias c:
@@ -668,7 +724,7 @@ struct gelim_mixed_plan {
   int fp64 = 0;             // factor precision: 0 fp32 ("hip-mixed"), 1 fp64 ("hip-rbt")
   double* M = nullptr;      // np x ldm: the transformed matrix, then its block-LDU factor
   double* Dinv = nullptr;   // nblk x NB x NB: inverse of every (Schur) diagonal block
-  double* W = nullptr;      // 2 x NB x np: A_kk^-1 A_k,rest (double-buffered under lookahead)
+  double* W = nullptr;      // 4 x NB x np: A_kk^-1 A_k,rest (pairs of blocks, double-buffered under lookahead)
   float* A21f = nullptr;    // np x NB, NB x np: rounded GEMM operands (fp32 engine only)
   float* Wf = nullptr;
   double* ud = nullptr;     // U's butterfly diagonals (8 x np/4)
@@ -730,7 +786,7 @@ extern "C" gelim_mixed_plan* gelim_mixed_plan_create2(int64_t n, const double* u
   const int64_t nblk = np / gelim::NB;
   if (hipMalloc((void**)&p->M, sizeof(double) * (size_t)np * p->ldm) != hipSuccess) return fail("matrix");
   if (hipMalloc((void**)&p->Dinv, sizeof(double) * (size_t)np * gelim::NB) != hipSuccess) return fail("inverses");
-  if (hipMalloc((void**)&p->W, 2 * sizeof(double) * (size_t)np * gelim::NB) != hipSuccess) return fail("W buffer");
+  if (hipMalloc((void**)&p->W, 4 * sizeof(double) * (size_t)np * gelim::NB) != hipSuccess) return fail("W buffer");
   // lookahead (fp64): from 32 blocks (n = 4096) unless GELIM_RBT_LOOKAHEAD says otherwise
   {
     const char* e = std::getenv("GELIM_RBT_LOOKAHEAD");
@@ -787,7 +843,13 @@ extern "C" int gelim_mixed_factor(gelim_mixed_plan* p, const double* aug, int64_
   hipLaunchKernelGGL(rbt_matrix_kernel<double>, grid, dim3(256), 0, s, aug, ld, (int)p->n, (int)np, p->ud, p->vd,
                      p->M, ldm);
   HIP_TRY(hipGetLastError());
-  if (p->lookahead)
+  static const int pairs = [] {
+    const char* e = std::getenv("GELIM_RBT_PAIRS");
+    return e ? std::atoi(e) : 1;
+  }();
+  if (p->lookahead && pairs)
+    GELIM_TRY(factor_la2(p->M, ldm, np, p->Dinv, p->W, p->info, s, p->side, p->e0, p->e1, p->cap));
+  else if (p->lookahead)
     GELIM_TRY(factor_la(p->M, ldm, np, p->Dinv, p->W, p->info, s, p->side, p->e0, p->e1, p->cap));
   else
     GELIM_TRY(factor_impl(p->M, ldm, np, p->Dinv, p->W, p->fp64 ? nullptr : p->A21f, p->fp64 ? nullptr : p->Wf,

@@ -740,7 +740,8 @@ struct gelim_mixed_plan {
   double* dv = nullptr;
   double* xb = nullptr;
   double* om = nullptr;     // device scalar: the backward error
-  int lookahead = 0;        // fp64 engine: one-block lookahead on a side stream
+  int lookahead = 0;        // fp64 engine: lookahead on a side stream
+  int pairs = 1;            // lookahead over pairs of blocks (K = 256 trailing updates)
   int cap = 0;              // side-stream GEMM grid cap (CUs)
   hipStream_t side = nullptr;
   hipEvent_t e0 = nullptr, e1 = nullptr;
@@ -791,6 +792,8 @@ extern "C" gelim_mixed_plan* gelim_mixed_plan_create2(int64_t n, const double* u
   {
     const char* e = std::getenv("GELIM_RBT_LOOKAHEAD");
     p->lookahead = fp64 && (e ? std::atoi(e) != 0 : np >= 4096);
+    const char* ep = std::getenv("GELIM_RBT_PAIRS");
+    p->pairs = ep ? std::atoi(ep) != 0 : 1;
   }
   if (p->lookahead) {
     int dev = 0, ncu = 256;
@@ -843,11 +846,7 @@ extern "C" int gelim_mixed_factor(gelim_mixed_plan* p, const double* aug, int64_
   hipLaunchKernelGGL(rbt_matrix_kernel<double>, grid, dim3(256), 0, s, aug, ld, (int)p->n, (int)np, p->ud, p->vd,
                      p->M, ldm);
   HIP_TRY(hipGetLastError());
-  static const int pairs = [] {
-    const char* e = std::getenv("GELIM_RBT_PAIRS");
-    return e ? std::atoi(e) : 1;
-  }();
-  if (p->lookahead && pairs)
+  if (p->lookahead && p->pairs)
     GELIM_TRY(factor_la2(p->M, ldm, np, p->Dinv, p->W, p->info, s, p->side, p->e0, p->e1, p->cap));
   else if (p->lookahead)
     GELIM_TRY(factor_la(p->M, ldm, np, p->Dinv, p->W, p->info, s, p->side, p->e0, p->e1, p->cap));

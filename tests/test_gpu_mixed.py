@@ -123,7 +123,7 @@ def test_diag_inverses_and_factor(gelim, cuda, backend, n):
     s.close()
 
 
-@pytest.mark.parametrize("n", [1, 100, 1000, 2048, 4000, 8192])
+@pytest.mark.parametrize("n", [1, 100, 129, 1000, 2048, 4000, 4200, 5000, 8192])
 def test_rbt_random_reaches_fp64(gelim, cuda, n):
     """fp64 block-LDU factors: a few classic refinement steps (each
     contracts the error by ~cond(A_bb) eps64 of the worst diagonal block)."""
@@ -176,3 +176,21 @@ def test_rbt_singular_raises(gelim, cuda):
     with pytest.raises(gelim.SingularMatrixError):
         s.solve(aug, check=True)
     assert s.last_fallback is not None
+
+
+@pytest.mark.parametrize("env", [{}, {"GELIM_RBT_LOOKAHEAD": "0"}, {"GELIM_RBT_PAIRS": "0"}])
+def test_rbt_schedules_agree(gelim, cuda, env, monkeypatch):
+    """The three factorisation schedules -- lookahead over pairs (the default
+    from n = 4096), one-block lookahead, no lookahead; all read when the plan
+    is created -- give fp64-class answers on 4200 = 33 blocks (an odd count:
+    the pair loop ends on a single block)."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    n = 4200
+    aug = gelim.random_system(n, seed=77, device=cuda)
+    s = gelim.GaussSolver(n, backend="hip-rbt", device=cuda)
+    x = s.solve(aug, check=True)
+    assert s.last_fallback is None, s.last_fallback
+    ref = torch.linalg.solve(aug[:, :n], aug[:, n])
+    assert ((x - ref).abs().max() / ref.abs().max()).item() < 1e-9
+    s.close()

@@ -781,8 +781,12 @@ __device__ __forceinline__ void updater(const Args& g, Shared& sh, int s) {
   }
 }
 
+// Up to 2 slots two workgroups may share a CU (128 VGPRs); 3 and 4 slots (the
+// n <= 1536 / 2048 engines: np + 1 <= 129 workgroups, one per CU) get the
+// whole 256-VGPR budget -- with (NT, 2) the 4-slot engine spilled 137 VGPRs
+// to scratch (profiles/graph_recapture.txt: resident 2048 5.6 ms).
 template <int R, int MODE>
-__global__ __launch_bounds__(NT, 2) void rlu_kernel(Args g) {
+__global__ __launch_bounds__(NT, R <= 2 ? 2 : 1) void rlu_kernel(Args g) {
   __shared__ Shared sh;
   if (blockIdx.x == 0)
     engine<R, MODE>(g, sh);
@@ -798,7 +802,7 @@ struct Layout {
 
 Layout layout(int64_t n) {
   Layout L;
-  L.R = n <= 512 ? 1 : n <= 1024 ? 2 : n <= 2048 ? 4 : 0;
+  L.R = n <= 512 ? 1 : n <= 1024 ? 2 : n <= 1536 ? 3 : n <= 2048 ? 4 : 0;
   if (!L.R || n < 1) return Layout{};
   L.np = (int)((n + kW - 1) / kW);
   auto up = [](size_t b) { return (b + 255) & ~size_t(255); };
@@ -835,6 +839,7 @@ bool rlu_coresident(int64_t n) {
   hipError_t e = hipSuccess;
   if (L.R == 1) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, rlu_kernel<1, 1>, NT, 0);
   else if (L.R == 2) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, rlu_kernel<2, 1>, NT, 0);
+  else if (L.R == 3) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, rlu_kernel<3, 1>, NT, 0);
   else e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, rlu_kernel<4, 1>, NT, 0);
   return e == hipSuccess && coresident(per, L.np + 1);
 }
@@ -880,6 +885,9 @@ int rlu_factor(const double* src, int64_t lds, double* work, int64_t ldw, int64_
   } else if (L.R == 2) {
     if (part) hipLaunchKernelGGL((rlu_kernel<2, 1>), grid, block, 0, s, a);
     else hipLaunchKernelGGL((rlu_kernel<2, 0>), grid, block, 0, s, a);
+  } else if (L.R == 3) {
+    if (part) hipLaunchKernelGGL((rlu_kernel<3, 1>), grid, block, 0, s, a);
+    else hipLaunchKernelGGL((rlu_kernel<3, 0>), grid, block, 0, s, a);
   } else {
     if (part) hipLaunchKernelGGL((rlu_kernel<4, 1>), grid, block, 0, s, a);
     else hipLaunchKernelGGL((rlu_kernel<4, 0>), grid, block, 0, s, a);

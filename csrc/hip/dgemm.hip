@@ -16,13 +16,18 @@
 //  * K in steps of BK = 16, A and B tiles double-buffered in LDS (one barrier
 //    per step); A is stored transposed ([k][m]) and negated when alpha < 0,
 //    B as is ([k][n]); rows padded to 144 doubles so the two 16-lane halves
-//    of every ds_read_b64 land on disjoint bank sets;
+//    of every ds_read_b64 land on disjoint bank sets; the transposed A tile
+//    is XOR-swizzled (column m ^ (k & 14)) so its ds_write_b64 stores are
+//    conflict-free (unswizzled: 8-way, 64 % of the kernel's LDS cycles,
+//    profiles/pmc_rbt_8192.txt);
 //  * f64 MFMA operand maps (cdna_hip_programming.md §3): A lane l holds
 //    A[l&15][k=l>>4], B lane l holds B[k=l>>4][l&15], C/D register r of lane l
 //    is C[row=(l>>4)+4r][col=l&15] (NOT the f32 C/D map);
 //  * C is read into the accumulators up front and written back once;
 //  * tiles are dealt to XCDs in contiguous runs (consecutive tiles share an
-//    A row panel -> same L2).
+//    A row panel -> same L2); GELIM_DGEMM_GROUP=g deals a grouped order
+//    instead (runs of g tile rows, column-major inside a run) -- measured
+//    within noise for g = 4, 8, 16 (profiles/dgemm_r3_lds.txt).
 // Interior tiles use 16-byte loads with no bounds logic; edge tiles clamp
 // rows/columns (results outside C are never stored) and zero k >= K.
 // Contract (checked on the host): A and B 16-byte aligned, lda / ldb / K
@@ -68,7 +73,25 @@ struct Args {
   int tiles_n, ntiles;
   double alpha;
   int acc;  // 1: C += alpha A B, 0: C = alpha A B (C is not read)
+  int group;  // tile order: runs of `group` tile rows, column-major inside a run (<= 1: row-major)
 };
+
+// Tile index -> (tile row, tile column).  Grouped order: the 64 workgroups an
+// XCD runs at once (consecutive indices of its run) cover an 8 x 8 block of
+// tiles -- 8 A row panels and 8 B column panels through that XCD's L2 instead
+// of 1 A panel and 64 B panels (row-major order).
+__device__ __forceinline__ void tile_coords(const Args& g, int tile, int& tr, int& tc) {
+  if (g.group <= 1) {
+    tr = tile / g.tiles_n;
+    tc = tile % g.tiles_n;
+    return;
+  }
+  const int tiles_m = g.ntiles / g.tiles_n, per = g.group * g.tiles_n;
+  const int gid = tile / per, first = gid * g.group, l = tile - gid * per;
+  const int gs = min(tiles_m - first, g.group);
+  tr = first + l % gs;
+  tc = l / gs;
+}
 
 // 16-byte chunks per thread per tile: A Tx16 -> T*8 chunks, B 16xT -> T*8
 template <int T>
@@ -119,8 +142,11 @@ __device__ __forceinline__ void store_stage(const Stage<T>& st, double* As, doub
   for (int h = 0; h < kCA; ++h) {
     const int idx = t + kThreads * h;
     const int row = idx >> 3, kc = (idx & 7) * 2;
-    As[kc * SA_ + row] = alpha * st.a[h].x;
-    As[(kc + 1) * SA_ + row] = alpha * st.a[h].y;
+    // XOR swizzle: element (k, m) lives at column m ^ (k & 14), so the 8
+    // k-chunks of one row that a 16-lane store group holds land on 8
+    // distinct bank pairs instead of one (8-way -> conflict-free)
+    As[kc * SA_ + (row ^ kc)] = alpha * st.a[h].x;
+    As[(kc + 1) * SA_ + (row ^ kc)] = alpha * st.a[h].y;
   }
 #pragma unroll
   for (int h = 0; h < kCB; ++h) {
@@ -143,6 +169,10 @@ __device__ __forceinline__ void tile_body(const Args& g, int m0, int n0, double*
   const int wm = (wave >> 1) * WM, wn = (wave & 1) * WN;
   const int r16 = lane & 15, q = lane >> 4;
 
+  // the first stage's loads go out before C's, so its LDS store waits only
+  // for them (vmcnt is in order)
+  Stage<T> st;
+  load_stage<FULL, T>(st, g, m0, n0, 0, t);
   dev::d4 acc[MB][NB];
 #pragma unroll
   for (int i = 0; i < MB; ++i)
@@ -154,26 +184,25 @@ __device__ __forceinline__ void tile_body(const Args& g, int m0, int n0, double*
         const int row = m0 + wm + 16 * i + q + 4 * r;
         // edge tiles: clamped address, the value is never stored back
         acc[i][j][r] = g.acc ? g.C[(int64_t)(FULL ? row : min(row, g.M - 1)) * g.ldc + (FULL ? col : min(col, g.N - 1))]
-                             : 0.0;
+                           : 0.0;
       }
     }
 
-  Stage<T> st;
-  load_stage<FULL, T>(st, g, m0, n0, 0, t);
   store_stage<T>(st, As[0], Bs[0], g.alpha, t);
   __syncthreads();
   const int nk = (g.K + BK - 1) / BK;
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
     if (kt + 1 < nk) load_stage<FULL, T>(st, g, m0, n0, (kt + 1) * BK, t);
-    const double* a_s = As[cur] + wm + r16;
+    const double* a_s = As[cur] + wm;
     const double* b_s = Bs[cur] + wn + r16;
 #pragma unroll
     for (int kk = 0; kk < BK; kk += 4) {
       const int k = kk + q;
+      const int ac = k * SA + (r16 ^ (k & 14));  // the swizzled column of A(m = .. + r16, k)
       double af[MB], bf[NB];
 #pragma unroll
-      for (int i = 0; i < MB; ++i) af[i] = a_s[k * SA + 16 * i];
+      for (int i = 0; i < MB; ++i) af[i] = a_s[ac + 16 * i];
 #pragma unroll
       for (int j = 0; j < NB; ++j) bf[j] = b_s[k * SB + 16 * j];
 #pragma unroll
@@ -207,7 +236,9 @@ __global__ __launch_bounds__(kThreads, 2) void dgemm_kernel(Args g) {
   const int orig = blockIdx.x;
   const int q = g.ntiles / 8, rem = g.ntiles % 8, xcd = orig % 8;
   const int tile = (xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q) + orig / 8;
-  const int m0 = (tile / g.tiles_n) * T, n0 = (tile % g.tiles_n) * T;
+  int tr, tc;
+  tile_coords(g, tile, tr, tc);
+  const int m0 = tr * T, n0 = tc * T;
   if (m0 + T <= g.M && n0 + T <= g.N && (g.K % BK) == 0)
     tile_body<true, T>(g, m0, n0, lds, threadIdx.x);
   else
@@ -237,7 +268,9 @@ __global__ __launch_bounds__(kPThreads, 1) void dgemm_persist_kernel(Args g) {
     const int tile0 = 2 * pr + half;
     const bool store = tile0 < g.ntiles;
     const int tile = store ? tile0 : g.ntiles - 1;
-    const int m0 = (tile / g.tiles_n) * BM, n0 = (tile % g.tiles_n) * BN;
+    int tr, tc;
+    tile_coords(g, tile, tr, tc);
+    const int m0 = tr * BM, n0 = tc * BN;
     // an opaque copy of t per pair: nothing thread-dependent is hoisted out
     // of the loop (hoisted address terms pushed the body past 256 VGPRs)
     int tt = t;
@@ -265,7 +298,11 @@ int dgemm_capped(double* C, int64_t ldc, const double* A, int64_t lda, const dou
     return GELIM_FAIL(GELIM_E_ARG, "dgemm: unsupported alignment / leading dimensions (K=" + std::to_string(K) +
                                        " lda=" + std::to_string(lda) + " ldb=" + std::to_string(ldb) + ")");
   const int tm = (int)((M + BM - 1) / BM), tn = (int)((N + BN - 1) / BN);
-  Args g{C, ldc, A, lda, B, ldb, (int)M, (int)N, (int)K, tn, tm * tn, alpha, accumulate ? 1 : 0};
+  static const int group = [] {
+    const char* e = std::getenv("GELIM_DGEMM_GROUP");
+    return e ? std::atoi(e) : 1;  // grouped orders 4 / 8 / 16 measured within noise of row-major
+  }();
+  Args g{C, ldc, A, lda, B, ldb, (int)M, (int)N, (int)K, tn, tm * tn, alpha, accumulate ? 1 : 0, group};
   // max_wg > 0: at most max_wg CUs (rounded down to a multiple of 8)
   const int cap = max_wg > 0 ? std::max(8, max_wg / 8 * 8) : 0;
   // few tiles: one 256-thread workgroup per tile already stays within the

@@ -188,36 +188,52 @@ __global__ __launch_bounds__(256) void rbt_vec_kernel(const double* __restrict__
 // more corrections and fell back at n >= 4096).
 constexpr int kTl = 8;    // tile columns (and rows, TR = 8)
 
+// Row k / column k as 16 chunks of 8 doubles at a stride of 10: a
+// ds_read_b128 lane group reads all 16 chunks at once (16 distinct column
+// groups), and at a stride of 8 they fell on 4 bank sets (4-way, 42 % of the
+// kernel's LDS cycles, profiles/pmc_rbt_8192.txt); at 10 (80 B = 20 banks)
+// they tile the 64 banks exactly.
+constexpr int kGjStride = kTl + 2;
+constexpr int gj_at(int i) { return (i / kTl) * kGjStride + i % kTl; }
+
 template <typename TI>
 struct alignas(16) GjLds {
-  TI row[2][NB];
-  TI col[2][NB];
+  TI row[2][NB / kTl * kGjStride];
+  TI col[2][NB / kTl * kGjStride];
 };
+
+// 1 / pivot: v_rcp_f64 + two Newton steps (within an ulp of the IEEE
+// quotient; the refinement absorbs the rest) -- 3 dependent FMAs instead of
+// the ~8-deep IEEE division sequence on the critical path of every column
+__device__ __forceinline__ double gj_recip(double piv) {
+  double pk = __builtin_amdgcn_rcp(piv);
+  pk = fma(pk, fma(-piv, pk, 1.0), pk);
+  return fma(pk, fma(-piv, pk, 1.0), pk);
+}
 
 // Step k = 8 kg + KK of the Gauss-Jordan inverse on TR x 8 tiles (TR = 8:
 // 256 threads, one wave per SIMD; TR = 4: 512 threads, two waves per SIMD).
+// The raw row / column are published and every thread scales after the
+// barrier (publishing u and g ready to use -- the reciprocal taken from the
+// pivot's lane by v_readlane in the publishing wave -- made the factor 7 %
+// slower: the publisher's longer path before its bulk update is the
+// critical one, profiles/rbt_engine_round3.txt).
 template <int TR, int KK>
 __device__ __forceinline__ void gj_step(double (&a)[TR][kTl], GjLds<double>& sh, int kg, int rg, int cg) {
   const int k = kTl * kg + KK;
   constexpr int par = KK & 1;  // kTl is even: k and KK share parity
   constexpr int RPG = kTl / TR;  // row groups per column group
-  // 1 / pivot: v_rcp_f64 + two Newton steps (within an ulp of the IEEE
-  // quotient; the refinement absorbs the rest) -- 3 dependent FMAs instead of
-  // the ~8-deep IEEE division sequence on the critical path of every column
-  const double piv = sh.row[par][k];
-  double pk = __builtin_amdgcn_rcp(piv);
-  pk = fma(pk, fma(-piv, pk, 1.0), pk);
-  pk = fma(pk, fma(-piv, pk, 1.0), pk);
+  const double pk = gj_recip(sh.row[par][gj_at(k)]);
   double u[kTl], g[TR];
 #pragma unroll
   for (int j = 0; j < kTl; j += 2) {
-    const double2 v = *reinterpret_cast<const double2*>(&sh.row[par][kTl * cg + j]);
+    const double2 v = *reinterpret_cast<const double2*>(&sh.row[par][kGjStride * cg + j]);
     u[j] = v.x * pk;
     u[j + 1] = v.y * pk;
   }
 #pragma unroll
   for (int i = 0; i < TR; i += 2) {
-    const double2 v = *reinterpret_cast<const double2*>(&sh.col[par][TR * rg + i]);
+    const double2 v = *reinterpret_cast<const double2*>(&sh.col[par][gj_at(TR * rg) + i]);
     g[i] = v.x;
     g[i + 1] = v.y;
   }
@@ -239,12 +255,12 @@ __device__ __forceinline__ void gj_step(double (&a)[TR][kTl], GjLds<double>& sh,
   if (more && rg == rg1) {
 #pragma unroll
     for (int j = 0; j < kTl; j += 2)
-      *reinterpret_cast<double2*>(&sh.row[par ^ 1][kTl * cg + j]) = make_double2(a[r1][j], a[r1][j + 1]);
+      *reinterpret_cast<double2*>(&sh.row[par ^ 1][kGjStride * cg + j]) = make_double2(a[r1][j], a[r1][j + 1]);
   }
   if (more && cg == kg1) {
 #pragma unroll
     for (int i = 0; i < TR; i += 2)
-      *reinterpret_cast<double2*>(&sh.col[par ^ 1][TR * rg + i]) = make_double2(a[i][kk1], a[i + 1][kk1]);
+      *reinterpret_cast<double2*>(&sh.col[par ^ 1][gj_at(TR * rg) + i]) = make_double2(a[i][kk1], a[i + 1][kk1]);
   }
 #pragma unroll
   for (int i = 0; i < TR; ++i)
@@ -279,11 +295,11 @@ __global__ __launch_bounds__(16 * NB / TR) void diag_inv_kernel(const T* __restr
   }
   if (rg == 0) {
 #pragma unroll
-    for (int j = 0; j < kTl; ++j) sh.row[0][kTl * cg + j] = a[0][j];
+    for (int j = 0; j < kTl; ++j) sh.row[0][kGjStride * cg + j] = a[0][j];
   }
   if (cg == 0) {
 #pragma unroll
-    for (int i = 0; i < TR; ++i) sh.col[0][TR * rg + i] = a[i][0];
+    for (int i = 0; i < TR; ++i) sh.col[0][gj_at(TR * rg) + i] = a[i][0];
   }
   __syncthreads();
   for (int kg = 0; kg < NB / kTl; ++kg) gj_steps<TR>(a, sh, kg, rg, cg, std::make_integer_sequence<int, kTl>{});

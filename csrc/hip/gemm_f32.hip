@@ -11,9 +11,10 @@
 //             block per wave, four workgroups per CU) or, when there are at
 //             least 2 128x128 tiles per CU, 128x64x16 tiles (2x1 blocks per
 //             wave).  LDS holds A transposed ([k][m]) and B as is ([k][n]), so
-//             both fragment reads are unit-stride across lanes; rows padded
-//             by 4 floats (PMC: ~14 % LDS bank-conflict cycles remain on the
-//             transposed A stores, profiles/pmc_counters_2048.txt).
+//             both fragment reads are unit-stride across lanes; A rows padded
+//             by 2 floats, B rows by 4: no LDS bank conflicts (SQ_LDS_BANK_
+//             CONFLICT = 0; 14 % of the LDS cycles with A padded by 4,
+//             profiles/gemm_microbench.txt).
 // The naive kernels use 64-bit indexing (the reference's int products
 // overflow for n > 46340).
 #include <hip/hip_runtime.h>
@@ -69,7 +70,9 @@ __global__ void naive_elem_kernel(Mat p) {
 //    vs 120-121 for 128 x 128 x 32 (GELIM_SGEMM_SHAPE picks any compiled
 //    shape for A/B runs).
 constexpr int kMmThreads = 256;
-constexpr int APAD = 4, BPAD = 4;
+// APAD = 2: a row stride = 2 mod 8 floats puts the 4 k-chunks of the transposed A
+// stores on distinct bank octets (APAD = 4: 2-way, 14 % of the LDS cycles)
+constexpr int APAD = 2, BPAD = 4;
 
 template <int BM, int BN, int BK>
 struct Tile {

@@ -691,6 +691,91 @@ int factor_la2(double* M, int64_t ldm, int64_t np, double* Dinv, double* W4, int
   return GELIM_OK;
 }
 
+// factor_la2 with a third stream (aux) that takes every update the next
+// diagonal inverse does not read, so it runs UNDER that inverse (a one-
+// workgroup kernel) instead of before it.  Per pair (k, k+1):
+//   main: W1 = D_k A[k, k+1:];  A[k+1, k+1] -= A[k+1, k] W1[:, :128]   (diagonal block only)
+//   aux:  A[k+2:, k+1] -= A[k+2:, k] W1[:, :128];  A[k+1, k+2:] -= A[k+1, k] W1[:, 128:]
+//   main: D_{k+1}; [join aux]; W2 = D_{k+1} A[k+1, k+2:]; [wait side p-1; side p may start]
+//   main: panel rows k+2 only: A[k+2, panel] -= A[k+2, k:k+2] [W1; W2][:, panel]
+//   aux:  panel rows k+3..:   A[k+3:, panel] -= ...;  panel's block rows right of it (K = 256)
+//   main: D_{k+2}; [join aux before the next pair]
+// Measured slower than factor_la2 (4096: 4.10 vs 3.96 ms, 8192: 13.64 vs
+// 13.07 ms; forced at 2048: 1.73 vs 1.51 ms without lookahead): the inverse
+// does not speed up by having the GEMMs beside it, and each pair adds four
+// cross-stream event waits.  Off by default (GELIM_RBT_AUX=1).
+// Regions: aux writes column k+1 below block k+1, row k+1 right of it, the
+// panel below its first block row and the panel's block rows right of the
+// panel; the side (after the wait on pair p-1) writes rows and columns past
+// the panel; main writes only what the next inverse reads.  Every region a
+// stream reads was written before the event it waited on.
+int factor_la3(double* M, int64_t ldm, int64_t np, double* Dinv, double* W4, int* info, hipStream_t s,
+               hipStream_t side, hipStream_t aux, hipEvent_t e0, hipEvent_t e1, hipEvent_t ea, hipEvent_t eb,
+               int cap) {
+  const int64_t nblk = np / NB;
+  GELIM_TRY(diag_inv(M, ldm, 0, Dinv, info, s));
+  bool side_used = false, aux_used = false;
+  auto fork = [&]() -> int {  // aux continues after everything main issued so far
+    HIP_TRY(hipEventRecord(ea, s));
+    HIP_TRY(hipStreamWaitEvent(aux, ea, 0));
+    return GELIM_OK;
+  };
+  auto join = [&]() -> int {  // main continues after everything aux issued so far
+    if (!aux_used) return GELIM_OK;
+    HIP_TRY(hipEventRecord(eb, aux));
+    HIP_TRY(hipStreamWaitEvent(s, eb, 0));
+    aux_used = false;
+    return GELIM_OK;
+  };
+  for (int64_t k = 0, pair = 0; k + 1 < nblk; k += 2, ++pair) {
+    GELIM_TRY(join());  // the previous pair's panel below its first block row / block rows right of it
+    const int64_t k0 = k * NB, r1 = np - k0 - NB, r2 = r1 - NB;
+    double* Wp = W4 + (pair & 1) * 2 * NB * np;  // 2 NB rows, ld r1
+    double* Ak = M + (k0 + NB) * ldm + k0;       // A[k+1:, k]
+    GELIM_TRY(dgemm_ex(Wp, r1, Dinv + k * NB * NB, NB, M + k0 * ldm + k0 + NB, ldm, NB, r1, NB, 1.0, 0, s));
+    GELIM_TRY(dgemm_ex(M + (k0 + NB) * ldm + k0 + NB, ldm, Ak, ldm, Wp, r1, NB, NB, NB, -1.0, 1, s));
+    if (r2 > 0) {
+      GELIM_TRY(fork());
+      GELIM_TRY(dgemm_ex(M + (k0 + 2 * NB) * ldm + k0 + NB, ldm, Ak + NB * ldm, ldm, Wp, r1, r2, NB, NB, -1.0, 1, aux));
+      GELIM_TRY(dgemm_ex(M + (k0 + NB) * ldm + k0 + 2 * NB, ldm, Ak, ldm, Wp + NB, r1, NB, r2, NB, -1.0, 1, aux));
+      aux_used = true;
+    }
+    GELIM_TRY(diag_inv(M, ldm, k0 + NB, Dinv + (k + 1) * NB * NB, info, s));
+    if (r2 <= 0) break;  // block k+1 was the last
+    GELIM_TRY(join());
+    GELIM_TRY(dgemm_ex(Wp + NB * r1 + NB, r1, Dinv + (k + 1) * NB * NB, NB, M + (k0 + NB) * ldm + k0 + 2 * NB, ldm,
+                       NB, r2, NB, 1.0, 0, s));
+    if (side_used) HIP_TRY(hipStreamWaitEvent(s, e1, 0));  // side's pair p-1 update (rows / columns >= k+2)
+    const int64_t pw = std::min<int64_t>(2 * NB, r2);  // panel width
+    const int64_t r4 = r2 - pw;                       // columns right of the panel
+    double* A2 = M + (k0 + 2 * NB) * ldm + k0;        // A[k+2:, k:k+2]
+    double* P = M + (k0 + 2 * NB) * ldm + k0 + 2 * NB;  // the panel's first element
+    if (r4 > 0) {
+      // the side's region (rows / columns past the panel) reads only the
+      // final L columns k, k+1 and this pair's W
+      HIP_TRY(hipEventRecord(e0, s));
+      HIP_TRY(hipStreamWaitEvent(side, e0, 0));
+      GELIM_TRY(dgemm_capped(M + (k0 + 2 * NB + pw) * ldm + k0 + 2 * NB + pw, ldm, M + (k0 + 2 * NB + pw) * ldm + k0,
+                             ldm, Wp + NB + pw, r1, r4, r4, 2 * NB, -1.0, cap, side, 1));
+      HIP_TRY(hipEventRecord(e1, side));
+      side_used = true;
+    }
+    GELIM_TRY(dgemm_ex(P, ldm, A2, ldm, Wp + NB, r1, NB, pw, 2 * NB, -1.0, 1, s));  // block row k+2 of the panel
+    if (r2 > NB || r4 > 0) {
+      GELIM_TRY(fork());
+      if (r2 > NB)
+        GELIM_TRY(dgemm_ex(P + NB * ldm, ldm, A2 + NB * ldm, ldm, Wp + NB, r1, r2 - NB, pw, 2 * NB, -1.0, 1, aux));
+      if (r4 > 0)
+        GELIM_TRY(dgemm_ex(P + pw, ldm, A2, ldm, Wp + NB + pw, r1, pw, r4, 2 * NB, -1.0, 1, aux));
+      aux_used = true;
+    }
+    GELIM_TRY(diag_inv(M, ldm, k0 + 2 * NB, Dinv + (k + 2) * NB * NB, info, s));
+  }
+  GELIM_TRY(join());
+  if (side_used) HIP_TRY(hipStreamWaitEvent(s, e1, 0));
+  return GELIM_OK;
+}
+
 // Block-LDU solve: forward z_k = D_k^-1 (c_k - sum_{j<k} A_kj z_j) keeping
 // y_k = c_k - sum (the block-unit-lower solve's result), then backward
 // x_k = D_k^-1 (y_k - sum_{j>k} A_kj x_j).  c -> (z, y) -> x (x may alias c:
@@ -761,6 +846,9 @@ struct gelim_mixed_plan {
   int cap = 0;              // side-stream GEMM grid cap (CUs)
   hipStream_t side = nullptr;
   hipEvent_t e0 = nullptr, e1 = nullptr;
+  int aux_on = 0;              // pairs: updates the next inverse does not read on a third stream (factor_la3)
+  hipStream_t aux = nullptr;
+  hipEvent_t ea = nullptr, eb = nullptr;
 };
 
 extern "C" int64_t gelim_mixed_max_n(void) { return (int64_t)gelim::kMaxBlocks * gelim::NB; }
@@ -771,6 +859,9 @@ extern "C" void gelim_mixed_plan_destroy(gelim_mixed_plan* p) {
                   (void*)p->rv, (void*)p->wv, (void*)p->dv, (void*)p->xb, (void*)p->om, (void*)p->flags, (void*)p->c,
                   (void*)p->y, (void*)p->z, (void*)p->info})
     (void)hipFree(q);
+  if (p->ea) (void)hipEventDestroy(p->ea);
+  if (p->eb) (void)hipEventDestroy(p->eb);
+  if (p->aux) (void)hipStreamDestroy(p->aux);
   if (p->e0) (void)hipEventDestroy(p->e0);
   if (p->e1) (void)hipEventDestroy(p->e1);
   if (p->side) (void)hipStreamDestroy(p->side);
@@ -810,6 +901,8 @@ extern "C" gelim_mixed_plan* gelim_mixed_plan_create2(int64_t n, const double* u
     p->lookahead = fp64 && (e ? std::atoi(e) != 0 : np >= 4096);
     const char* ep = std::getenv("GELIM_RBT_PAIRS");
     p->pairs = ep ? std::atoi(ep) != 0 : 1;
+    const char* ex = std::getenv("GELIM_RBT_AUX");
+    p->aux_on = ex ? std::atoi(ex) != 0 : 0;  // measured slower (profiles/rbt_engine_round3.txt)
   }
   if (p->lookahead) {
     int dev = 0, ncu = 256;
@@ -825,6 +918,11 @@ extern "C" gelim_mixed_plan* gelim_mixed_plan_create2(int64_t n, const double* u
     if (hipStreamCreateWithFlags(&p->side, hipStreamNonBlocking) != hipSuccess) return fail("side stream");
     if (hipEventCreateWithFlags(&p->e0, hipEventDisableTiming) != hipSuccess) return fail("event");
     if (hipEventCreateWithFlags(&p->e1, hipEventDisableTiming) != hipSuccess) return fail("event");
+    if (p->pairs && p->aux_on) {
+      if (hipStreamCreateWithFlags(&p->aux, hipStreamNonBlocking) != hipSuccess) return fail("aux stream");
+      if (hipEventCreateWithFlags(&p->ea, hipEventDisableTiming) != hipSuccess) return fail("event");
+      if (hipEventCreateWithFlags(&p->eb, hipEventDisableTiming) != hipSuccess) return fail("event");
+    }
   }
   if (!fp64 && hipMalloc((void**)&p->A21f, sizeof(float) * (size_t)np * gelim::NB) != hipSuccess) return fail("A21f");
   if (!fp64 && hipMalloc((void**)&p->Wf, sizeof(float) * (size_t)np * gelim::NB) != hipSuccess) return fail("Wf");
@@ -862,7 +960,10 @@ extern "C" int gelim_mixed_factor(gelim_mixed_plan* p, const double* aug, int64_
   hipLaunchKernelGGL(rbt_matrix_kernel<double>, grid, dim3(256), 0, s, aug, ld, (int)p->n, (int)np, p->ud, p->vd,
                      p->M, ldm);
   HIP_TRY(hipGetLastError());
-  if (p->lookahead && p->pairs)
+  if (p->lookahead && p->pairs && p->aux)
+    GELIM_TRY(factor_la3(p->M, ldm, np, p->Dinv, p->W, p->info, s, p->side, p->aux, p->e0, p->e1, p->ea, p->eb,
+                         p->cap));
+  else if (p->lookahead && p->pairs)
     GELIM_TRY(factor_la2(p->M, ldm, np, p->Dinv, p->W, p->info, s, p->side, p->e0, p->e1, p->cap));
   else if (p->lookahead)
     GELIM_TRY(factor_la(p->M, ldm, np, p->Dinv, p->W, p->info, s, p->side, p->e0, p->e1, p->cap));

@@ -178,16 +178,33 @@ def test_rbt_singular_raises(gelim, cuda):
     assert s.last_fallback is not None
 
 
-@pytest.mark.parametrize("env", [{}, {"GELIM_RBT_LOOKAHEAD": "0"}, {"GELIM_RBT_PAIRS": "0"}])
+@pytest.mark.parametrize(
+    "env", [{}, {"GELIM_RBT_AUX": "1"}, {"GELIM_RBT_LOOKAHEAD": "0"}, {"GELIM_RBT_PAIRS": "0"}])
 def test_rbt_schedules_agree(gelim, cuda, env, monkeypatch):
-    """The three factorisation schedules -- lookahead over pairs (the default
-    from n = 4096), one-block lookahead, no lookahead; all read when the plan
-    is created -- give fp64-class answers on 4200 = 33 blocks (an odd count:
-    the pair loop ends on a single block)."""
+    """The four factorisation schedules -- lookahead over pairs (the default
+    from n = 4096), the same with the updates the next inverse does not read
+    on a third stream, one-block lookahead, no lookahead; all read when the
+    plan is created -- give fp64-class answers on 4200 = 33 blocks (an odd
+    count: the pair loop ends on a single block)."""
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     n = 4200
     aug = gelim.random_system(n, seed=77, device=cuda)
+    s = gelim.GaussSolver(n, backend="hip-rbt", device=cuda)
+    x = s.solve(aug, check=True)
+    assert s.last_fallback is None, s.last_fallback
+    ref = torch.linalg.solve(aug[:, :n], aug[:, n])
+    assert ((x - ref).abs().max() / ref.abs().max()).item() < 1e-9
+    s.close()
+
+
+@pytest.mark.parametrize("n", [256, 384, 2048])
+def test_rbt_three_stream_small(gelim, cuda, n, monkeypatch):
+    """The three-stream schedule forced on small orders (2, 3 and 16 blocks:
+    no side update, a panel of one block, the general case)."""
+    monkeypatch.setenv("GELIM_RBT_LOOKAHEAD", "1")
+    monkeypatch.setenv("GELIM_RBT_AUX", "1")
+    aug = gelim.random_system(n, seed=n + 3, device=cuda)
     s = gelim.GaussSolver(n, backend="hip-rbt", device=cuda)
     x = s.solve(aug, check=True)
     assert s.last_fallback is None, s.last_fallback

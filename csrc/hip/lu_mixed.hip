@@ -322,15 +322,18 @@ __global__ __launch_bounds__(16 * NB / TR) void diag_inv_kernel(const T* __restr
 }
 
 // Launch of the diagonal inverse: GELIM_GJ_TR = 4 (default: 512 threads, two
-// waves per SIMD) or 8 (256 threads).  With the padded LDS chunks 4 x 8 tiles
+// waves per SIMD), 8 (256 threads) or 2 (1024 threads: 2048 1.52 ms, slower).  With the padded LDS chunks 4 x 8 tiles
 // are the faster shape (hip-rbt factor 2048 1.43 vs 1.52 ms, 4096 3.85 vs
 // 4.00, 8192 12.94 vs 13.07; before the padding 8 x 8 was, 1.64 vs 1.73).
 // Reserving the inverse's CU (LDS-exclusive launch, no GEMM workgroup beside
 // it) changed nothing measurable (profiles/rbt_engine_round3.txt).
 int diag_inv(double* M, int64_t ldm, int64_t k0, double* Di, int* info, hipStream_t s) {
   const char* e = std::getenv("GELIM_GJ_TR");  // read per launch (tests switch it)
-  const int tr = e && std::atoi(e) == 8 ? 8 : 4;
-  if (tr == 4)
+  const int tr = e && (std::atoi(e) == 8 || std::atoi(e) == 2) ? std::atoi(e) : 4;
+  if (tr == 2)
+    hipLaunchKernelGGL((diag_inv_kernel<double, 2>), dim3(1), dim3(16 * NB / 2), 0, s, M, ldm, (int)k0, Di,
+                       (double*)nullptr, info);
+  else if (tr == 4)
     hipLaunchKernelGGL((diag_inv_kernel<double, 4>), dim3(1), dim3(16 * NB / 4), 0, s, M, ldm, (int)k0, Di,
                        (double*)nullptr, info);
   else

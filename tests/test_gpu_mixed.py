@@ -88,12 +88,12 @@ def test_mixed_singular_raises(gelim, cuda):
     assert s.last_fallback is not None
 
 
-@pytest.mark.parametrize("tr", ["4", "8"])
+@pytest.mark.parametrize("tr", ["2", "4", "8"])
 @pytest.mark.parametrize("backend", ["hip-mixed", "hip-rbt"])
 @pytest.mark.parametrize("n", [130, 1000])
 def test_diag_inverses_and_factor(gelim, cuda, backend, n, tr, monkeypatch):
-    """Every stored diagonal-block inverse (Gauss-Jordan, fp64; 4 x 8 tiles on
-    512 threads or 8 x 8 on 256, GELIM_GJ_TR) inverts the Schur diagonal
+    """Every stored diagonal-block inverse (Gauss-Jordan, fp64; 2 x 8, 4 x 8
+    or 8 x 8 tiles on 1024 / 512 / 256 threads, GELIM_GJ_TR) inverts the Schur diagonal
     block the block-LDU factor left in place; fp64 oracle."""
     import ctypes
 

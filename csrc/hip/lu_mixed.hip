@@ -535,6 +535,19 @@ __global__ __launch_bounds__(256) void fill_sentinel_kernel(unsigned long long* 
   if (i < n) p[i] = kSentinel;
 }
 
+// One launch before both triangular solves: the error words zeroed and both
+// hand-off buffers (forward z, backward x; x must not alias the forward's
+// input) sentinel-filled.
+__global__ __launch_bounds__(256) void prep_solves_kernel(unsigned* __restrict__ flags, unsigned long long* __restrict__ z,
+                                                          unsigned long long* __restrict__ x, int n) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i < 4) flags[i] = 0u;
+  if (i < n) {
+    z[i] = kSentinel;
+    x[i] = kSentinel;
+  }
+}
+
 // omega = max_i |r_i| / w_i (componentwise backward error; w_i = 0 counts as
 // 0), one workgroup, written to *out.
 __global__ __launch_bounds__(1024) void berr_kernel(const double* __restrict__ r, const double* __restrict__ w, int n,
@@ -801,10 +814,16 @@ int solve_impl(const T* M, int64_t ldm, int64_t np, const double* Dinv, const do
   if (!fits || nblk > kMaxBlocks || !coresident(1, 8 * kXcdSlots))
     return GELIM_FAIL(GELIM_E_ARG, "mixed solve: the block rows of this order cannot all be resident");
   int* err = reinterpret_cast<int*>(flags);  // flags[0]: error word
-  GELIM_TRY(zero_async(flags, 16, s));
   const unsigned g = (unsigned)((np + 255) / 256);
-  hipLaunchKernelGGL(fill_sentinel_kernel, dim3(g), dim3(256), 0, s, reinterpret_cast<unsigned long long*>(z),
-                     (int)np);
+  const bool alias = x == c;  // x is then sentinel-filled only after the forward solve has read c
+  if (alias) {
+    GELIM_TRY(zero_async(flags, 16, s));
+    hipLaunchKernelGGL(fill_sentinel_kernel, dim3(g), dim3(256), 0, s, reinterpret_cast<unsigned long long*>(z),
+                       (int)np);
+  } else {
+    hipLaunchKernelGGL(prep_solves_kernel, dim3(g), dim3(256), 0, s, flags, reinterpret_cast<unsigned long long*>(z),
+                       reinterpret_cast<unsigned long long*>(x), (int)np);
+  }
   HIP_TRY(hipGetLastError());
   static const int pack = [] {
     const char* e = std::getenv("GELIM_TRSV_PACK");
@@ -814,9 +833,11 @@ int solve_impl(const T* M, int64_t ldm, int64_t np, const double* Dinv, const do
   hipLaunchKernelGGL((blk_trsv_kernel<T, false>), dim3(grid), dim3(kDT), 0, s, M, ldm, Dinv, c, z, y, nblk, err,
                      g_trsv_stamps, pack);
   HIP_TRY(hipGetLastError());
-  hipLaunchKernelGGL(fill_sentinel_kernel, dim3(g), dim3(256), 0, s, reinterpret_cast<unsigned long long*>(x),
-                     (int)np);
-  HIP_TRY(hipGetLastError());
+  if (alias) {
+    hipLaunchKernelGGL(fill_sentinel_kernel, dim3(g), dim3(256), 0, s, reinterpret_cast<unsigned long long*>(x),
+                       (int)np);
+    HIP_TRY(hipGetLastError());
+  }
   hipLaunchKernelGGL((blk_trsv_kernel<T, true>), dim3(grid), dim3(kDT), 0, s, M, ldm, Dinv, y, x, (double*)nullptr,
                      nblk, err, (unsigned long long*)nullptr, pack);
   HIP_TRY(hipGetLastError());
@@ -840,6 +861,7 @@ struct gelim_mixed_plan {
   double* c = nullptr;      // U^T r (np)
   double* y = nullptr;      // L^-1 c (np)
   double* z = nullptr;      // U^-1 y (np)
+  double* xs = nullptr;     // the backward solve's hand-off buffer (np): filled with z before the forward solve
   int* info = nullptr;
   int err_host = 0;
   double* rv = nullptr;     // refinement (gelim_mixed_solve): r, |b| + |A||x|, correction, best x (n each)
@@ -863,7 +885,7 @@ extern "C" void gelim_mixed_plan_destroy(gelim_mixed_plan* p) {
   if (!p) return;
   for (void* q : {(void*)p->M, (void*)p->Dinv, (void*)p->W, (void*)p->A21f, (void*)p->Wf, (void*)p->ud, (void*)p->vd,
                   (void*)p->rv, (void*)p->wv, (void*)p->dv, (void*)p->xb, (void*)p->om, (void*)p->flags, (void*)p->c,
-                  (void*)p->y, (void*)p->z, (void*)p->info})
+                  (void*)p->y, (void*)p->z, (void*)p->xs, (void*)p->info})
     (void)hipFree(q);
   if (p->ea) (void)hipEventDestroy(p->ea);
   if (p->eb) (void)hipEventDestroy(p->eb);
@@ -939,6 +961,7 @@ extern "C" gelim_mixed_plan* gelim_mixed_plan_create2(int64_t n, const double* u
   if (hipMalloc((void**)&p->c, sizeof(double) * np) != hipSuccess) return fail("c");
   if (hipMalloc((void**)&p->y, sizeof(double) * np) != hipSuccess) return fail("y");
   if (hipMalloc((void**)&p->z, sizeof(double) * np) != hipSuccess) return fail("z");
+  if (hipMalloc((void**)&p->xs, sizeof(double) * np) != hipSuccess) return fail("xs");
   if (hipMalloc((void**)&p->info, 16) != hipSuccess) return fail("info");
   for (double** b : {&p->rv, &p->wv, &p->dv, &p->xb})
     if (hipMalloc((void**)b, sizeof(double) * (size_t)n) != hipSuccess) return fail("refinement vectors");
@@ -992,10 +1015,10 @@ extern "C" int gelim_mixed_apply(gelim_mixed_plan* p, const double* r, int64_t i
   const unsigned g = (unsigned)((h + 255) / 256);
   hipLaunchKernelGGL(rbt_vec_kernel, dim3(g), dim3(256), 0, s, r, incr, (int)p->n, (int)np, p->ud, 1, p->c, (int)np);
   HIP_TRY(hipGetLastError());
-  // c -> z (scratch), y (block-unit-lower result) -> c (the solution of the transformed system)
-  GELIM_TRY(solve_impl<double>(p->M, p->ldm, np, p->Dinv, p->c, p->z, p->y, p->c, p->flags, s));
-  // x = V z, only the first n entries are kept (the padding's are zero in exact arithmetic)
-  hipLaunchKernelGGL(rbt_vec_kernel, dim3(g), dim3(256), 0, s, p->c, (int64_t)1, (int)np, (int)np, p->vd, 0, d,
+  // c -> z (scratch), y (block-unit-lower result) -> xs (the solution of the transformed system)
+  GELIM_TRY(solve_impl<double>(p->M, p->ldm, np, p->Dinv, p->c, p->z, p->y, p->xs, p->flags, s));
+  // x = V xs, only the first n entries are kept (the padding's are zero in exact arithmetic)
+  hipLaunchKernelGGL(rbt_vec_kernel, dim3(g), dim3(256), 0, s, p->xs, (int64_t)1, (int)np, (int)np, p->vd, 0, d,
                      (int)p->n);
   HIP_TRY(hipGetLastError());
   return GELIM_OK;

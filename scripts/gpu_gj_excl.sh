@@ -1,6 +1,8 @@
 #!/usr/bin/env bash
 # Gauss-Jordan inverse alone on its CU (GELIM_GJ_EXCL KiB of reserved LDS) x tile shape
-# (GELIM_GJ_TR), under the default schedules and with lookahead forced at 2048
+# (GELIM_GJ_TR), under the default schedules and with lookahead forced at 2048.
+# Record of the round-3 run in profiles/rbt_engine_round3.txt: the LDS reservation changed
+# nothing measurable and GELIM_GJ_EXCL was removed afterwards (it is ignored now).
 set -u
 cd "${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 OUT=gpurun_out/gjexcl

@@ -298,10 +298,10 @@ int dgemm_capped(double* C, int64_t ldc, const double* A, int64_t lda, const dou
     return GELIM_FAIL(GELIM_E_ARG, "dgemm: unsupported alignment / leading dimensions (K=" + std::to_string(K) +
                                        " lda=" + std::to_string(lda) + " ldb=" + std::to_string(ldb) + ")");
   const int tm = (int)((M + BM - 1) / BM), tn = (int)((N + BN - 1) / BN);
-  static const int group = [] {
-    const char* e = std::getenv("GELIM_DGEMM_GROUP");
-    return e ? std::atoi(e) : 1;  // grouped orders 4 / 8 / 16 measured within noise of row-major
-  }();
+  // read per launch (tests switch it); grouped orders 4 / 8 / 16 measured
+  // within noise of row-major
+  const char* eg = std::getenv("GELIM_DGEMM_GROUP");
+  const int group = eg ? std::atoi(eg) : 1;
   Args g{C, ldc, A, lda, B, ldb, (int)M, (int)N, (int)K, tn, tm * tn, alpha, accumulate ? 1 : 0, group};
   // max_wg > 0: at most max_wg CUs (rounded down to a multiple of 8)
   const int cap = max_wg > 0 ? std::max(8, max_wg / 8 * 8) : 0;

@@ -287,8 +287,9 @@ __global__ __launch_bounds__(kPThreads, 1) void dgemm_persist_kernel(Args g) {
 
 // C (M x N, ldc) += alpha * A (M x K, lda) * B (K x N, ldb); alpha in {+1, -1}
 // in practice (any value works: A is scaled once on its way into LDS).
-int dgemm_capped(double* C, int64_t ldc, const double* A, int64_t lda, const double* B, int64_t ldb, int64_t M,
-                 int64_t N, int64_t K, double alpha, int max_wg, hipStream_t s, int accumulate = 1) {
+// group < 0: the GELIM_DGEMM_GROUP tile order (read once), else that order.
+int dgemm_launch(double* C, int64_t ldc, const double* A, int64_t lda, const double* B, int64_t ldb, int64_t M,
+                 int64_t N, int64_t K, double alpha, int max_wg, hipStream_t s, int accumulate, int group_arg) {
   if (M <= 0 || N <= 0 || K <= 0) return GELIM_OK;
   if (M > INT32_MAX || N > INT32_MAX || K > INT32_MAX) return GELIM_FAIL(GELIM_E_ARG, "dgemm: dimension > 2^31");
   // 16-byte operand chunks: 16-byte aligned A and B, even leading dimensions
@@ -298,10 +299,11 @@ int dgemm_capped(double* C, int64_t ldc, const double* A, int64_t lda, const dou
     return GELIM_FAIL(GELIM_E_ARG, "dgemm: unsupported alignment / leading dimensions (K=" + std::to_string(K) +
                                        " lda=" + std::to_string(lda) + " ldb=" + std::to_string(ldb) + ")");
   const int tm = (int)((M + BM - 1) / BM), tn = (int)((N + BN - 1) / BN);
-  // read per launch (tests switch it); grouped orders 4 / 8 / 16 measured
-  // within noise of row-major
-  const char* eg = std::getenv("GELIM_DGEMM_GROUP");
-  const int group = eg ? std::atoi(eg) : 1;
+  static const int group_env = [] {
+    const char* e = std::getenv("GELIM_DGEMM_GROUP");
+    return e ? std::atoi(e) : 1;  // grouped orders 4 / 8 / 16 measured within noise of row-major
+  }();
+  const int group = group_arg >= 0 ? group_arg : group_env;
   Args g{C, ldc, A, lda, B, ldb, (int)M, (int)N, (int)K, tn, tm * tn, alpha, accumulate ? 1 : 0, group};
   // max_wg > 0: at most max_wg CUs (rounded down to a multiple of 8)
   const int cap = max_wg > 0 ? std::max(8, max_wg / 8 * 8) : 0;
@@ -344,6 +346,11 @@ int dgemm_capped(double* C, int64_t ldc, const double* A, int64_t lda, const dou
   return GELIM_OK;
 }
 
+int dgemm_capped(double* C, int64_t ldc, const double* A, int64_t lda, const double* B, int64_t ldb, int64_t M,
+                 int64_t N, int64_t K, double alpha, int max_wg, hipStream_t s, int accumulate = 1) {
+  return dgemm_launch(C, ldc, A, lda, B, ldb, M, N, K, alpha, max_wg, s, accumulate, -1);
+}
+
 int dgemm(double* C, int64_t ldc, const double* A, int64_t lda, const double* B, int64_t ldb, int64_t M,
           int64_t N, int64_t K, double alpha, hipStream_t s) {
   return dgemm_capped(C, ldc, A, lda, B, ldb, M, N, K, alpha, 0, s);
@@ -360,6 +367,14 @@ int dgemm_ex(double* C, int64_t ldc, const double* A, int64_t lda, const double*
 extern "C" int gelim_gpu_dgemm(double* dC, int64_t ldc, const double* dA, int64_t lda, const double* dB,
                                int64_t ldb, int64_t M, int64_t N, int64_t K, double alpha, void* stream) {
   return gelim::dgemm(dC, ldc, dA, lda, dB, ldb, M, N, K, alpha, (hipStream_t)stream);
+}
+
+// an explicit tile order (runs of `group` tile rows; tests of the grouped order)
+extern "C" int gelim_gpu_dgemm_grouped(double* dC, int64_t ldc, const double* dA, int64_t lda, const double* dB,
+                                       int64_t ldb, int64_t M, int64_t N, int64_t K, double alpha, int max_wg,
+                                       int group, void* stream) {
+  return gelim::dgemm_launch(dC, ldc, dA, lda, dB, ldb, M, N, K, alpha, max_wg, (hipStream_t)stream, 1,
+                             group < 0 ? 0 : group);
 }
 
 // the persistent form on at most max_wg CUs (tests / benchmarks)

@@ -69,6 +69,7 @@ _PROTOS = {
     "gelim_gpu_gemm_update": (_int, [_vp, _i64, _vp, _i64, _vp, _i64, _i64, _i64, _i64, _vp]),
     "gelim_gpu_dgemm": (_int, [_vp, _i64, _vp, _i64, _vp, _i64, _i64, _i64, _i64, _dbl, _vp]),
     "gelim_gpu_dgemm_capped": (_int, [_vp, _i64, _vp, _i64, _vp, _i64, _i64, _i64, _i64, _dbl, _int, _vp]),
+    "gelim_gpu_dgemm_grouped": (_int, [_vp, _i64, _vp, _i64, _vp, _i64, _i64, _i64, _i64, _dbl, _int, _int, _vp]),
     "gelim_gpu_leaf_factor": (_int, [_vp, _i64, _i64, _i64, _int, _vp, _vp, _vp, _vp]),
     "gelim_gpu_leaf_factor_ws": (_int, [_vp, _i64, _i64, _i64, _int, _vp, _vp, _vp, _vp, _int, _vp]),
     "gelim_gpu_leaf_workspace_bytes": (_i64, []),

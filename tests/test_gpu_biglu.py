@@ -43,14 +43,16 @@ def test_dgemm_matches_torch(gelim, cuda, M, N, K, alpha, cap):
     assert torch.equal(Cf[:, N:], C0[:, N:])  # padding untouched
 
 
-@pytest.mark.parametrize("group", ["4", "8"])
+@pytest.mark.parametrize("group", [4, 8])
 @pytest.mark.parametrize("M,N,K", [(1300, 1000, 32), (2100, 3000, 64), (200, 700, 16)])
-@pytest.mark.parametrize("cap", [None, 224])
-def test_dgemm_grouped_tile_order(gelim, cuda, M, N, K, group, cap, monkeypatch):
-    """GELIM_DGEMM_GROUP: the grouped tile order (runs of g tile rows, the
+@pytest.mark.parametrize("cap", [0, 224])
+def test_dgemm_grouped_tile_order(gelim, cuda, M, N, K, group, cap):
+    """The grouped tile order (GELIM_DGEMM_GROUP; runs of g tile rows, the
     last run short: 11 / 17 / 2 tile rows of 128, or of 64 for the thin-tile
-    path) still covers every tile exactly once."""
-    monkeypatch.setenv("GELIM_DGEMM_GROUP", group)
+    path) still covers every tile exactly once, plain and persistent."""
+    from gelim import _native
+    from gelim.utils.tensors import stream_handle
+
     torch.manual_seed(M + N + K)
     ldn = N + 2
     Cf = torch.randn(M, ldn, dtype=torch.float64, device=cuda)
@@ -58,7 +60,9 @@ def test_dgemm_grouped_tile_order(gelim, cuda, M, N, K, group, cap, monkeypatch)
     Bf = torch.randn(K, ldn, dtype=torch.float64, device=cuda)
     C, B = Cf[:, :N], Bf[:, :N]
     ref = C - A @ B
-    _dgemm(gelim, C, A, B, -1.0, cap)
+    rc = _native.lib().gelim_gpu_dgemm_grouped(C.data_ptr(), C.stride(0), A.data_ptr(), A.stride(0), B.data_ptr(),
+                                               B.stride(0), M, N, K, -1.0, cap, group, stream_handle(C.device))
+    _native.check(rc, "dgemm")
     torch.cuda.synchronize()
     assert torch.allclose(C, ref, rtol=1e-12, atol=1e-11 * K)
 

@@ -261,6 +261,12 @@ def main() -> None:
     if not args.headline_only and on_gpu:
         # strong scaling over ALL ranks: the BASELINE.json multi-GPU configs
         _section(result, "dist_gauss_8192", lambda: bench_dist_gauss(comm, gelim, torch, 8192))
+        # the headline's 2048 system over ALL ranks (strong scaling, SURVEY §7.4-5: latency-bound,
+        # reported as measured): every block a broadcast panel, and the default form (the whole
+        # 2048 system is the tail: one all_gather + the single-GPU engine on every rank)
+        _section(result, "dist_gauss_2048", lambda: {
+            "panels": bench_dist_gauss(comm, gelim, torch, 2048, tail=0),
+            "tail_engine": bench_dist_gauss(comm, gelim, torch, 2048)})
         _section(result, "dist_matmul_16384", lambda: bench_dist_matmul(comm, gelim, torch, 16384))
         # single-GPU large systems (each rank its own: weak)
         _section(result, "gauss_8192_1gpu", lambda: bench_single(comm, gelim, torch, 8192, seed=77 + rank))
@@ -280,19 +286,30 @@ def main() -> None:
             v = rb.get(nn, {}).get("hip-rbt")
             if isinstance(v, dict) and "time_s" in v:
                 result[f"gauss_{nn}_rbt_s"] = v["time_s"]
+    d2 = result.get("dist_gauss_2048")
+    if isinstance(d2, dict) and "panels" in d2:
+        result["dist_gauss_2048_s"] = d2["panels"]["time_s"]
+        result["dist_gauss_2048_tail_engine_s"] = d2["tail_engine"]["time_s"]
     dm = result.get("dist_matmul_16384")
     if isinstance(dm, dict) and "summa" in dm:
         result["dist_matmul_16384_summa_s"] = dm["summa"]["time_s"]
 
     # -- speedup vs the reference's sequential loops --------------------------
+    # The sequential Gauss loop (~0.6 s at 2048) is timed in EVERY run on this
+    # host; the i-j-k matmul (~40 s) only with --measure-seq, else stored.
     seq = None
-    if args.measure_seq and rank == 0:
-        seq = measure_host_seq(n)
-        seq["source"] = "measured in this run on this host"
-    elif HOST_SEQ_FILE.exists():
-        seq = json.loads(HOST_SEQ_FILE.read_text())
-        seq["source"] = (f"STORED: {HOST_SEQ_FILE.relative_to(ROOT)} (measured {seq.get('measured_at', '?')} on "
-                         f"{seq.get('host', '?')}), not re-measured in this run; --measure-seq re-measures")
+    if rank == 0:
+        if args.measure_seq:
+            seq = measure_host_seq(n)
+            seq["source"] = "measured in this run on this host (Gauss and matmul)"
+        else:
+            stored = json.loads(HOST_SEQ_FILE.read_text()) if HOST_SEQ_FILE.exists() else {}
+            seq = measure_host_seq(n, matmul=False)
+            if "matmul_2048_s" in stored:
+                seq["matmul_2048_s"] = stored["matmul_2048_s"]
+            seq["source"] = (f"gauss_{n}_s measured in this run on this host; matmul_2048_s STORED: "
+                             f"{HOST_SEQ_FILE.relative_to(ROOT)} (measured {stored.get('measured_at', '?')} on "
+                             f"{stored.get('host', '?')}); --measure-seq re-measures it (~40 s)")
     if seq and rank == 0:
         result["host_seq"] = seq
         if "gauss_2048_s" in seq and n == 2048:
@@ -334,14 +351,15 @@ def bench_matmul(gelim, torch, dev) -> dict:
             "vs_reference_cuda_v2_cold": BASELINE_MATMUL_S / cold, "max_rel_err": max(rel, prel)}
 
 
-def bench_dist_gauss(comm, gelim, torch, n: int) -> dict:
-    """The 8192^2 system distributed over ALL ranks (strong scaling; column
+def bench_dist_gauss(comm, gelim, torch, n: int, tail: int | None = None) -> dict:
+    """The n^2 system distributed over ALL ranks (strong scaling; column
     block-cyclic, wide-panel leaves, RCCL broadcast with lookahead); second
-    solve timed."""
+    solve timed.  tail=0: every block is a broadcast panel (no trailing
+    system handed to the single-GPU engine)."""
     from gelim.parallel import DistributedGauss
 
     dev = comm.device
-    dg = DistributedGauss(comm, n)
+    dg = DistributedGauss(comm, n, tail=tail)
     holder = {}
 
     def run():
@@ -353,7 +371,8 @@ def bench_dist_gauss(comm, gelim, torch, n: int) -> dict:
     x = holder["x"]
     return {"time_s": dt, "error": gelim.ops.gauss.error_metric(x), "ranks": comm.world_size,
             "tflops_total": (2.0 / 3.0) * n ** 3 / dt * 1e-12, "block": dg.layout.D,
-            "lookahead": dg.lookahead, "layout": "1-D column block-cyclic"}
+            "lookahead": dg.lookahead, "layout": "1-D column block-cyclic",
+            "broadcast_panels": dg._panel_blocks(use_tail=True), "tail_rows": dg.tail_rows}
 
 
 def bench_dist_matmul(comm, gelim, torch, n: int) -> dict:
@@ -482,11 +501,11 @@ def bench_external(comm, gelim, torch) -> dict:
     return out
 
 
-def measure_host_seq(n: int) -> dict:
+def measure_host_seq(n: int, matmul: bool = True) -> dict:
     """The reference's sequential loops on this host (the speedup denominator,
-    SURVEY.md §6 caveat): Gauss internal-style elimination and i-j-k matmul."""
-    import torch
-
+    SURVEY.md §6 caveat): the external programs' partial-pivoting elimination
+    (OpenMP_and_MPI/gauss_openmp/gauss_external_input.c:153-182 run on one
+    thread) and the i-j-k matmul (CUDA_and_OpenMP/Version-2/cuda_matmul.cu:28-39)."""
     import gelim
 
     aug = gelim.random_system(n, seed=1234)
@@ -495,13 +514,13 @@ def measure_host_seq(n: int) -> dict:
     t0 = time.perf_counter()
     gelim.ops.gauss.cpu_gauss_(A, b, "seq", "partial")
     gauss_s = time.perf_counter() - t0
-    Am, Bm = gelim.ops.matmul.reference_inputs(2048)
-    t0 = time.perf_counter()
-    gelim.ops.cpu_matmul(Am, Bm)
-    mm_s = time.perf_counter() - t0
-    res = {"gauss_2048_s": gauss_s, "matmul_2048_s": mm_s, "host": os.uname().nodename,
-           "cpus": os.cpu_count(), "measured_at": time.strftime("%Y-%m-%dT%H:%M:%S")}
-    del torch
+    res = {f"gauss_{n}_s": gauss_s, "host": os.uname().nodename, "cpus": os.cpu_count(),
+           "measured_at": time.strftime("%Y-%m-%dT%H:%M:%S")}
+    if matmul:
+        Am, Bm = gelim.ops.matmul.reference_inputs(2048)
+        t0 = time.perf_counter()
+        gelim.ops.cpu_matmul(Am, Bm)
+        res["matmul_2048_s"] = time.perf_counter() - t0
     return res
 
 

@@ -190,64 +190,6 @@ __global__ __launch_bounds__(256) void backsub_persist_kernel(const T* __restric
   __syncthreads();
 }
 
-// ---- forward substitution L x = y, L unit lower (the mixed engine) ----------
-// The same persistent scheme run top-down: block b waits for the solved
-// blocks c < b (wave 0 takes block b-1 itself, waves 1..3 the earlier ones
-// round-robin), then wave 0 solves its unit-lower triangle.  y is fp64, x is
-// written in the factor's type T (the input of the upper solve that follows).
-__device__ __forceinline__ double solve_diag_lower(const double (&row)[kBS], double yv, int nb) {
-  const int l = threadIdx.x & 63;
-  double xv = 0.0;
-#pragma unroll
-  for (int i = 0; i < kBS; ++i) {
-    if (i < nb) {
-      const uint64_t b = __builtin_bit_cast(uint64_t, yv);  // x_i = y_i in lane i (unit diagonal)
-      const double xi = __builtin_bit_cast(
-          double, ((uint64_t)(unsigned)__builtin_amdgcn_readlane((int)(b >> 32), i) << 32) |
-                      (unsigned)__builtin_amdgcn_readlane((int)b, i));
-      if (l == i) xv = xi;
-      yv = (l > i) ? fma(-row[i], xi, yv) : yv;
-    }
-  }
-  return xv;
-}
-
-template <typename T>
-__global__ __launch_bounds__(256) void fwdsub_persist_kernel(const T* __restrict__ L, int64_t ldl,
-                                                             const double* __restrict__ y, double* __restrict__ xs,
-                                                             T* __restrict__ out, int n, unsigned* flags, int* err) {
-  __shared__ double part[4][kBS];
-  const int b = blockIdx.x;
-  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
-  const int r0 = b * kBS, rows = min(kBS, n - r0);
-  const int i = r0 + min(lane, rows - 1);
-  double acc = 0.0;
-  bool ok = true;
-  if (wv == 0) {
-    double drow[kBS];
-    double rinv = 1.0;
-    load_diag<T>(L, ldl, nullptr, n, r0, rows, 1, drow, rinv);
-    const double v = y[i];
-    if (b > 0) ok = apply_block<T>(L, ldl, i, b - 1, n, xs, flags, err, false, acc);
-    __syncthreads();
-    if (!ok) return;
-    const double yv = v + acc + part[1][lane] + part[2][lane] + part[3][lane];
-    const double xv = solve_diag_lower(drow, yv, rows);
-    if (lane < rows) {
-      __hip_atomic_store(reinterpret_cast<unsigned long long*>(xs + r0 + lane), __builtin_bit_cast(unsigned long long, xv),
-                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      out[r0 + lane] = (T)xv;
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (lane == 0) __hip_atomic_store(&flags[b], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return;
-  }
-  // background waves: blocks 0 .. b-2, wave 1 + c % 3
-  for (int c = wv - 1; c <= b - 2 && ok; c += 3) ok = apply_block<T>(L, ldl, i, c, n, xs, flags, err, true, acc);
-  part[wv][lane] = acc;
-  __syncthreads();
-}
-
 // ---- fallback: one launch per block ----------------------------------------
 
 template <typename T>
@@ -367,25 +309,6 @@ int backsub_f32(const float* U, int64_t ldu, const float* y, int64_t incy, doubl
                 double* bnorm, int64_t n, int unit, double* yw, hipStream_t s, const int* perm,
                 int* err) {
   return backsub_impl<float>(U, ldu, y, incy, x, bnorm, n, unit, yw, s, perm, err);
-}
-
-// L x = y with L the unit-lower part of the fp32 factor at L (ldl); y fp64,
-// x written as fp32 into out; xs: n doubles of scratch (the published x),
-// flags: (n / 64 + 2) words of scratch.  Persistent form only (every block
-// resident: n <= 16384); returns an error beyond that.
-int fwdsub_unit_f32(const float* L, int64_t ldl, const double* y, float* out, int64_t n, double* xs,
-                    unsigned* flags, hipStream_t s) {
-  const int64_t nblk = (n + kBS - 1) / kBS;
-  int per = 0;
-  if (nblk > kMaxPersistBlocks ||
-      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fwdsub_persist_kernel<float>, 256, 0) != hipSuccess ||
-      !coresident(per, nblk))
-    return GELIM_FAIL(GELIM_E_ARG, "fwdsub: the blocks of this order cannot all be resident");
-  GELIM_TRY(zero_async(flags, ((size_t)nblk + 2) * 4, s));
-  hipLaunchKernelGGL(fwdsub_persist_kernel<float>, dim3((unsigned)nblk), dim3(256), 0, s, L, ldl, y, xs, out, (int)n,
-                     flags, reinterpret_cast<int*>(flags + nblk));
-  HIP_TRY(hipGetLastError());
-  return GELIM_OK;
 }
 
 }  // namespace gelim

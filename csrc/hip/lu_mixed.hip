@@ -535,13 +535,11 @@ __global__ __launch_bounds__(256) void fill_sentinel_kernel(unsigned long long* 
   if (i < n) p[i] = kSentinel;
 }
 
-// One launch before both triangular solves: the error words zeroed and both
-// hand-off buffers (forward z, backward x; x must not alias the forward's
-// input) sentinel-filled.
-__global__ __launch_bounds__(256) void prep_solves_kernel(unsigned* __restrict__ flags, unsigned long long* __restrict__ z,
+// One launch before both triangular solves: both hand-off buffers (forward
+// z, backward x; x must not alias the forward's input) sentinel-filled.
+__global__ __launch_bounds__(256) void prep_solves_kernel(unsigned long long* __restrict__ z,
                                                           unsigned long long* __restrict__ x, int n) {
   const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i < 4) flags[i] = 0u;
   if (i < n) {
     z[i] = kSentinel;
     x[i] = kSentinel;
@@ -801,6 +799,13 @@ int factor_la3(double* M, int64_t ldm, int64_t np, double* Dinv, double* W4, int
 // it is sentinel-filled only after the forward solve has read c).
 unsigned long long* g_trsv_stamps = nullptr;  // diagnostics: 3 realtime stamps per workgroup (lower solve)
 
+// Returns GELIM_OK, kNotResident (a positive code: the caller falls back to
+// partial pivoting) when the persistent grid cannot be co-resident, or < 0.
+// The error word flags[0] is NOT cleared here: the caller zeroes it once per
+// outer solve (gelim_mixed_reset_error), so a hand-off timeout of any inner
+// apply stays visible until it is checked.
+constexpr int kNotResident = 1;
+
 template <typename T>
 int solve_impl(const T* M, int64_t ldm, int64_t np, const double* Dinv, const double* c, double* z, double* y,
                double* x, unsigned* flags, hipStream_t s) {
@@ -811,24 +816,28 @@ int solve_impl(const T* M, int64_t ldm, int64_t np, const double* Dinv, const do
            hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, blk_trsv_kernel<T, true>, kDT, 0) == hipSuccess &&
            a >= 1 && b >= 1;
   }();
-  if (!fits || nblk > kMaxBlocks || !coresident(1, 8 * kXcdSlots))
-    return GELIM_FAIL(GELIM_E_ARG, "mixed solve: the block rows of this order cannot all be resident");
+  static const int pack_env = [] {
+    const char* e = std::getenv("GELIM_TRSV_PACK");
+    return e ? std::atoi(e) : 1;
+  }();
+  // the XCD-packed chain maps positions across the whole 8 x 32 grid (position
+  // 32 is workgroup 1, waiting on position 31 = workgroup 248), so it needs
+  // every one of them resident; one workgroup per block row needs only nblk
+  // (workgroups are dispatched in order, each waits on lower ids only)
+  if (!fits || nblk > kMaxBlocks) return kNotResident;
+  const int pack = pack_env && coresident(1, 8 * kXcdSlots) ? 1 : 0;
+  if (!pack && !coresident(1, nblk)) return kNotResident;
   int* err = reinterpret_cast<int*>(flags);  // flags[0]: error word
   const unsigned g = (unsigned)((np + 255) / 256);
   const bool alias = x == c;  // x is then sentinel-filled only after the forward solve has read c
   if (alias) {
-    GELIM_TRY(zero_async(flags, 16, s));
     hipLaunchKernelGGL(fill_sentinel_kernel, dim3(g), dim3(256), 0, s, reinterpret_cast<unsigned long long*>(z),
                        (int)np);
   } else {
-    hipLaunchKernelGGL(prep_solves_kernel, dim3(g), dim3(256), 0, s, flags, reinterpret_cast<unsigned long long*>(z),
+    hipLaunchKernelGGL(prep_solves_kernel, dim3(g), dim3(256), 0, s, reinterpret_cast<unsigned long long*>(z),
                        reinterpret_cast<unsigned long long*>(x), (int)np);
   }
   HIP_TRY(hipGetLastError());
-  static const int pack = [] {
-    const char* e = std::getenv("GELIM_TRSV_PACK");
-    return e ? std::atoi(e) : 1;
-  }();
   const unsigned grid = pack ? 8u * kXcdSlots : (unsigned)nblk;
   hipLaunchKernelGGL((blk_trsv_kernel<T, false>), dim3(grid), dim3(kDT), 0, s, M, ldm, Dinv, c, z, y, nblk, err,
                      g_trsv_stamps, pack);
@@ -1016,7 +1025,8 @@ extern "C" int gelim_mixed_apply(gelim_mixed_plan* p, const double* r, int64_t i
   hipLaunchKernelGGL(rbt_vec_kernel, dim3(g), dim3(256), 0, s, r, incr, (int)p->n, (int)np, p->ud, 1, p->c, (int)np);
   HIP_TRY(hipGetLastError());
   // c -> z (scratch), y (block-unit-lower result) -> xs (the solution of the transformed system)
-  GELIM_TRY(solve_impl<double>(p->M, p->ldm, np, p->Dinv, p->c, p->z, p->y, p->xs, p->flags, s));
+  const int rc = solve_impl<double>(p->M, p->ldm, np, p->Dinv, p->c, p->z, p->y, p->xs, p->flags, s);
+  if (rc != GELIM_OK) return rc;  // < 0: error; kNotResident: the caller falls back
   // x = V xs, only the first n entries are kept (the padding's are zero in exact arithmetic)
   hipLaunchKernelGGL(rbt_vec_kernel, dim3(g), dim3(256), 0, s, p->xs, (int64_t)1, (int)np, (int)np, p->vd, 0, d,
                      (int)p->n);
@@ -1025,6 +1035,13 @@ extern "C" int gelim_mixed_apply(gelim_mixed_plan* p, const double* r, int64_t i
 }
 
 extern "C" int gelim_mixed_solve_error(gelim_mixed_plan* p, void* stream);
+
+// Zero the solves' hand-off error word (once per outer solve: every apply of
+// that solve then only ever sets it, so one check covers all of them).
+extern "C" int gelim_mixed_reset_error(gelim_mixed_plan* p, void* stream) {
+  if (!p) return GELIM_FAIL(GELIM_E_ARG, "mixed_reset_error: null plan");
+  return gelim::zero_async(p->flags, 16, (hipStream_t)stream);
+}
 
 // The whole randomised solve of an augmented fp64 system (n x >= n+1 at aug,
 // leading dimension ld) into x (n fp64, device): factorisation, x = (LU)^-1 b,
@@ -1048,7 +1065,12 @@ extern "C" int gelim_mixed_solve(gelim_mixed_plan* p, const double* aug, int64_t
   const int rc = gelim_mixed_factor(p, aug, ld, stream);
   if (rc < 0) return rc;
   if (rc > 0) return 1;
-  GELIM_TRY(gelim_mixed_apply(p, aug + n, ld, x, stream));
+  GELIM_TRY(gelim_mixed_reset_error(p, stream));
+  {
+    const int ra = gelim_mixed_apply(p, aug + n, ld, x, stream);
+    if (ra < 0) return ra;
+    if (ra > 0) return 1;  // the persistent solves cannot be resident: partial pivoting instead
+  }
   const double eps = 2.220446049250313e-16;
   const double strict = 4.0 * eps, loose = std::max(std::sqrt((double)n), 8.0) * eps;
   double prev = INFINITY, best = INFINITY;
@@ -1059,28 +1081,37 @@ extern "C" int gelim_mixed_solve(gelim_mixed_plan* p, const double* aug, int64_t
     HIP_TRY(hipGetLastError());
     double om = 0.0;
     HIP_TRY(hipMemcpyAsync(&om, p->om, 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(&p->err_host, p->flags, 4, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
+    // the error word covers every apply since the reset (the first one
+    // included): a timed-out hand-off leaves x incomplete -> fall back
+    if (p->err_host != 0) {
+      if (steps) *steps = it;
+      return 1;
+    }
     if (steps) *steps = it;
     if (berr) *berr = om;
     if (om <= strict) return 0;
     if (!(om < 0.9 * prev) || it == max_steps) {  // NaN, stagnated or out of steps
+      // the better of the current x and the saved best one, if acceptable
+      if (om <= best && om <= loose) return 0;
       if (best <= loose) {
         HIP_TRY(hipMemcpyAsync(x, p->xb, sizeof(double) * n, hipMemcpyDeviceToDevice, s));
         if (berr) *berr = best;
         return 0;
       }
-      return om <= loose ? 0 : 1;
+      return 1;
     }
     if (om < best) {
       best = om;
       HIP_TRY(hipMemcpyAsync(p->xb, x, sizeof(double) * n, hipMemcpyDeviceToDevice, s));
     }
     prev = om;
-    GELIM_TRY(gelim_mixed_apply(p, p->rv, 1, p->dv, stream));
+    const int ra = gelim_mixed_apply(p, p->rv, 1, p->dv, stream);
+    if (ra < 0) return ra;
+    if (ra > 0) return 1;
     hipLaunchKernelGGL(axpy_kernel, dim3(g), dim3(256), 0, s, x, p->dv, n);
     HIP_TRY(hipGetLastError());
-    if (gelim_mixed_solve_error(p, stream) != 0)
-      return GELIM_FAIL(GELIM_E_HIP, "mixed_solve: a triangular-solve hand-off timed out");
   }
 }
 

@@ -80,6 +80,7 @@ _PROTOS = {
     "gelim_mixed_plan_create": (_vp, [_i64, _vp, _vp]),
     "gelim_mixed_plan_create2": (_vp, [_i64, _vp, _vp, _int]),
     "gelim_mixed_solve_error": (_int, [_vp, _vp]),
+    "gelim_mixed_reset_error": (_int, [_vp, _vp]),
     "gelim_mixed_debug_ptrs": (_i64, [_vp, _vp]),
     "gelim_mixed_debug_copy": (_int, [_vp, _vp, _i64]),
     "gelim_mixed_plan_np": (_i64, [_vp]),

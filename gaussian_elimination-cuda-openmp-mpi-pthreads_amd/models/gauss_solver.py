@@ -12,8 +12,8 @@ Backends
                       fp32 on the matrix cores + fp64 GMRES-IR on the
                       original system, falling back to `hip` (fp64, partial
                       pivoting) whenever it does not reach the fp64 error
-                      class (csrc/hip/lu_mixed.hip); also selected by
-                      backend="hip", dtype=torch.float32
+                      class (csrc/hip/lu_mixed.hip); explicit opt-in only
+                      (slower than hip-rbt at every benched n)
   hip-rbt           : the same transform and NO-pivoting blocked LU with fp64
                       factors (fp64 MFMA GEMMs, no per-column global arg-max)
                       + classic fp64 iterative refinement, same fallback
@@ -60,7 +60,13 @@ class GaussSolver:
         self.last_fallback = None
         self.last_berr = None
         if backend in ("hip", "hip-blocked") and dtype == torch.float32:
-            backend = self.backend = MIXED_BACKEND
+            # round 3 mapped this to hip-mixed, which is slower than hip-rbt at
+            # every benched n (GMRES-IR pays a triangular-solve pair per
+            # iteration): fp32 factors are now an explicit opt-in
+            raise ValueError("the blocked LU is fp64 (partial-pivoting accuracy on the reference matrices); "
+                             "for fp32 factors choose backend='hip-mixed' (fp32 trailing products + fp64 "
+                             "GMRES-IR) or backend='hip-pivot' (the reference loop in fp32); the fastest "
+                             "fp64-class solver is backend='hip-rbt'")
         self.gpu = backend in GPU_BACKENDS or backend in RBT_BACKENDS
         if backend in RBT_BACKENDS:
             self._init_mixed(device, seed=0x5eed, fp64=RBT_BACKENDS[backend])
@@ -111,6 +117,14 @@ class GaussSolver:
             self._fp64 = GaussSolver(self.n, backend="hip", pivot=self.pivot, device=self.device)
         return self._fp64.solve(aug64, check=check)
 
+    class _NotResident(Exception):
+        """The persistent block solves cannot be co-resident on this device."""
+
+    def _apply(self, r: torch.Tensor, inc: int, out: torch.Tensor, sh) -> None:
+        rc = _native.check(_native.lib().gelim_mixed_apply(self._mixed, ptr(r), inc, ptr(out), sh), "mixed_apply")
+        if rc > 0:
+            raise GaussSolver._NotResident()
+
     def _gmres(self, aug64: torch.Tensor, r: torch.Tensor, restart: int = 30, tol: float = 1e-6) -> torch.Tensor:
         """d ~ A^-1 r by left-preconditioned GMRES in fp64 (Carson-Higham
         GMRES-IR): M^-1 = V (LU)^-1 U^T from the fp32 factors, A v on the
@@ -127,7 +141,7 @@ class GaussSolver:
         Vb = torch.empty((restart + 1, n), dtype=torch.float64, device=dev)
         w = torch.empty(n, dtype=torch.float64, device=dev)
         z = torch.empty(n, dtype=torch.float64, device=dev)
-        _native.check(lib.gelim_mixed_apply(self._mixed, ptr(r), 1, ptr(z), sh), "mixed_apply")
+        self._apply(r, 1, z, sh)
         beta = float(z.norm())
         if not beta > 0.0 or beta != beta:
             return torch.zeros(n, dtype=torch.float64, device=dev)
@@ -139,7 +153,7 @@ class GaussSolver:
         k = 0
         for j in range(restart):
             _native.check(lib.gelim_gpu_matvec(ptr(aug64), ld, n, ptr(Vb[j]), ptr(w), sh), "matvec")
-            _native.check(lib.gelim_mixed_apply(self._mixed, ptr(w), 1, ptr(z), sh), "mixed_apply")
+            self._apply(w, 1, z, sh)
             B = Vb[:j + 1]
             h = B @ z
             z -= B.T @ h
@@ -181,8 +195,6 @@ class GaussSolver:
         the ORIGINAL system.  A stall, a zero pivot or too many steps hand the
         system to the fp64 partial-pivoting engine (last_fallback says why;
         last_steps counts outer corrections, last_inner GMRES iterations)."""
-        import math
-
         n, dev = self.n, self.device
         lib = _native.lib()
         aug64 = aug.to(dev, torch.float64)
@@ -213,9 +225,26 @@ class GaussSolver:
         _native.check(rc, "mixed_factor")
         if rc > 0:
             return self._fallback(aug64, f"no-pivot LU: zero or non-finite pivot at column {rc - 1}", check)
+        try:
+            return self._refine_fp32(aug64, max_steps, check)
+        except GaussSolver._NotResident:
+            return self._fallback(aug64, "the persistent block solves cannot be co-resident", check)
+
+    def _refine_fp32(self, aug64: torch.Tensor, max_steps: int, check: bool) -> torch.Tensor:
+        """hip-mixed: x from the fp32-product factors, then GMRES-IR
+        corrections (see _solve_mixed)."""
+        import math
+
+        n, dev = self.n, self.device
+        lib = _native.lib()
+        ld = aug64.stride(0)
+        sh = stream_handle(dev)
+        # the hand-off error word is zeroed once per solve; every apply only
+        # sets it, so the check after each correction covers all of them
+        _native.check(lib.gelim_mixed_reset_error(self._mixed, sh), "mixed_reset_error")
         b = aug64[:, n]
         x = torch.empty(n, dtype=torch.float64, device=dev)
-        _native.check(lib.gelim_mixed_apply(self._mixed, ptr(b), ld, ptr(x), sh), "mixed_apply")
+        self._apply(b, ld, x, sh)
         # componentwise backward error w = max_i |r_i| / (|b| + |A||x|)_i (one
         # native pass gives r and the denominator): refine until w <= 4 eps64;
         # once a correction stops reducing it by 10 %, accept w <= sqrt(n) eps64.  A
@@ -234,25 +263,21 @@ class GaussSolver:
             self.last_berr = om
             if om <= strict:
                 return x
+            if lib.gelim_mixed_solve_error(self._mixed, sh) != 0:
+                return self._fallback(aug64, "a triangular-solve hand-off timed out", check)
             if not om < 0.9 * prev or it == max_steps:  # NaN, stagnated or out of steps
+                # the better of the current x and the saved best one, if acceptable
+                if om <= loose and (best is None or om <= best[0]):
+                    return x
                 if best is not None and best[0] <= loose:
                     self.last_berr = best[0]
                     return best[1]
-                if om <= loose:
-                    return x
                 return self._fallback(aug64, f"refinement stalled after {it} corrections "
                                              f"(componentwise backward error {om:.3e} > {loose:.3e})", check)
             if best is None or om < best[0]:
                 best = (om, x.clone())
             prev = om
-            if self.dtype == torch.float64:
-                d = torch.empty(n, dtype=torch.float64, device=dev)
-                _native.check(lib.gelim_mixed_apply(self._mixed, ptr(r), 1, ptr(d), sh), "mixed_apply")
-                x += d
-            else:
-                x += self._gmres(aug64, r)
-            if lib.gelim_mixed_solve_error(self._mixed, sh) != 0:
-                raise _native.GelimError(_native.E_HIP, "mixed engine: a triangular-solve hand-off timed out")
+            x += self._gmres(aug64, r)
         raise AssertionError("unreachable")
 
     # -- GPU ---------------------------------------------------------------

@@ -43,7 +43,7 @@ def dead_rank(rank, world, port, outdir):
     os._exit(0)
 
 
-def gauss(rank, world, port, outdir, n, block, seed, device, mode, lookahead=None):
+def gauss(rank, world, port, outdir, n, block, seed, device, mode, lookahead=None, tail=None):
     import torch
 
     import gelim
@@ -52,8 +52,11 @@ def gauss(rank, world, port, outdir, n, block, seed, device, mode, lookahead=Non
 
     try:
         comm = _init(rank, world, port, device)
-        dg = DistributedGauss(comm, n, block=block, lookahead=lookahead)
-        (Path(outdir) / f"meta{rank}.txt").write_text(f"{comm.backend} {comm.world_size} {dg.wide} {dg.lookahead}")
+        dg = DistributedGauss(comm, n, block=block, lookahead=lookahead, tail=tail)
+        # G: blocks eliminated as broadcast panels (the rest is the tail system)
+        G = dg._panel_blocks(use_tail=bool(dg.lookahead)) if dg.wide else dg.layout.nblocks
+        (Path(outdir) / f"meta{rank}.txt").write_text(
+            f"{comm.backend} {comm.world_size} {dg.wide} {dg.lookahead} {G}")
         if mode == "random":
             loc = dg.generate_random(seed=seed)
         else:

@@ -43,6 +43,10 @@ def test_bench_single_rank_cpu():
     assert r.returncode == 0, r.stdout + r.stderr
     j = _line(r.stdout)
     assert j["world_size"] == 1 and j["backend"] == "none" and j["launcher"] == "single process"
+    # the sequential Gauss denominator is timed in every run (SURVEY.md §6 caveat)
+    assert j["host_seq"]["source"].startswith("gauss_64_s measured in this run") or \
+        "measured in this run" in j["host_seq"]["source"]
+    assert j["host_seq"]["gauss_64_s"] > 0
 
 
 def test_bench_world_mismatch_fails_loudly():

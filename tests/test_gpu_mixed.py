@@ -36,9 +36,12 @@ def test_mixed_random_reaches_fp64(gelim, cuda, n):
     s.close()
 
 
-def test_mixed_is_selected_by_fp32_dtype(gelim, cuda):
-    s = gelim.GaussSolver(300, backend="hip", dtype=torch.float32, device=cuda)
-    assert s.backend == "hip-mixed"
+def test_mixed_is_explicit_opt_in(gelim, cuda):
+    """hip-mixed is slower than hip-rbt at every benched n, so fp32 on the
+    blocked backend no longer selects it silently: it must be asked for."""
+    with pytest.raises(ValueError, match="hip-mixed"):
+        gelim.GaussSolver(300, backend="hip", dtype=torch.float32, device=cuda)
+    s = gelim.GaussSolver(300, backend="hip-mixed", device=cuda)
     x, steps = s.solve_refined(gelim.random_system(300, seed=2, device=cuda))
     assert gelim.ops.gauss.error_metric(x) < 1e-9 and steps >= 1
 
@@ -212,6 +215,22 @@ def test_rbt_three_stream_small(gelim, cuda, n, monkeypatch):
     s = gelim.GaussSolver(n, backend="hip-rbt", device=cuda)
     x = s.solve(aug, check=True)
     assert s.last_fallback is None, s.last_fallback
+    ref = torch.linalg.solve(aug[:, :n], aug[:, n])
+    assert ((x - ref).abs().max() / ref.abs().max()).item() < 1e-9
+    s.close()
+
+
+@pytest.mark.parametrize("backend", ["hip-rbt", "hip-mixed"])
+def test_not_coresident_falls_back(gelim, cuda, backend, monkeypatch):
+    """When the persistent block solves cannot be co-resident (forced here;
+    a GPU with fewer CUs, or a busy one), the engine hands the system to the
+    partial-pivoting solver instead of failing the solve."""
+    monkeypatch.setenv("GELIM_FORCE_NONPERSISTENT", "1")
+    n = 700
+    aug = gelim.random_system(n, seed=13, device=cuda)
+    s = gelim.GaussSolver(n, backend=backend, device=cuda)
+    x = s.solve(aug, check=True)
+    assert s.last_fallback is not None
     ref = torch.linalg.solve(aug[:, :n], aug[:, n])
     assert ((x - ref).abs().max() / ref.abs().max()).item() < 1e-9
     s.close()

@@ -19,6 +19,9 @@ Sections after the headline (first-class fields of the same line, each timed
 between device syncs + barriers, max over ranks):
   matmul_2048           2048^2 fp32, reference timer scope, warm + cold first call
   dist_gauss_8192(_s)   ONE 8192^2 system over ALL N ranks (strong scaling)
+  dist_gauss_8192_rbt(_s) the same system over ALL N ranks on the randomised
+                        block-LDU engine (no pivot chain; parallel/dist_rbt.py)
+  dist_gauss_2048(_s)   the headline's 2048^2 system over ALL N ranks (strong)
   dist_matmul_16384(_s) 16384^2 fp32 over ALL N ranks (strong scaling)
   gauss_8192_1gpu(_s)   one 8192^2 system per GPU on the single-GPU solver
   hip_pivot_2048        the per-pivot algorithm (fp64, fp32)
@@ -29,8 +32,9 @@ between device syncs + barriers, max over ranks):
                         fp64-class answers by a different algorithm than the
                         headline's partial pivoting, so reported beside it
   external_matrices     the reference's .dat matrices vs its best OpenMP times
-  host_seq              sequential denominators (stored unless --measure-seq;
-                        the field says which)
+  host_seq              sequential denominators: the Gauss loop timed in every
+                        run on this host, the ~40 s i-j-k matmul stored unless
+                        --measure-seq (the source field says which)
 
   python bench.py [--gpus N --steps K --warmup W] [--n 2048] [--headline-only]
 
@@ -261,6 +265,7 @@ def main() -> None:
     if not args.headline_only and on_gpu:
         # strong scaling over ALL ranks: the BASELINE.json multi-GPU configs
         _section(result, "dist_gauss_8192", lambda: bench_dist_gauss(comm, gelim, torch, 8192))
+        _section(result, "dist_gauss_8192_rbt", lambda: bench_dist_rbt(comm, gelim, torch, 8192))
         # the headline's 2048 system over ALL ranks (strong scaling, SURVEY §7.4-5: latency-bound,
         # reported as measured): every block a broadcast panel, and the default form (the whole
         # 2048 system is the tail: one all_gather + the single-GPU engine on every rank)
@@ -275,7 +280,8 @@ def main() -> None:
         _section(result, "hip_pivot_2048", lambda: bench_pivot(comm, gelim, torch, n))
         _section(result, "gauss_rbt", lambda: bench_rbt(comm, gelim, torch))
         _section(result, "external_matrices", lambda: bench_external(comm, gelim, torch))
-    for key, short in (("dist_gauss_8192", "dist_gauss_8192_s"), ("dist_matmul_16384", "dist_matmul_16384_s"),
+    for key, short in (("dist_gauss_8192", "dist_gauss_8192_s"), ("dist_gauss_8192_rbt", "dist_gauss_8192_rbt_s"),
+                       ("dist_matmul_16384", "dist_matmul_16384_s"),
                        ("gauss_8192_1gpu", "gauss_8192_1gpu_s"), ("gauss_32768_1gpu", "gauss_32768_1gpu_s")):
         v = result.get(key)
         if isinstance(v, dict) and "time_s" in v:
@@ -373,6 +379,42 @@ def bench_dist_gauss(comm, gelim, torch, n: int, tail: int | None = None) -> dic
             "tflops_total": (2.0 / 3.0) * n ** 3 / dt * 1e-12, "block": dg.layout.D,
             "lookahead": dg.lookahead, "layout": "1-D column block-cyclic",
             "broadcast_panels": dg._panel_blocks(use_tail=True), "tail_rows": dg.tail_rows}
+
+
+def bench_dist_rbt(comm, gelim, torch, n: int) -> dict:
+    """The n^2 system over ALL ranks with the randomised block-LDU engine
+    (parallel/dist_rbt.py: butterfly transform local to each rank, one
+    [Dinv_k | L_k] broadcast per 128-column block with lookahead, super-block
+    solves, fp64 refinement on the original system); second solve timed.  One
+    rank: the single-GPU native solve of the same padded system, and the
+    distributed schedule on that one rank beside it."""
+    from gelim.parallel import DistributedRBT
+
+    dev = comm.device
+
+    def timed(d):
+        holder = {}
+
+        def run():
+            holder["x"] = d.solve_(holder.pop("loc"))
+
+        for _ in range(2):
+            holder["loc"] = d.generate_random(seed=99)
+            dt = _timed(comm, torch, dev, run)
+        return dt, holder["x"]
+
+    d = DistributedRBT(comm, n)
+    dt, x = timed(d)
+    out = {"time_s": dt, "error": gelim.ops.gauss.error_metric(x), "ranks": comm.world_size,
+           "padded_order": d.np, "corrections": d.last_steps, "backward_error": d.last_berr,
+           "fallback": d.last_fallback, "tflops_total": (2.0 / 3.0) * n ** 3 / dt * 1e-12,
+           "path": "single-GPU native solve" if d.fast else "distributed schedule"}
+    d.close()
+    if comm.world_size == 1:
+        d1 = DistributedRBT(comm, n, single_fast_path=False)
+        out["schedule_one_rank_s"], _ = timed(d1)
+        d1.close()
+    return out
 
 
 def bench_dist_matmul(comm, gelim, torch, n: int) -> dict:

@@ -59,6 +59,7 @@
 
 #include "device_common.h"
 #include "gelim/internal.h"
+#include "rbt.h"
 
 namespace gelim {
 int matmul_f32(const float* A, int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc, int64_t M, int64_t N,
@@ -79,24 +80,7 @@ constexpr int kQW = NB / 4;     // columns per quarter
 constexpr int kMaxBlocks = 256;  // persistent solves: every block row resident
 constexpr unsigned long long kSpinTicks = 20000000ull;  // 200 ms at 100 MHz
 
-// ---- the butterfly group matrices -------------------------------------------
-// d: 8 arrays of h doubles: R0[i], R0[i+h], S0[i], S0[i+h], Ra[i], Sa[i], Rb[i], Sb[i]
-__device__ __forceinline__ void group_w(const double* __restrict__ d, int h, int i, double (&W)[4][4]) {
-  const double r0 = d[i], r0h = d[h + i], s0 = d[2 * h + i], s0h = d[3 * h + i];
-  const double ra = d[4 * h + i], sa = d[5 * h + i], rb = d[6 * h + i], sb = d[7 * h + i];
-  // L0 (order i, i+h, i+2h, i+3h)
-  const double L0[4][4] = {{r0, 0, s0, 0}, {0, r0h, 0, s0h}, {r0, 0, -s0, 0}, {0, r0h, 0, -s0h}};
-  const double L1[4][4] = {{ra, sa, 0, 0}, {ra, -sa, 0, 0}, {0, 0, rb, sb}, {0, 0, rb, -sb}};
-#pragma unroll
-  for (int a = 0; a < 4; ++a)
-#pragma unroll
-    for (int b = 0; b < 4; ++b) {
-      double v = 0.0;
-#pragma unroll
-      for (int c = 0; c < 4; ++c) v += L1[a][c] * L0[c][b];
-      W[a][b] = 0.5 * v;  // (1/sqrt2)^2
-    }
-}
+using rbt::group_w;
 
 // M[g] = U_i^T A_g V_j for every 4 x 4 group; A is the n x n system (row
 // major, lda), padded on the fly to np with an identity block.
@@ -276,12 +260,13 @@ __device__ __forceinline__ void gj_steps(double (&a)[TR][kTl], GjLds<double>& sh
   (gj_step<TR, KK>(a, sh, kg, rg, cg), ...);
 }
 
-// Dinv = A[k0.., k0..]^-1 (fp64, row-major NB x NB) of the T block of A; with
-// Tinv, also a T copy (the fp32 engine's GEMM operand).  The block is read,
-// not modified.  info: atomicMin of 1 + k0 when the inverse is not finite (a
-// zero / tiny pivot).
+// Dinv = Ablk^-1 (fp64, row-major NB x NB) of the NB x NB T block at Ablk
+// (leading dimension lda); with Tinv, also a T copy (the fp32 engine's GEMM
+// operand).  The block is read, not modified.  info: atomicMin of 1 + k0 (the
+// block's first global column) when the inverse is not finite (a zero / tiny
+// pivot).
 template <typename T, int TR>
-__global__ __launch_bounds__(16 * NB / TR) void diag_inv_kernel(const T* __restrict__ A, int64_t lda, int k0,
+__global__ __launch_bounds__(16 * NB / TR) void diag_inv_kernel(const T* __restrict__ Ablk, int64_t lda, int k0,
                                                                double* __restrict__ Dinv, T* __restrict__ Tinv,
                                                                int* __restrict__ info) {
   __shared__ GjLds<double> sh;
@@ -289,7 +274,7 @@ __global__ __launch_bounds__(16 * NB / TR) void diag_inv_kernel(const T* __restr
   double a[TR][kTl];
 #pragma unroll
   for (int i = 0; i < TR; ++i) {
-    const T* src = A + (int64_t)(k0 + TR * rg + i) * lda + k0 + kTl * cg;
+    const T* src = Ablk + (int64_t)(TR * rg + i) * lda + kTl * cg;
 #pragma unroll
     for (int j = 0; j < kTl; ++j) a[i][j] = (double)src[j];
   }
@@ -327,20 +312,27 @@ __global__ __launch_bounds__(16 * NB / TR) void diag_inv_kernel(const T* __restr
 // 4.00, 8192 12.94 vs 13.07; before the padding 8 x 8 was, 1.64 vs 1.73).
 // Reserving the inverse's CU (LDS-exclusive launch, no GEMM workgroup beside
 // it) changed nothing measurable (profiles/rbt_engine_round3.txt).
-int diag_inv(double* M, int64_t ldm, int64_t k0, double* Di, int* info, hipStream_t s) {
+// The inverse of the NB x NB block at Ablk; `col` (its first global column)
+// only labels a non-finite result in info.
+int block_inv(const double* Ablk, int64_t lda, int64_t col, double* Di, int* info, hipStream_t s) {
   const char* e = std::getenv("GELIM_GJ_TR");  // read per launch (tests switch it)
   const int tr = e && (std::atoi(e) == 8 || std::atoi(e) == 2) ? std::atoi(e) : 4;
   if (tr == 2)
-    hipLaunchKernelGGL((diag_inv_kernel<double, 2>), dim3(1), dim3(16 * NB / 2), 0, s, M, ldm, (int)k0, Di,
+    hipLaunchKernelGGL((diag_inv_kernel<double, 2>), dim3(1), dim3(16 * NB / 2), 0, s, Ablk, lda, (int)col, Di,
                        (double*)nullptr, info);
   else if (tr == 4)
-    hipLaunchKernelGGL((diag_inv_kernel<double, 4>), dim3(1), dim3(16 * NB / 4), 0, s, M, ldm, (int)k0, Di,
+    hipLaunchKernelGGL((diag_inv_kernel<double, 4>), dim3(1), dim3(16 * NB / 4), 0, s, Ablk, lda, (int)col, Di,
                        (double*)nullptr, info);
   else
-    hipLaunchKernelGGL((diag_inv_kernel<double, 8>), dim3(1), dim3(16 * NB / 8), 0, s, M, ldm, (int)k0, Di,
+    hipLaunchKernelGGL((diag_inv_kernel<double, 8>), dim3(1), dim3(16 * NB / 8), 0, s, Ablk, lda, (int)col, Di,
                        (double*)nullptr, info);
   HIP_TRY(hipGetLastError());
   return GELIM_OK;
+}
+
+// Diagonal block k0 of the np x np matrix M.
+int diag_inv(double* M, int64_t ldm, int64_t k0, double* Di, int* info, hipStream_t s) {
+  return block_inv(M + k0 * ldm + k0, ldm, k0, Di, info, s);
 }
 
 // ---- persistent block triangular solves ----------------------------------------
@@ -1147,5 +1139,29 @@ extern "C" int64_t gelim_mixed_debug_ptrs(gelim_mixed_plan* p, void** out) {
 // Synchronous device-to-device copy of `bytes` (tests: reading the buffers above).
 extern "C" int gelim_mixed_debug_copy(void* dst, const void* src, int64_t bytes) {
   HIP_TRY(hipMemcpy(dst, src, (size_t)bytes, hipMemcpyDeviceToDevice));
+  return GELIM_OK;
+}
+
+// ---- building blocks of the distributed engine (parallel/dist_rbt.py) --------
+
+// Dinv = inverse of the 128 x 128 fp64 block at Ablk (leading dimension lda)
+// by the Gauss-Jordan kernel above; *info (device) gets atomicMin'd with
+// 1 + col when the result is not finite.
+extern "C" int gelim_rbt_block_inverse(const double* Ablk, int64_t lda, int64_t col, double* Dinv, int* info,
+                                       void* stream) {
+  if (!Ablk || !Dinv || !info || lda < gelim::NB) return GELIM_FAIL(GELIM_E_ARG, "rbt_block_inverse: bad argument");
+  return gelim::block_inv(Ablk, lda, col, Dinv, info, (hipStream_t)stream);
+}
+
+// out = U^T [b; 0] (transpose = 1) or out = V y (transpose = 0) for the
+// butterfly with diagonals d (8 x np/4, device), b / y of n entries (stride
+// incb), out of nout entries -- replicated vectors of the distributed solve.
+extern "C" int gelim_rbt_vec(const double* b, int64_t incb, int64_t n, int64_t np, const double* d, int transpose,
+                             double* out, int64_t nout, void* stream) {
+  if (!b || !d || !out || np % 4 || n > np || nout > np) return GELIM_FAIL(GELIM_E_ARG, "rbt_vec: bad argument");
+  const int64_t h = np / 4;
+  hipLaunchKernelGGL(gelim::rbt_vec_kernel, dim3((unsigned)((h + 255) / 256)), dim3(256), 0, (hipStream_t)stream, b,
+                     incb, (int)n, (int)np, d, transpose, out, (int)nout);
+  HIP_TRY(hipGetLastError());
   return GELIM_OK;
 }

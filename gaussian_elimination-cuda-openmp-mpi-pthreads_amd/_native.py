@@ -81,6 +81,13 @@ _PROTOS = {
     "gelim_mixed_plan_create2": (_vp, [_i64, _vp, _vp, _int]),
     "gelim_mixed_solve_error": (_int, [_vp, _vp]),
     "gelim_mixed_reset_error": (_int, [_vp, _vp]),
+    "gelim_rbt_block_inverse": (_int, [_vp, _i64, _i64, _vp, _vp, _vp]),
+    "gelim_rbt_vec": (_int, [_vp, _i64, _i64, _i64, _vp, _int, _vp, _i64, _vp]),
+    "gelim_drbt_transform": (_int, [_vp, _i64, _vp, _i64, _i64, _i64, _int, _int, _vp, _vp, _vp]),
+    "gelim_drbt_super_solve": (_int, [_vp, _i64, _vp, _int, _vp, _vp, _vp, _int, _vp]),
+    "gelim_drbt_gemv": (_int, [_vp, _i64, _i64, _i64, _vp, _vp, _dbl, _vp]),
+    "gelim_drbt_matvec_abs": (_int, [_vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp]),
+    "gelim_gpu_dgemm_ex": (_int, [_vp, _i64, _vp, _i64, _vp, _i64, _i64, _i64, _i64, _dbl, _int, _int, _vp]),
     "gelim_mixed_debug_ptrs": (_i64, [_vp, _vp]),
     "gelim_mixed_debug_copy": (_int, [_vp, _vp, _i64]),
     "gelim_mixed_plan_np": (_i64, [_vp]),

@@ -1,0 +1,521 @@
+"""Distributed randomised solver: the `hip-rbt` engine (random butterfly
+transform + block LDU WITHOUT pivoting + fp64 refinement, csrc/hip/lu_mixed.hip)
+over one process per GPU (RCCL).
+
+Why a second distributed solver: the partial-pivoting DistributedGauss has
+the owner of each block factor its panel alone, one global arg-max per
+column, while the other ranks wait -- its critical path barely shrinks with
+P (profiles/dist_gauss_8rank_critical_path.md).  Without pivoting there is no
+per-column reduction at all: a block step is one 128 x 128 Gauss-Jordan
+inverse plus GEMMs that every rank runs on its own columns, which is the
+reference MPI program's "every worker updates rows at every step"
+(OpenMP_and_MPI/gauss_mpi/gauss_internal_input.c:130-199) with resident data
+and one broadcast per 128-column block instead of 2 (n - i) rows shipped per
+pivot.
+
+Layout: 128-column blocks, block g on rank g % P (a rank's blocks left to
+right), the right-hand side replicated as one extra local column.  The order
+is padded with an identity block to np, a multiple of 512 P: then every
+butterfly column group {j, j + np/4, j + np/2, j + 3np/4} lies on one rank
+and the transform M = U^T A V is local (csrc/hip/dist_rbt.hip).
+
+Factorisation (block k, owner o = k % P; the single-GPU factor_impl's steps):
+  owner:      Dinv_k = M_kk^-1 (Gauss-Jordan, one workgroup)
+              broadcast [Dinv_k | M_{>k,k}]  (128 x 128 + (np - 128 (k+1)) x 128)
+  every rank: W = Dinv_k M_{k, own cols > k};  M_{>k, own cols > k} -= M_{>k,k} W
+The off-diagonal blocks stay in place as the block-LDU factor, the inverses
+with their owners.  Lookahead on two streams (DistributedGauss's scheme): the
+owner of k+1 applies panel k to block k+1 first on the main stream, inverts it
+and starts its broadcast, while the side stream applies panel k to the rest;
+panel buffers rotate over three slots.
+
+Solves (every apply of (LU)^-1, replicated vectors): super-blocks of P
+blocks -- one block per rank, the same local block index s on every rank.
+The super-diagonal S x S blocks (S = 128 P) and all inverses are all_gathered
+once after the factorisation; then per super-block, one all_reduce of the S
+partial sums, a redundant S x S block-triangular solve on every rank
+(gelim_drbt_super_solve) and a local GEMV of the rank's own block column.
+That is np / S collectives of S doubles per direction.
+
+Refinement: x += (LU)^-1 (b - A x) on the ORIGINAL (padded) system until the
+componentwise backward error max_i |r_i| / (|b| + |A||x|)_i <= 4 eps64 (one
+all_reduce of [A_loc x_loc, |A_loc||x_loc|] per step), exactly the single-GPU
+rule (gelim_mixed_solve); a non-finite inverse or a stall hands the system to
+DistributedGauss (partial pivoting) with the same 128-column block layout.
+
+One rank: the single-GPU native solve (gelim_mixed_solve) on the local
+storage, which IS the padded augmented system (single_fast_path=False runs
+the distributed schedule on one rank, for tests).
+
+CPU ranks (gloo tests without a GPU) run the same schedule with torch CPU
+ops standing in for the HIP kernels (dense butterflies, torch.linalg.inv,
+matmul) -- the orchestration, layouts and collectives are identical.
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import torch
+
+from .. import _native
+from ..utils.tensors import ptr, stream_handle
+from .comm import Communicator
+
+NB = 128  # block width (= the single-GPU engine's)
+NBUF = 3  # broadcast buffers in rotation
+SEED = 0x5EED  # butterfly seed (the single-GPU GaussSolver's)
+
+
+def padded_order(n: int, P: int) -> int:
+    """np: n rounded up to a multiple of 512 P (butterfly column groups local)."""
+    q = 4 * NB * P
+    return -(-n // q) * q
+
+
+def butterfly_diagonals(npad: int, seed: int = SEED) -> tuple[np.ndarray, np.ndarray]:
+    """U's and V's butterfly diagonals, 8 x npad/4 each: exp(r / 10), r uniform
+    in [-1/2, 1/2] -- GaussSolver._init_mixed's draw for the same npad."""
+    rng = np.random.default_rng(seed)
+    ud = np.exp((rng.random(2 * npad) - 0.5) / 10.0)
+    vd = np.exp((rng.random(2 * npad) - 0.5) / 10.0)
+    return ud, vd
+
+
+def butterfly_dense(d: np.ndarray, npad: int) -> torch.Tensor:
+    """Dense npad x npad butterfly W with W[i + c h, i + q h] = W_i[c][q]
+    (csrc/hip/rbt.h group_w), so U^T A V = W_u^T A W_v (CPU path, tests)."""
+    h = npad // 4
+    i = np.arange(h)
+    r0, r0h, s0, s0h, ra, sa, rb, sb = (d[k * h:(k + 1) * h] for k in range(8))
+    z = np.zeros(h)
+    L0 = np.array([[r0, z, s0, z], [z, r0h, z, s0h], [r0, z, -s0, z], [z, r0h, z, -s0h]])  # 4 x 4 x h
+    L1 = np.array([[ra, sa, z, z], [ra, -sa, z, z], [z, z, rb, sb], [z, z, rb, -sb]])
+    Wg = 0.5 * np.einsum("ach,cbh->abh", L1, L0)  # W_i[a][b]
+    W = np.zeros((npad, npad))
+    for a in range(4):
+        for b in range(4):
+            W[i + a * h, i + b * h] = Wg[a, b]
+    return torch.from_numpy(W)
+
+
+class DistributedRBT:
+    """Randomised block-LDU solve of one n x n system over all ranks of comm."""
+
+    def __init__(self, comm: Communicator, n: int, seed: int = SEED, lookahead: bool = True,
+                 single_fast_path: bool = True, max_steps: int = 6):
+        self.comm, self.n = comm, n
+        self.P, self.rank = comm.world_size, comm.rank
+        self.device = comm.device
+        self.gpu = self.device.type == "cuda"
+        self.lookahead = lookahead
+        self.max_steps = max_steps
+        self.np = padded_order(n, self.P)
+        self.nb = self.np // NB
+        self.nloc = self.np // self.P
+        self.nbl = self.nb // self.P  # local blocks = super-blocks
+        self.ld = self.nloc + 2       # b in column nloc; even, 16-byte rows
+        self.fast = single_fast_path and self.P == 1 and self.gpu
+        self._ud, self._vd = butterfly_diagonals(self.np, seed)
+        lb = torch.arange(self.nloc) // NB
+        self.gcol = ((lb * self.P + self.rank) * NB + torch.arange(self.nloc) % NB).to(self.device)
+        self.last_steps, self.last_berr, self.last_fallback = 0, None, None
+        self._plan = None
+        self._fallback_solver = None
+        dev = self.device
+        f64 = dict(dtype=torch.float64, device=dev)
+        if self.fast:
+            lib = _native.lib()
+            with torch.cuda.device(dev):
+                self._plan = lib.gelim_mixed_plan_create2(self.np, self._ud.ctypes.data, self._vd.ctypes.data, 1)
+            if not self._plan:
+                raise _native.GelimError(_native.E_ARG, _native.last_error())
+            return
+        self.ud = torch.from_numpy(self._ud).to(dev)
+        self.vd = torch.from_numpy(self._vd).to(dev)
+        self.M = torch.zeros((self.np, self.ld), **f64)
+        self.Dinv = torch.zeros((self.nbl, NB, NB), **f64)
+        self._bsz = NB * NB + self.np * NB
+        self._bufs = [torch.zeros(self._bsz, **f64) for _ in range(NBUF if lookahead else 2)]
+        self._Wm = torch.zeros((NB, NB), **f64)
+        self._Ws = torch.zeros((NB, self.nloc), **f64)
+        self._info = torch.full((1,), 0x7F7F7F7F, dtype=torch.int32, device=dev)
+        if self.gpu:
+            self._side = torch.cuda.Stream(dev)
+        else:
+            self._Wu = butterfly_dense(self._ud, self.np)
+            Wv = butterfly_dense(self._vd, self.np)
+            gc = self.gcol.cpu()
+            self._Wv_loc = Wv[gc][:, gc].contiguous()
+            self._Wv = Wv
+
+    # -- data placement -------------------------------------------------------
+    def empty_local(self) -> torch.Tensor:
+        """np x ld storage: the rank's columns of the padded system, b (replicated) in column nloc."""
+        return torch.zeros((self.np, self.ld), dtype=torch.float64, device=self.device)
+
+    def _pad_identity(self, loc: torch.Tensor) -> None:
+        pad = (self.gcol >= self.n).nonzero().flatten()
+        if pad.numel():
+            loc[self.gcol[pad], pad] = 1.0
+
+    def scatter_from_global(self, aug: torch.Tensor) -> torch.Tensor:
+        n = self.n
+        loc = self.empty_local()
+        real = (self.gcol < n).nonzero().flatten()
+        loc[:n, real] = aug[:, :n].to(self.device)[:, self.gcol[real]]
+        loc[:n, self.nloc] = aug[:, n].to(self.device)
+        self._pad_identity(loc)
+        return loc
+
+    def generate_random(self, seed: int = 0) -> torch.Tensor:
+        """The rank's columns of ops.init.random_system(n, seed) (bit-identical
+        A) and b = A (1..n) by one all_reduce of the partial products."""
+        n = self.n
+        loc = self.empty_local()
+        lib = _native.lib()
+        for lb in range(self.nbl):
+            g = lb * self.P + self.rank
+            w = max(0, min(NB, n - g * NB))
+            if w == 0:
+                continue
+            view = loc[:n, lb * NB:lb * NB + w]
+            if self.gpu:
+                _native.check(lib.gelim_gpu_init_random_block(ptr(view), loc.stride(0), 0, n, g * NB, w, seed,
+                                                              stream_handle(self.device)), "init_random_block")
+            else:
+                tmp = torch.empty((n, w), dtype=torch.float64)
+                lib.gelim_init_random_block_f64(ptr(tmp), w, 0, n, g * NB, w, seed)
+                view.copy_(tmp)
+        idx = torch.where(self.gcol < n, self.gcol + 1, torch.zeros_like(self.gcol)).to(torch.float64)
+        b = loc[:, :self.nloc] @ idx
+        self.comm.all_reduce(b)
+        loc[:, self.nloc] = b
+        self._pad_identity(loc)
+        return loc
+
+    # -- building blocks (HIP kernels on GPU ranks, torch on CPU ranks) ---------
+    def _sh(self, stream=None):
+        if not self.gpu:
+            return None
+        return stream.cuda_stream if stream is not None else stream_handle(self.device)
+
+    def _transform(self, loc: torch.Tensor) -> None:
+        if self.gpu:
+            _native.check(_native.lib().gelim_drbt_transform(ptr(loc), self.ld, ptr(self.M), self.ld, self.np,
+                                                             self.nloc, self.P, self.rank, ptr(self.ud), ptr(self.vd),
+                                                             self._sh()), "drbt_transform")
+        else:
+            self.M[:, :self.nloc] = self._Wu.T @ loc[:, :self.nloc] @ self._Wv_loc
+
+    def _inverse(self, k: int, out: torch.Tensor) -> None:
+        lc = (k // self.P) * NB
+        blk = self.M[k * NB:(k + 1) * NB, lc:lc + NB]
+        if self.gpu:
+            _native.check(_native.lib().gelim_rbt_block_inverse(ptr(blk), self.ld, k * NB, ptr(out),
+                                                                ptr(self._info), self._sh()), "rbt_block_inverse")
+        else:
+            inv = torch.linalg.inv(blk)
+            if not bool(torch.isfinite(inv).all()):
+                self._info.fill_(min(int(self._info.item()), k * NB + 1))
+            out.copy_(inv)
+
+    def _gemm(self, C: torch.Tensor, A: torch.Tensor, B: torch.Tensor, alpha: float, acc: bool, stream=None) -> None:
+        """C (+)= alpha A B on 2-D row-major views."""
+        M_, N_ = C.shape
+        K_ = A.shape[1]
+        if M_ == 0 or N_ == 0:
+            return
+        if self.gpu:
+            _native.check(_native.lib().gelim_gpu_dgemm_ex(ptr(C), C.stride(0), ptr(A), A.stride(0), ptr(B),
+                                                           B.stride(0), M_, N_, K_, alpha, int(acc), 0,
+                                                           self._sh(stream)), "dgemm_ex")
+        elif acc:
+            C.add_(A @ B, alpha=alpha)
+        else:
+            torch.matmul(A, B, out=C)
+            if alpha != 1.0:
+                C.mul_(alpha)
+
+    def _apply_panel(self, k: int, buf: torch.Tensor, cb: int, ce: int, W: torch.Tensor, stream=None) -> None:
+        """Panel k (buf = [Dinv_k | L_k]) applied to local columns [cb, ce)."""
+        if ce <= cb:
+            return
+        m = self.np - (k + 1) * NB
+        Dk = buf[:NB * NB].view(NB, NB)
+        Wv = W[:, :ce - cb]
+        self._gemm(Wv, Dk, self.M[k * NB:(k + 1) * NB, cb:ce], 1.0, False, stream)
+        if m > 0:
+            L = buf[NB * NB:NB * NB + m * NB].view(m, NB)
+            self._gemm(self.M[(k + 1) * NB:, cb:ce], L, Wv, -1.0, True, stream)
+
+    def _pack(self, k: int, buf: torch.Tensor) -> None:
+        """Owner of block k: invert its diagonal block and pack [Dinv_k | L_k]."""
+        lb = k // self.P
+        self._inverse(k, self.Dinv[lb])
+        buf[:NB * NB].copy_(self.Dinv[lb].view(-1))
+        m = self.np - (k + 1) * NB
+        if m > 0:
+            buf[NB * NB:NB * NB + m * NB].view(m, NB).copy_(self.M[(k + 1) * NB:, lb * NB:(lb + 1) * NB])
+
+    def _bsize(self, k: int) -> int:
+        return NB * NB + (self.np - (k + 1) * NB) * NB
+
+    # -- factorisation --------------------------------------------------------
+    def factor_(self, loc: torch.Tensor) -> int:
+        """Transform + block-LDU factorisation; returns 0 or 1 + the first
+        column whose diagonal-block inverse is not finite (min over ranks)."""
+        self._info.fill_(0x7F7F7F7F)
+        self._transform(loc)
+        if self.lookahead and self.gpu:
+            self._factor_lookahead()
+        else:
+            self._factor_serial()
+        v = self._info.to(torch.int64)
+        self.comm.all_reduce(v, "min")
+        val = int(v.item())
+        return 0 if val == 0x7F7F7F7F else val
+
+    def _factor_serial(self) -> None:
+        comm, r, P = self.comm, self.rank, self.P
+        B = self._bufs
+        for k in range(self.nb):
+            buf = B[k & 1]
+            o = k % P
+            if r == o:
+                self._pack(k, buf)
+            comm.broadcast(buf[:self._bsize(k)], src=o)
+            self._apply_panel(k, buf, self._first_col_after(k), self.nloc, self._Ws)
+
+    def _first_col_after(self, k: int) -> int:
+        """Local column offset of this rank's first block with global index > k."""
+        q = max(0, -(-(k + 1 - self.rank) // self.P))
+        return min(q * NB, self.nloc)
+
+    def _factor_lookahead(self) -> None:
+        """Two streams (module docstring).  main: [wait panel k] [panel k ->
+        block k+1] [invert k+1, pack] [broadcast k+1]; side: [wait panel k]
+        [panel k -> the next block this rank inverts after k+1] (ev_first)
+        [panel k -> every other column] (ev_rest)."""
+        comm, r, P, nb = self.comm, self.rank, self.P, self.nb
+        main = torch.cuda.current_stream(self.device)
+        side = self._side
+        side.wait_stream(main)  # M as the transform left it
+        B = self._bufs
+        nbuf = len(B)
+        ev_avail = [torch.cuda.Event() for _ in range(nb)]
+        ev_first = [torch.cuda.Event() for _ in range(nb)]
+        ev_rest = [torch.cuda.Event() for _ in range(nb)]
+        handles = {}
+        if r == 0:
+            self._pack(0, B[0])
+        handles[0] = comm.broadcast_async(B[0][:self._bsize(0)], src=0)
+        for k in range(nb):
+            buf = B[k % nbuf]
+            handles.pop(k).wait()  # main waits for panel k
+            ev_avail[k].record(main)
+            c0 = self._first_col_after(k)
+            nxt = k + 1 < nb
+            o1 = (k + 1) % P if nxt else -1
+            cs = c0 + (NB if o1 == r else 0)  # block k+1 is main's
+            wf = NB if cs < self.nloc else 0
+            side.wait_event(ev_avail[k])
+            with torch.cuda.stream(side):
+                self._apply_panel(k, buf, cs, cs + wf, self._Ws, side)
+                ev_first[k].record(side)
+                self._apply_panel(k, buf, cs + wf, self.nloc, self._Ws, side)
+                ev_rest[k].record(side)
+            if o1 == r:
+                if k >= 1:
+                    main.wait_event(ev_first[k - 1])  # panel k-1 reached block k+1 on the side stream
+                self._apply_panel(k, buf, c0, c0 + NB, self._Wm)
+                if k + 1 >= nbuf:
+                    main.wait_event(ev_rest[k + 1 - nbuf])  # its buffer slot is free again
+                self._pack(k + 1, B[(k + 1) % nbuf])
+            if nxt:
+                if o1 != r and k + 1 >= nbuf:
+                    main.wait_event(ev_rest[k + 1 - nbuf])
+                handles[k + 1] = comm.broadcast_async(B[(k + 1) % nbuf][:self._bsize(k + 1)], src=o1)
+        main.wait_event(ev_rest[nb - 1])
+
+    # -- solves ----------------------------------------------------------------
+    def _gather_solve_blocks(self) -> None:
+        """All ranks get every super-diagonal S x S block of the factor and every
+        diagonal-block inverse (one all_gather each)."""
+        P, S, ns = self.P, NB * self.P, self.nbl
+        mine = torch.empty((ns, S, NB), dtype=torch.float64, device=self.device)
+        for s in range(ns):
+            mine[s] = self.M[s * S:(s + 1) * S, s * NB:(s + 1) * NB]
+        g = torch.empty((P, ns, S, NB), dtype=torch.float64, device=self.device)
+        self.comm.all_gather(g.view(-1), mine.view(-1))
+        self._Fs = g.permute(1, 2, 0, 3).reshape(ns, S, S).contiguous()
+        gd = torch.empty((P, ns, NB, NB), dtype=torch.float64, device=self.device)
+        self.comm.all_gather(gd.view(-1), self.Dinv.contiguous().view(-1))
+        self._Ds = gd.permute(1, 0, 2, 3).contiguous()  # (ns, P, 128, 128)
+        del mine, g, gd
+
+    def _super_solve(self, s: int, rhs: torch.Tensor, x: torch.Tensor, ysave: torch.Tensor | None,
+                     upper: bool) -> None:
+        P = self.P
+        if self.gpu:
+            _native.check(_native.lib().gelim_drbt_super_solve(ptr(self._Fs[s]), NB * P, ptr(self._Ds[s]), P,
+                                                               ptr(rhs), ptr(x), ptr(ysave), int(upper), self._sh()),
+                          "drbt_super_solve")
+            return
+        F, D = self._Fs[s], self._Ds[s]
+        order = reversed(range(P)) if upper else range(P)
+        for b in order:
+            R = slice(b * NB, (b + 1) * NB)
+            C = slice((b + 1) * NB, P * NB) if upper else slice(0, b * NB)
+            y = rhs[R] - F[R, C] @ x[C]
+            if ysave is not None:
+                ysave[R] = y
+            x[R] = D[b] @ y
+
+    def _gemv(self, A: torch.Tensor, x: torch.Tensor, y: torch.Tensor) -> None:
+        """y += A x."""
+        if A.shape[0] == 0:
+            return
+        if self.gpu:
+            _native.check(_native.lib().gelim_drbt_gemv(ptr(A), A.stride(0), A.shape[0], A.shape[1], ptr(x), ptr(y),
+                                                        1.0, self._sh()), "drbt_gemv")
+        else:
+            y += A @ x
+
+    def _rbt_vec(self, v: torch.Tensor, d: torch.Tensor, transpose: bool, out: torch.Tensor) -> None:
+        if self.gpu:
+            _native.check(_native.lib().gelim_rbt_vec(ptr(v), 1, self.np, self.np, ptr(d), int(transpose), ptr(out),
+                                                      self.np, self._sh()), "rbt_vec")
+        else:
+            W = self._Wu if transpose else self._Wv
+            out.copy_(W.T @ v if transpose else W @ v)
+
+    def apply(self, rhs: torch.Tensor) -> torch.Tensor:
+        """(U^T)^-1-free correction: V (LU)^-1 U^T rhs for a replicated np-vector."""
+        P, S, ns = self.P, NB * self.P, self.nbl
+        r = self.rank
+        dev = self.device
+        c = torch.empty(self.np, dtype=torch.float64, device=dev)
+        self._rbt_vec(rhs, self.ud if self.gpu else None, True, c)
+        z = torch.empty_like(c)
+        y = torch.empty_like(c)
+        acc = torch.zeros_like(c)
+        for s in range(ns):
+            R = slice(s * S, (s + 1) * S)
+            t = acc[R].clone()
+            self.comm.all_reduce(t)
+            self._super_solve(s, c[R] - t, z[R], y[R], False)
+            if s + 1 < ns:
+                zb = z[s * S + r * NB:s * S + (r + 1) * NB]
+                self._gemv(self.M[(s + 1) * S:, s * NB:(s + 1) * NB], zb, acc[(s + 1) * S:])
+        xs = torch.empty_like(c)
+        acc.zero_()
+        for s in reversed(range(ns)):
+            R = slice(s * S, (s + 1) * S)
+            t = acc[R].clone()
+            self.comm.all_reduce(t)
+            self._super_solve(s, y[R] - t, xs[R], None, True)
+            if s > 0:
+                xb = xs[s * S + r * NB:s * S + (r + 1) * NB]
+                self._gemv(self.M[:s * S, s * NB:(s + 1) * NB], xb, acc[:s * S])
+        out = torch.empty_like(c)
+        self._rbt_vec(xs, self.vd if self.gpu else None, False, out)
+        return out
+
+    def _residual(self, loc: torch.Tensor, x: torch.Tensor) -> tuple[torch.Tensor, float]:
+        """r = b - A x of the ORIGINAL n-system (x[n:] is zero: the identity
+        padding is not part of the problem, as in gelim_mixed_solve) and the
+        componentwise backward error max_{i<n} |r_i| / (|b| + |A||x|)_i (one
+        all_reduce); r[n:] = 0."""
+        xl = x[self.gcol].contiguous()
+        yw = torch.empty((2, self.np), dtype=torch.float64, device=self.device)
+        A = loc[:, :self.nloc]
+        if self.gpu:
+            _native.check(_native.lib().gelim_drbt_matvec_abs(ptr(loc), self.ld, self.np, self.nloc, ptr(xl),
+                                                              ptr(yw[0]), ptr(yw[1]), self._sh()), "drbt_matvec_abs")
+        else:
+            yw[0] = A @ xl
+            yw[1] = A.abs() @ xl.abs()
+        self.comm.all_reduce(yw)
+        n = self.n
+        b = loc[:n, self.nloc]
+        r = torch.zeros(self.np, dtype=torch.float64, device=self.device)
+        r[:n] = b - yw[0, :n]
+        w = b.abs() + yw[1, :n]
+        tiny = torch.finfo(torch.float64).tiny
+        rn = r[:n]
+        om = torch.where(w > 0, rn.abs() / w.clamp_min(tiny), torch.where(rn != 0, torch.full_like(rn, math.inf), rn))
+        return r, float(om.max())
+
+    # -- the solve --------------------------------------------------------------
+    def solve_(self, loc: torch.Tensor) -> torch.Tensor:
+        """x (n entries, replicated on every rank) of the local system `loc`
+        (np x ld from generate_random / scatter_from_global; kept intact, it is
+        the residual's system)."""
+        self.last_steps, self.last_berr, self.last_fallback = 0, None, None
+        if self.fast:
+            return self._solve_single(loc)
+        info = self.factor_(loc)
+        if info:
+            return self._fallback(loc, f"no-pivot LU: non-finite diagonal-block inverse at column {info - 1}")
+        self._gather_solve_blocks()
+        x = self.apply(loc[:, self.nloc].contiguous())
+        x[self.n:] = 0.0
+        eps = torch.finfo(torch.float64).eps
+        strict, loose = 4.0 * eps, max(math.sqrt(self.n), 8.0) * eps
+        prev, best, xb = math.inf, math.inf, None
+        for it in range(self.max_steps + 1):
+            r, om = self._residual(loc, x)
+            self.last_steps, self.last_berr = it, om
+            if om <= strict:
+                return x[:self.n]
+            if not om < 0.9 * prev or it == self.max_steps:  # NaN, stagnated or out of steps
+                if om <= loose and om <= best:
+                    return x[:self.n]
+                if best <= loose:
+                    self.last_berr = best
+                    return xb[:self.n]
+                return self._fallback(loc, f"refinement stalled after {it} corrections (componentwise backward "
+                                           f"error {om:.3e})")
+            if om < best:
+                best, xb = om, x.clone()
+            prev = om
+            x = x + self.apply(r)
+            x[self.n:] = 0.0
+        raise AssertionError("unreachable")
+
+    def _solve_single(self, loc: torch.Tensor) -> torch.Tensor:
+        """One rank: the native single-GPU solve of the padded augmented system."""
+        import ctypes
+
+        x = torch.empty(self.np, dtype=torch.float64, device=self.device)
+        st, be = ctypes.c_int(0), ctypes.c_double(0.0)
+        rc = _native.check(_native.lib().gelim_mixed_solve(self._plan, ptr(loc), self.ld, ptr(x), self.max_steps,
+                                                           ctypes.byref(st), ctypes.byref(be), self._sh()),
+                           "mixed_solve")
+        self.last_steps, self.last_berr = st.value, be.value
+        if rc == 1:
+            return self._fallback(loc, f"no-pivot LU: zero pivot or refinement stalled after {st.value} corrections")
+        return x[:self.n]
+
+    def _fallback(self, loc: torch.Tensor, reason: str) -> torch.Tensor:
+        """Partial pivoting (DistributedGauss) on the same system: its
+        128-column block layout puts block g on rank g % P at the same local
+        column, so the slab is a copy of ours."""
+        from .dist_gauss import DistributedGauss
+
+        self.last_fallback = reason
+        if self._fallback_solver is None:
+            self._fallback_solver = DistributedGauss(self.comm, self.n, block=NB)
+        dg = self._fallback_solver
+        gl = dg.empty_local()
+        rows = min(dg.n_pad, self.np)
+        w = min(dg.nloc, self.nloc)
+        gl[:rows, :w] = loc[:rows, :w]
+        gl[:rows, dg.nloc] = loc[:rows, self.nloc]
+        return dg.solve_(gl)
+
+    def close(self) -> None:
+        if self._plan:
+            _native.lib().gelim_mixed_plan_destroy(self._plan)
+            self._plan = None

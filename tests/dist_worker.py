@@ -99,3 +99,28 @@ def matmul(rank, world, port, outdir, M, K, N, algo, device):
     except Exception:
         (Path(outdir) / f"err{rank}.txt").write_text(traceback.format_exc())
         raise
+
+
+def rbt(rank, world, port, outdir, n, seed, device, mode, lookahead=True, fast=True):
+    """DistributedRBT (randomised block LDU over the ranks): x to x{rank}.pt,
+    [steps, berr, fallback] to meta{rank}.txt."""
+    import torch
+
+    import gelim
+    from gelim.parallel import DistributedRBT
+    from gelim.parallel import comm as C
+
+    try:
+        comm = _init(rank, world, port, device)
+        d = DistributedRBT(comm, n, lookahead=lookahead, single_fast_path=fast)
+        if mode == "random":
+            loc = d.generate_random(seed=seed)
+        else:
+            loc = d.scatter_from_global(gelim.augment_with_rhs(gelim.utils.io.load_fixture(mode)))
+        x = d.solve_(loc)
+        torch.save(x.cpu(), Path(outdir) / f"x{rank}.pt")
+        (Path(outdir) / f"meta{rank}.txt").write_text(f"{d.last_steps} {d.last_berr} {d.last_fallback}")
+        C.destroy()
+    except Exception:
+        (Path(outdir) / f"err{rank}.txt").write_text(traceback.format_exc())
+        raise

@@ -73,6 +73,10 @@ template <typename T>
 int pivot_elimination(T* A, int64_t lda, int64_t n, int mode, T* mcol, int* info, hipStream_t s, int* ipiv,
                       double* diag);
 template <typename T>
+int pivot_persistent(T* A, int64_t lda, int64_t n, int mode, int* info, int* ipiv, double* diag, void* ws,
+                     hipStream_t s);
+size_t pivot_persist_ws_bytes(int64_t n);
+template <typename T>
 int pivot_lower_resolve(const T* A, int64_t lda, int64_t n, const int* ipiv, const double* diag, const double* c,
                         T* y, hipStream_t s);
 }  // namespace gelim
@@ -89,6 +93,7 @@ struct gelim_gauss_plan {
   double* diag = nullptr;                // hip-pivot: pivot values of the stored factors
   void* ry = nullptr;                    // hip-pivot re-solve: L~^-1 P c (plan dtype)
   double* tmp = nullptr;
+  void* pws = nullptr;                   // hip-pivot: the persistent kernel's exchange granules
   hipStream_t cap = nullptr;
   hipStream_t side = nullptr;            // lookahead: wide trailing updates
   std::vector<hipEvent_t> ev_panel, ev_wide;
@@ -452,16 +457,25 @@ int enqueue(gelim_gauss_plan* p, const void* src, int64_t src_ld, void* dx, void
     return backsub_f64(A, lda, A + n, lda, static_cast<double*>(dx),
                        static_cast<double*>(bnorm), n, 0, p->yw, s);
   }
+  // hip-pivot: one persistent launch for the whole elimination when the
+  // system fits the chip's registers (n <= 2048) and the grid is
+  // co-resident (pivot_persist.hip), else two launches per column
   if (p->eb == 8) {
     double* A = static_cast<double*>(p->work);
-    GELIM_TRY(pivot_elimination<double>(A, lda, n, p->pivot, static_cast<double*>(p->mcol),
-                                        p->info, s, p->piv, p->diag));
+    int rc = pivot_persistent<double>(A, lda, n, p->pivot, p->info, p->piv, p->diag, p->pws, s);
+    if (rc < 0) return rc;
+    if (rc == 1)
+      GELIM_TRY(pivot_elimination<double>(A, lda, n, p->pivot, static_cast<double*>(p->mcol),
+                                          p->info, s, p->piv, p->diag));
     return backsub_f64(A, lda, A + n, lda, static_cast<double*>(dx),
                        static_cast<double*>(bnorm), n, 1, p->yw, s);
   }
   float* A = static_cast<float*>(p->work);
-  GELIM_TRY(pivot_elimination<float>(A, lda, n, p->pivot, static_cast<float*>(p->mcol), p->info,
-                                     s, p->piv, p->diag));
+  int rc = pivot_persistent<float>(A, lda, n, p->pivot, p->info, p->piv, p->diag, p->pws, s);
+  if (rc < 0) return rc;
+  if (rc == 1)
+    GELIM_TRY(pivot_elimination<float>(A, lda, n, p->pivot, static_cast<float*>(p->mcol), p->info,
+                                       s, p->piv, p->diag));
   return backsub_f32(A, lda, A + n, lda, static_cast<double*>(dx), static_cast<double*>(bnorm), n,
                      1, p->yw, s);
 }
@@ -570,6 +584,8 @@ extern "C" gelim_gauss_plan* gelim_gauss_plan_create(int64_t n, int algo, int pi
   if (hipMalloc((void**)&p->tmp, (size_t)2 * 32 * (n + 1) * sizeof(double)) != hipSuccess)
     return fail("tmp");
   if (hipStreamCreateWithFlags(&p->cap, hipStreamNonBlocking) != hipSuccess) return fail("stream");
+  if (algo == GELIM_GPU_PIVOT && hipMalloc(&p->pws, gelim::pivot_persist_ws_bytes(n)) != hipSuccess)
+    return fail("pivot exchange buffers");
   if (const char* e = std::getenv("GELIM_LOOKAHEAD")) p->lookahead = std::atoi(e) != 0;
   if (const char* e = std::getenv("GELIM_SCHEDULE")) p->fused = std::string(e) != "classic";
   if (p->lookahead) p->fused = false;
@@ -659,6 +675,7 @@ extern "C" void gelim_gauss_plan_destroy(gelim_gauss_plan* p) {
   (void)hipFree(p->diag);
   (void)hipFree(p->ry);
   (void)hipFree(p->tmp);
+  (void)hipFree(p->pws);
   (void)hipFree(p->big_ws);
   (void)hipFree(p->big_pairs);
   (void)hipFree(p->big_net);

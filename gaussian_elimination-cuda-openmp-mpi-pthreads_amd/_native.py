@@ -87,6 +87,7 @@ _PROTOS = {
     "gelim_drbt_super_solve": (_int, [_vp, _i64, _vp, _int, _vp, _vp, _vp, _int, _vp]),
     "gelim_drbt_gemv": (_int, [_vp, _i64, _i64, _i64, _vp, _vp, _dbl, _vp]),
     "gelim_drbt_matvec_abs": (_int, [_vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp]),
+    "gelim_gpu_dgemm_thin": (_int, [_vp, _i64, _vp, _i64, _vp, _i64, _i64, _i64, _i64, _dbl, _int, _int, _vp]),
     "gelim_gpu_dgemm_ex": (_int, [_vp, _i64, _vp, _i64, _vp, _i64, _i64, _i64, _i64, _dbl, _int, _int, _vp]),
     "gelim_mixed_debug_ptrs": (_i64, [_vp, _vp]),
     "gelim_mixed_debug_copy": (_int, [_vp, _vp, _i64]),

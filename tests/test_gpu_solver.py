@@ -303,3 +303,30 @@ def test_zero_rule_tracks_positions(gelim, cuda, n):
         x = gelim.GaussSolver(n, backend=backend, pivot="zero", device=cuda).solve(aug)
         assert gelim.ops.gauss.error_metric(x) < 1e-9, backend
         assert torch.allclose(x.cpu(), ref, rtol=1e-8, atol=0), backend
+
+
+@pytest.mark.parametrize("pivot", ["partial", "zero"])
+@pytest.mark.parametrize("n", [1, 9, 257, 1000, 2048])
+def test_pivot_persistent_matches_two_kernel_form(gelim, cuda, pivot, n, monkeypatch):
+    """hip-pivot runs as ONE persistent launch for n <= 2048 (pivot_persist.hip:
+    registers hold the matrix, two tagged one-hop exchanges per column); the
+    two-kernel-per-column form (forced by GELIM_FORCE_NONPERSISTENT=1) is the
+    oracle, together with fp64 torch.linalg.solve."""
+    aug = gelim.random_system(n, seed=n + 41, device=cuda)
+    if pivot == "zero":  # no interchanges on a random matrix: make it diagonally dominant
+        aug[:, :n] += n * torch.eye(n, dtype=torch.float64, device=cuda)
+    s1 = gelim.GaussSolver(n, backend="hip-pivot", pivot=pivot, device=cuda)
+    x1 = s1.solve(aug, check=True)
+    monkeypatch.setenv("GELIM_FORCE_NONPERSISTENT", "1")
+    s2 = gelim.GaussSolver(n, backend="hip-pivot", pivot=pivot, device=cuda, use_graph=False)
+    x2 = s2.solve(aug, check=True)
+    ref = torch.linalg.solve(aug[:, :n], aug[:, n])
+    tol = 1e-9
+    assert ((x1 - x2).abs().max() / x2.abs().max()).item() < tol
+    assert ((x1 - ref).abs().max() / ref.abs().max()).item() < tol
+    # the stored factors answer a new right-hand side (resolve) the same way
+    c = torch.randn(n, dtype=torch.float64, device=cuda, generator=torch.Generator(cuda).manual_seed(1))
+    r1, r2 = s1.resolve(c), s2.resolve(c)
+    assert ((r1 - r2).abs().max() / r2.abs().max()).item() < tol
+    s1.close()
+    s2.close()

@@ -42,6 +42,9 @@
 #include "gelim/internal.h"
 
 namespace gelim {
+int dgemm_thin(double* C, int64_t ldc, const double* A, int64_t lda, const double* B, int64_t ldb, int64_t M,
+               int64_t N, int64_t K, double alpha, int accumulate, int variant, hipStream_t s);
+
 namespace {
 
 constexpr int BM = 128, BN = 128, BK = 16;  // the default (large) tile
@@ -332,6 +335,16 @@ int dgemm_launch(double* C, int64_t ldc, const double* A, int64_t lda, const dou
       return e ? std::atoi(e) : 0;
     }();
     const bool small = force ? force == 64 : (int64_t)tm * tn < (int64_t)ncu;
+    // thin problems with a short K (the block-LDU engine's column / row block
+    // updates and W products, K = 128 / 256): the register-direct kernel of
+    // dgemm_thin.hip (no LDS, no per-K-step barrier), GELIM_DGEMM_THIN=0 off
+    static const int thin = [] {
+      const char* e = std::getenv("GELIM_DGEMM_THIN");
+      return e ? std::atoi(e) : 0;
+    }();
+    if (thin && small && cap == 0 && force == 0 && K <= 256 &&
+        dgemm_thin(C, ldc, A, lda, B, ldb, M, N, K, alpha, accumulate, 0, s) == GELIM_OK)
+      return GELIM_OK;
     if (small && cap == 0) {
       const int tm6 = (int)((M + 63) / 64), tn6 = (int)((N + 63) / 64);
       Args g6 = g;

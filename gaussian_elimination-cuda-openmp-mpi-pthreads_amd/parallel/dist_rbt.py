@@ -125,9 +125,14 @@ class DistributedRBT:
         dev = self.device
         f64 = dict(dtype=torch.float64, device=dev)
         if self.fast:
+            # the plan solves the ORIGINAL n-system (its refinement must not see the
+            # identity padding) with the butterflies of order np (n padded to 128)
             lib = _native.lib()
+            # GaussSolver's draw for the plan's own padding: the same butterflies,
+            # so one rank reproduces the single-GPU hip-rbt solve bit for bit
+            self._ud, self._vd = butterfly_diagonals(int(lib.gelim_mixed_padded(n)), seed)
             with torch.cuda.device(dev):
-                self._plan = lib.gelim_mixed_plan_create2(self.np, self._ud.ctypes.data, self._vd.ctypes.data, 1)
+                self._plan = lib.gelim_mixed_plan_create2(n, self._ud.ctypes.data, self._vd.ctypes.data, 1)
             if not self._plan:
                 raise _native.GelimError(_native.E_ARG, _native.last_error())
             return
@@ -488,15 +493,23 @@ class DistributedRBT:
         """One rank: the native single-GPU solve of the padded augmented system."""
         import ctypes
 
-        x = torch.empty(self.np, dtype=torch.float64, device=self.device)
+        n = self.n
+        if n == self.np:  # the local storage is the augmented system [A | b]
+            aug, ld = loc, self.ld
+        else:  # b sits at column np: an (n, n+1) copy for the native solve
+            aug = torch.empty((n, n + 2), dtype=torch.float64, device=self.device)
+            aug[:, :n] = loc[:n, :n]
+            aug[:, n] = loc[:n, self.nloc]
+            ld = n + 2
+        x = torch.empty(n, dtype=torch.float64, device=self.device)
         st, be = ctypes.c_int(0), ctypes.c_double(0.0)
-        rc = _native.check(_native.lib().gelim_mixed_solve(self._plan, ptr(loc), self.ld, ptr(x), self.max_steps,
+        rc = _native.check(_native.lib().gelim_mixed_solve(self._plan, ptr(aug), ld, ptr(x), self.max_steps,
                                                            ctypes.byref(st), ctypes.byref(be), self._sh()),
                            "mixed_solve")
         self.last_steps, self.last_berr = st.value, be.value
         if rc == 1:
             return self._fallback(loc, f"no-pivot LU: zero pivot or refinement stalled after {st.value} corrections")
-        return x[:self.n]
+        return x
 
     def _fallback(self, loc: torch.Tensor, reason: str) -> torch.Tensor:
         """Partial pivoting (DistributedGauss) on the same system: its

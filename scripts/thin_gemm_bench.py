@@ -2,12 +2,17 @@
 factor_la2 at n = 8192, parallel/dist_rbt.py): dgemm.hip's LDS-tiled kernel
 (gelim_gpu_dgemm_ex) vs the register-direct thin kernel (dgemm_thin.hip,
 variants 1..5), microseconds per call (CUDA events, 50 calls) and TFLOP/s,
-each result checked against torch (hipBLAS) fp64.
+each result checked against torch (hipBLAS) fp64.  The event timing of
+back-to-back ctypes launches is host-bound below ~10 us; kernel times come
+from rocprofv3 (scripts/thin_gemm_prof.sh).
 
-  python scripts/thin_gemm_bench.py > profiles/dgemm_thin_r4.txt
+  python scripts/thin_gemm_bench.py [--shape i] > profiles/dgemm_thin_r4.txt
 """
+import os
 import sys
 from pathlib import Path
+
+os.environ.setdefault("GELIM_DGEMM_THIN", "0")  # "lds" = dgemm.hip's LDS-tiled kernel
 
 import torch
 
@@ -29,12 +34,18 @@ SHAPES = [  # M, N, K, accumulate, what
 
 
 def main():
+    import argparse
+
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--shape", type=int, default=-1, help="index into SHAPES (default: all)")
+    args = ap.parse_args()
+    shapes = SHAPES if args.shape < 0 else [SHAPES[args.shape]]
     dev = torch.device("cuda:0")
     lib = gelim._native.lib()
     sh = stream_handle(dev)
     g = torch.Generator(device=dev).manual_seed(0)
     print(f"{'shape':>22} {'kernel':>10} {'us':>8} {'TF/s':>7} {'rel_err':>9}  what")
-    for M, N, K, acc, what in SHAPES:
+    for M, N, K, acc, what in shapes:
         A = torch.randn(M, K + 2, dtype=torch.float64, device=dev, generator=g)[:, :K]
         B = torch.randn(K, N + 2, dtype=torch.float64, device=dev, generator=g)[:, :N]
         C0 = torch.randn(M, N + 2, dtype=torch.float64, device=dev, generator=g)[:, :N]

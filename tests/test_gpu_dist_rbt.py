@@ -63,6 +63,13 @@ def test_one_rank_schedule_matches_fast_path(gelim, cuda):
         d.close()
     assert _rel(out[False], out[True]) < 1e-11
     assert gelim.ops.gauss.error_metric(out[False]) < 1e-9
+    # the fast path is the single-GPU hip-rbt solve (same butterflies): same bits
+    aug = gelim.random_system(n, seed=4, device=cuda)
+    d = DistributedRBT(c, n)
+    s = gelim.GaussSolver(n, backend="hip-rbt", device=cuda)
+    assert torch.equal(s.solve(aug), d.solve_(d.scatter_from_global(aug)))
+    s.close()
+    d.close()
 
 
 @pytest.mark.parametrize("name", ["jpwh_991", "sherman3", "saylr4"])

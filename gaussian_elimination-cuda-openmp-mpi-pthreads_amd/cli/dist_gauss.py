@@ -17,6 +17,10 @@ Unlike the reference's master/worker scheme (rank 0 ships full rows out and
 back every pivot step), the matrix is resident and
 column block-cyclic: one panel broadcast per block (parallel/dist_gauss.py).
 
+--algo rbt runs the randomised block-LDU engine instead (parallel/dist_rbt.py:
+random butterfly transform, no pivot chain, fp64 refinement, partial-
+pivoting fallback), the distributed form of `--backend=hip-rbt`.
+
 --emulate P runs P ranks as threads of this one process on one device (the
 emulated communicator, parallel/emulated.py) — the distributed algorithm on a
 single GPU.  --checkpoint-dir / --checkpoint-every / --resume save and resume
@@ -49,6 +53,8 @@ def parse(argv=None):
                    help="the reference's -t: here the number of ranks (GPUs) -- set by the launcher "
                         "(torchrun --nproc-per-node N); a mismatch is reported, not silently ignored")
     p.add_argument("--pivot", default="partial", choices=["partial", "zero"])
+    p.add_argument("--algo", default="gauss", choices=["gauss", "rbt"],
+                   help="gauss: partial pivoting (DistributedGauss); rbt: randomised block LDU (DistributedRBT)")
     p.add_argument("--device", default=None, help="cpu | cuda (default: cuda when visible)")
     p.add_argument("--warmup", type=int, default=0, help="untimed solves before the timed one")
     p.add_argument("--verify", action="store_true", help="print the max error against the exact solution")
@@ -85,6 +91,33 @@ def synthetic_local(dg: DistributedGauss) -> torch.Tensor:
     return loc
 
 
+def synthetic_local_rbt(d) -> torch.Tensor:
+    """The internal system in DistributedRBT's layout (local column jl is
+    global column d.gcol[jl]; identity padding)."""
+    n = d.n
+    loc = d.empty_local()
+    real = (d.gcol < n).nonzero().flatten()
+    i = torch.arange(1, n + 1, dtype=torch.float64, device=d.device).view(n, 1)
+    j = (d.gcol[real] + 1).to(torch.float64).view(1, -1)
+    loc[:n, real] = 2.0 * torch.minimum(i, j)
+    loc[:n, d.nloc] = torch.arange(n, dtype=torch.float64, device=d.device)
+    d._pad_identity(loc)
+    return loc
+
+
+def make_solver(args, comm, n: int):
+    """(solver, local-system builder for the internal mode, block width)."""
+    if args.algo == "rbt":
+        from ..parallel.dist_rbt import NB, DistributedRBT
+
+        if args.checkpoint_dir:
+            raise SystemExit("--checkpoint-dir is supported by --algo gauss only")
+        d = DistributedRBT(comm, n)
+        return d, (lambda: synthetic_local_rbt(d)), NB
+    dg = DistributedGauss(comm, n, block=args.block, pivot=args.pivot)
+    return dg, (lambda: synthetic_local(dg)), dg.layout.D
+
+
 def main(argv=None) -> int:
     args = parse(argv)
     if args.emulate and args.emulate > 1:
@@ -116,14 +149,14 @@ def run(args, comm) -> int:
     try:
         if args.file is None:
             n = args.size
-            dg = DistributedGauss(comm, n, block=args.block, pivot=args.pivot)
+            dg, build, D = make_solver(args, comm, n)
             for _ in range(args.warmup):
-                dg.solve_(synthetic_local(dg))
+                dg.solve_(build())
             sync()
             ck = dg.checkpointer(args.checkpoint_dir, args.checkpoint_every) if args.checkpoint_dir else None
             t0 = time.perf_counter()
-            loc = synthetic_local(dg)
-            x = dg.solve_(loc, ckpt=ck, resume=args.resume)
+            loc = build()
+            x = dg.solve_(loc, ckpt=ck, resume=args.resume) if ck else dg.solve_(loc)
             sync()
             dt = time.perf_counter() - t0
             if comm.rank == 0:
@@ -136,20 +169,20 @@ def run(args, comm) -> int:
                     print(f"Max error vs exact solution: {err:e}")
                 if args.json:
                     json_line({"program": "dist_gauss_internal", "n": n, "ranks": comm.world_size,
-                                     "block": dg.layout.D, "time_s": dt, "max_abs_error": err,
+                                     "algo": args.algo, "block": D, "time_s": dt, "max_abs_error": err,
                                      "backend": comm.backend, "device": dev.type})
         else:
             A = load_global(args.file)
             n = A.shape[0]
             aug = augment_with_rhs(A)
-            dg = DistributedGauss(comm, n, block=args.block, pivot=args.pivot)
+            dg, _, D = make_solver(args, comm, n)
             for _ in range(args.warmup):
                 dg.solve_(dg.scatter_from_global(aug))
             loc = dg.scatter_from_global(aug)
             ck = dg.checkpointer(args.checkpoint_dir, args.checkpoint_every) if args.checkpoint_dir else None
             sync()
             t0 = time.perf_counter()
-            x = dg.solve_(loc, ckpt=ck, resume=args.resume)
+            x = dg.solve_(loc, ckpt=ck, resume=args.resume) if ck else dg.solve_(loc)
             sync()
             dt = time.perf_counter() - t0
             if comm.rank == 0:
@@ -159,7 +192,7 @@ def run(args, comm) -> int:
                 print(f"Error: {err:e}", flush=True)
                 if args.json:
                     json_line({"program": "dist_gauss_external", "file": args.file, "n": n,
-                                     "ranks": comm.world_size, "block": dg.layout.D, "time_s": dt,
+                                     "ranks": comm.world_size, "algo": args.algo, "block": D, "time_s": dt,
                                      "error": err, "backend": comm.backend, "device": dev.type})
     except _native.SingularMatrixError:
         if comm.rank == 0:

@@ -51,3 +51,19 @@ def test_dist_matmul_cli(algo, nproc):
     assert re.search(r"^GPU Time: \d+\.\d{6}$", out, re.M), out
     rel = float(re.search(r"Max relative error: (\S+)", out).group(1))
     assert rel < 1e-5
+
+
+def test_dist_gauss_cli_rbt_internal():
+    """--algo rbt: the randomised block-LDU engine over the ranks, same output."""
+    out = torchrun(2, "gelim.cli.dist_gauss", "-s", "300", "--algo", "rbt", "--device", "cpu", "--verify")
+    assert re.search(r"^Application time: \d+\.\d{6} Secs$", out, re.M), out
+    err = float(re.search(r"Max error vs exact solution: (\S+)", out).group(1))
+    assert err < 1e-10
+
+
+def test_dist_gauss_cli_rbt_external():
+    out = torchrun(2, "gelim.cli.dist_gauss", str(ROOT / "data" / "jpwh_991.coo.npz"), "--algo", "rbt",
+                   "--device", "cpu")
+    assert re.search(r"^Time:  \d+\.\d{6} seconds$", out, re.M), out
+    err = float(re.search(r"^Error: (\S+)$", out, re.M).group(1))
+    assert err < 1e-12

@@ -139,6 +139,78 @@ __global__ __launch_bounds__(256) void dgemm_thin_kernel(ThinArgs g) {
     }
 }
 
+// Deep-prefetch form: DEPTH chunks in flight (a register ring, the chunk loop
+// fully unrolled up to K = 256 so every ring index is static): the K loop
+// pays ceil(nch / DEPTH) memory round trips instead of nch.
+template <int MB, int NB, int KC, int DEPTH>
+__global__ __launch_bounds__(256) void dgemm_thin_deep_kernel(ThinArgs g) {
+  constexpr int kMaxCh = 256 / (4 * KC);
+  const int lane = threadIdx.x & 63;
+  const int wid = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (wid >= g.ntiles) return;
+  const int tr = wid / g.tiles_n, tc = wid - tr * g.tiles_n;
+  const int m0 = tr * 16 * MB, n0 = tc * 16 * NB;
+  const int r = lane & 15, q = lane >> 4;
+  const double* arow[MB];
+#pragma unroll
+  for (int i = 0; i < MB; ++i) arow[i] = g.A + (int64_t)min(m0 + 16 * i + r, g.M - 1) * g.lda + KC * q;
+  const double* bcol[NB];
+#pragma unroll
+  for (int j = 0; j < NB; ++j) bcol[j] = g.B + (int64_t)(KC * q) * g.ldb + min(n0 + 16 * j + r, g.N - 1);
+  const int nch = g.K / (4 * KC);
+  Chunk<MB, NB, KC> ring[DEPTH];
+#pragma unroll
+  for (int c = 0; c < DEPTH; ++c)
+    if (c < nch) load_chunk<MB, NB, KC>(ring[c], arow, bcol, g.ldb, c * 4 * KC);
+  dev::d4 cv[MB][NB];
+#pragma unroll
+  for (int i = 0; i < MB; ++i)
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      const int col = min(n0 + 16 * j + r, g.N - 1);
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const int row = min(m0 + 16 * i + q + 4 * rr, g.M - 1);
+        cv[i][j][rr] = g.acc ? g.C[(int64_t)row * g.ldc + col] : 0.0;
+      }
+    }
+  dev::d4 acc[MB][NB];
+#pragma unroll
+  for (int i = 0; i < MB; ++i)
+#pragma unroll
+    for (int j = 0; j < NB; ++j) acc[i][j] = dev::d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int c = 0; c < kMaxCh; ++c) {
+    if (c < nch) {
+      mma_chunk<MB, NB, KC>(acc, ring[c % DEPTH]);
+      if (c + DEPTH < nch) load_chunk<MB, NB, KC>(ring[c % DEPTH], arow, bcol, g.ldb, (c + DEPTH) * 4 * KC);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < MB; ++i)
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      const int col = n0 + 16 * j + r;
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const int row = m0 + 16 * i + q + 4 * rr;
+        if (row < g.M && col < g.N) g.C[(int64_t)row * g.ldc + col] = fma(g.alpha, acc[i][j][rr], cv[i][j][rr]);
+      }
+    }
+}
+
+template <int MB, int NB, int KC, int DEPTH>
+int launch_deep(double* C, int64_t ldc, const double* A, int64_t lda, const double* B, int64_t ldb, int64_t M,
+                int64_t N, int64_t K, double alpha, int accumulate, hipStream_t s) {
+  if (K > 256) return 1;
+  const int tm = (int)((M + 16 * MB - 1) / (16 * MB)), tn = (int)((N + 16 * NB - 1) / (16 * NB));
+  ThinArgs g{C, ldc, A, lda, B, ldb, (int)M, (int)N, (int)K, tn, tm * tn, alpha, accumulate ? 1 : 0};
+  hipLaunchKernelGGL((dgemm_thin_deep_kernel<MB, NB, KC, DEPTH>), dim3((unsigned)((g.ntiles + 3) / 4)), dim3(256), 0,
+                     s, g);
+  HIP_TRY(hipGetLastError());
+  return GELIM_OK;
+}
+
 template <int MB, int NB, int KC>
 int launch_thin(double* C, int64_t ldc, const double* A, int64_t lda, const double* B, int64_t ldb, int64_t M,
                 int64_t N, int64_t K, double alpha, int accumulate, hipStream_t s) {
@@ -152,7 +224,8 @@ int launch_thin(double* C, int64_t ldc, const double* A, int64_t lda, const doub
 }  // namespace
 
 // Shapes: variant 0 picks by shape (the wave tile along the long side),
-// 1..5 force (MB, NB, KC) = (2,2,4), (2,2,8), (1,4,4), (4,1,4), (2,4,4).
+// 1..5 force (MB, NB, KC) = (2,2,4), (2,2,8), (1,4,4), (4,1,4), (2,4,4);
+// 6..8 the deep-prefetch form (MB, NB, KC, DEPTH) = (1,1,4,8), (2,2,4,4), (1,2,4,6).
 // Contract: K a multiple of 32 (16 for KC = 4 variants), A 16-byte aligned,
 // lda even.  Returns 1 (nothing launched) when the contract does not hold.
 int dgemm_thin(double* C, int64_t ldc, const double* A, int64_t lda, const double* B, int64_t ldb, int64_t M,
@@ -177,6 +250,15 @@ int dgemm_thin(double* C, int64_t ldc, const double* A, int64_t lda, const doubl
     case 5:
       if (K % 16) return 1;
       return launch_thin<2, 4, 4>(C, ldc, A, lda, B, ldb, M, N, K, alpha, accumulate, s);
+    case 6:  // deep prefetch: every K chunk of a 16 x 16 wave tile in flight (K <= 128)
+      if (K % 16) return 1;
+      return launch_deep<1, 1, 4, 8>(C, ldc, A, lda, B, ldb, M, N, K, alpha, accumulate, s);
+    case 7:
+      if (K % 16) return 1;
+      return launch_deep<2, 2, 4, 4>(C, ldc, A, lda, B, ldb, M, N, K, alpha, accumulate, s);
+    case 8:
+      if (K % 16) return 1;
+      return launch_deep<1, 2, 4, 6>(C, ldc, A, lda, B, ldb, M, N, K, alpha, accumulate, s);
     default:
       return 1;
   }

@@ -51,7 +51,8 @@ def main():
         C0 = torch.randn(M, N + 2, dtype=torch.float64, device=dev, generator=g)[:, :N]
         ref = (C0 if acc else 0) - A @ B
         flops = 2.0 * M * N * K
-        for name, v in [("lds", -1), ("thin1", 1), ("thin2", 2), ("thin3", 3), ("thin4", 4), ("thin5", 5)]:
+        for name, v in [("lds", -1), ("thin1", 1), ("thin2", 2), ("thin3", 3), ("thin4", 4), ("thin5", 5),
+                        ("deep6", 6), ("deep7", 7), ("deep8", 8)]:
             C = C0.clone() if True else None
             Cv = torch.empty(M, N + 2, dtype=torch.float64, device=dev)[:, :N]
             Cv.copy_(C0)

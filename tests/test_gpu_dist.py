@@ -99,8 +99,9 @@ def test_dist_gauss_gpu_processes_many_panels(tmp_path, gelim, cuda, world, n, b
     emu = run_emulated(world, body, device=cuda, timeout_s=150)[0]
     if world == 2:  # a 2-term sum has one rounding whatever the order: same bits
         assert torch.equal(xs[0], emu)
-    else:  # gloo may reduce in another order than rank 0, 1, 2
-        assert torch.allclose(xs[0], emu, rtol=1e-11, atol=1e-11)
+    else:  # gloo may sum b's 3 partial products in another order: b differs in its
+        # last bits, and the solve amplifies that by ~cond(A)
+        assert ((xs[0] - emu).abs().max() / emu.abs().max()).item() < 1e-9
     aug = gelim.random_system(n, seed=29, device=cuda)
     ref = _torch_ref(gelim, aug)
     assert torch.allclose(xs[0], ref, rtol=1e-7, atol=1e-7)

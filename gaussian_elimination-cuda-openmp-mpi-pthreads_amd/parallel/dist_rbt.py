@@ -20,14 +20,18 @@ butterfly column group {j, j + np/4, j + np/2, j + 3np/4} lies on one rank
 and the transform M = U^T A V is local (csrc/hip/dist_rbt.hip).
 
 Factorisation (block k, owner o = k % P; the single-GPU factor_impl's steps):
-  owner:      Dinv_k = M_kk^-1 (Gauss-Jordan, one workgroup)
-              broadcast [Dinv_k | M_{>k,k}]  (128 x 128 + (np - 128 (k+1)) x 128)
+  owner:      broadcast M_{>=k,k}, its column from the diagonal block down
+              ((np - 128 k) x 128), as soon as it is up to date; THEN
+              Dinv_k = M_kk^-1 (Gauss-Jordan, one workgroup) and broadcast
+              the 128 x 128 inverse -- the big transfer runs under the inverse
   every rank: W = Dinv_k M_{k, own cols > k};  M_{>k, own cols > k} -= M_{>k,k} W
 The off-diagonal blocks stay in place as the block-LDU factor, the inverses
 with their owners.  Lookahead on two streams (DistributedGauss's scheme): the
-owner of k+1 applies panel k to block k+1 first on the main stream, inverts it
-and starts its broadcast, while the side stream applies panel k to the rest;
-panel buffers rotate over three slots.
+owner of k+1 applies panel k to block k+1 first on the main stream and ships
+block k+1, while the side stream applies panel k to the rest; broadcast
+buffers rotate over three slots.  Critical path per block: max(column
+transfer, inverse + one small broadcast) + the 128-wide update of the next
+block (profiles/dist_rbt_8rank_critical_path.md).
 
 Solves (every apply of (LU)^-1, replicated vectors): super-blocks of P
 blocks -- one block per rank, the same local block index s on every rank.
@@ -140,8 +144,9 @@ class DistributedRBT:
         self.vd = torch.from_numpy(self._vd).to(dev)
         self.M = torch.zeros((self.np, self.ld), **f64)
         self.Dinv = torch.zeros((self.nbl, NB, NB), **f64)
-        self._bsz = NB * NB + self.np * NB
-        self._bufs = [torch.zeros(self._bsz, **f64) for _ in range(NBUF if lookahead else 2)]
+        nbuf = NBUF if lookahead else 2
+        self._xbufs = [torch.zeros(self.np * NB, **f64) for _ in range(nbuf)]  # column k from the diagonal down
+        self._dbufs = [torch.zeros(NB * NB, **f64) for _ in range(nbuf)]       # its diagonal block's inverse
         self._Wm = torch.zeros((NB, NB), **f64)
         self._Ws = torch.zeros((NB, self.nloc), **f64)
         self._info = torch.full((1,), 0x7F7F7F7F, dtype=torch.int32, device=dev)
@@ -242,29 +247,35 @@ class DistributedRBT:
             if alpha != 1.0:
                 C.mul_(alpha)
 
-    def _apply_panel(self, k: int, buf: torch.Tensor, cb: int, ce: int, W: torch.Tensor, stream=None) -> None:
-        """Panel k (buf = [Dinv_k | L_k]) applied to local columns [cb, ce)."""
+    def _apply_panel(self, k: int, xb: torch.Tensor, db: torch.Tensor, cb: int, ce: int, W: torch.Tensor,
+                     stream=None) -> None:
+        """Panel k (xb = column k from the diagonal block down, db = the
+        inverse of that diagonal block) applied to local columns [cb, ce):
+        W = Dinv_k M[k, cb:ce];  M[>k, cb:ce] -= L_k W."""
         if ce <= cb:
             return
         m = self.np - (k + 1) * NB
-        Dk = buf[:NB * NB].view(NB, NB)
+        Dk = db.view(NB, NB)
         Wv = W[:, :ce - cb]
         self._gemm(Wv, Dk, self.M[k * NB:(k + 1) * NB, cb:ce], 1.0, False, stream)
         if m > 0:
-            L = buf[NB * NB:NB * NB + m * NB].view(m, NB)
+            L = xb[NB * NB:NB * NB + m * NB].view(m, NB)
             self._gemm(self.M[(k + 1) * NB:, cb:ce], L, Wv, -1.0, True, stream)
 
-    def _pack(self, k: int, buf: torch.Tensor) -> None:
-        """Owner of block k: invert its diagonal block and pack [Dinv_k | L_k]."""
+    def _pack_col(self, k: int, xb: torch.Tensor) -> None:
+        """Owner of block k: its column from the diagonal block down, contiguous."""
+        lb = k // self.P
+        m = self.np - k * NB
+        xb[:m * NB].view(m, NB).copy_(self.M[k * NB:, lb * NB:(lb + 1) * NB])
+
+    def _invert(self, k: int, db: torch.Tensor) -> None:
+        """Owner of block k: Dinv_k (kept for the solves) into the broadcast buffer."""
         lb = k // self.P
         self._inverse(k, self.Dinv[lb])
-        buf[:NB * NB].copy_(self.Dinv[lb].view(-1))
-        m = self.np - (k + 1) * NB
-        if m > 0:
-            buf[NB * NB:NB * NB + m * NB].view(m, NB).copy_(self.M[(k + 1) * NB:, lb * NB:(lb + 1) * NB])
+        db.copy_(self.Dinv[lb].view(-1))
 
-    def _bsize(self, k: int) -> int:
-        return NB * NB + (self.np - (k + 1) * NB) * NB
+    def _xsize(self, k: int) -> int:
+        return (self.np - k * NB) * NB
 
     # -- factorisation --------------------------------------------------------
     def factor_(self, loc: torch.Tensor) -> int:
@@ -283,14 +294,15 @@ class DistributedRBT:
 
     def _factor_serial(self) -> None:
         comm, r, P = self.comm, self.rank, self.P
-        B = self._bufs
         for k in range(self.nb):
-            buf = B[k & 1]
+            xb, db = self._xbufs[k & 1], self._dbufs[k & 1]
             o = k % P
             if r == o:
-                self._pack(k, buf)
-            comm.broadcast(buf[:self._bsize(k)], src=o)
-            self._apply_panel(k, buf, self._first_col_after(k), self.nloc, self._Ws)
+                self._pack_col(k, xb)
+                self._invert(k, db)
+            comm.broadcast(xb[:self._xsize(k)], src=o)
+            comm.broadcast(db, src=o)
+            self._apply_panel(k, xb, db, self._first_col_after(k), self.nloc, self._Ws)
 
     def _first_col_after(self, k: int) -> int:
         """Local column offset of this rank's first block with global index > k."""
@@ -298,26 +310,41 @@ class DistributedRBT:
         return min(q * NB, self.nloc)
 
     def _factor_lookahead(self) -> None:
-        """Two streams (module docstring).  main: [wait panel k] [panel k ->
-        block k+1] [invert k+1, pack] [broadcast k+1]; side: [wait panel k]
-        [panel k -> the next block this rank inverts after k+1] (ev_first)
-        [panel k -> every other column] (ev_rest)."""
+        """Two streams and TWO broadcasts per block (module docstring).  The
+        owner of block k+1 ships its column (diagonal block down) as soon as
+        panel k has reached it, and only then inverts the diagonal block and
+        ships the 128 x 128 inverse: the big transfer runs under the inverse,
+        so a block costs max(transfer, inverse) on the critical path instead
+        of their sum.
+          main (owner of k+1): [wait column k, Dinv_k] [panel k -> block k+1]
+                               [pack column k+1, bcast] [invert k+1, bcast]
+          side (every rank):   [wait panel k] [panel k -> the next block this
+                               rank owns after k+1] (ev_first) [the rest] (ev_rest)"""
         comm, r, P, nb = self.comm, self.rank, self.P, self.nb
         main = torch.cuda.current_stream(self.device)
         side = self._side
         side.wait_stream(main)  # M as the transform left it
-        B = self._bufs
-        nbuf = len(B)
+        X, D = self._xbufs, self._dbufs
+        nbuf = len(X)
         ev_avail = [torch.cuda.Event() for _ in range(nb)]
         ev_first = [torch.cuda.Event() for _ in range(nb)]
         ev_rest = [torch.cuda.Event() for _ in range(nb)]
-        handles = {}
-        if r == 0:
-            self._pack(0, B[0])
-        handles[0] = comm.broadcast_async(B[0][:self._bsize(0)], src=0)
+        hx, hd = {}, {}
+
+        def ship(k: int) -> None:  # every rank: the two broadcasts of block k, in this order
+            o = k % P
+            if r == o:
+                self._pack_col(k, X[k % nbuf])
+            hx[k] = comm.broadcast_async(X[k % nbuf][:self._xsize(k)], src=o)
+            if r == o:
+                self._invert(k, D[k % nbuf])
+            hd[k] = comm.broadcast_async(D[k % nbuf], src=o)
+
+        ship(0)
         for k in range(nb):
-            buf = B[k % nbuf]
-            handles.pop(k).wait()  # main waits for panel k
+            xb, db = X[k % nbuf], D[k % nbuf]
+            hx.pop(k).wait()
+            hd.pop(k).wait()  # main waits for panel k
             ev_avail[k].record(main)
             c0 = self._first_col_after(k)
             nxt = k + 1 < nb
@@ -326,21 +353,18 @@ class DistributedRBT:
             wf = NB if cs < self.nloc else 0
             side.wait_event(ev_avail[k])
             with torch.cuda.stream(side):
-                self._apply_panel(k, buf, cs, cs + wf, self._Ws, side)
+                self._apply_panel(k, xb, db, cs, cs + wf, self._Ws, side)
                 ev_first[k].record(side)
-                self._apply_panel(k, buf, cs + wf, self.nloc, self._Ws, side)
+                self._apply_panel(k, xb, db, cs + wf, self.nloc, self._Ws, side)
                 ev_rest[k].record(side)
             if o1 == r:
                 if k >= 1:
                     main.wait_event(ev_first[k - 1])  # panel k-1 reached block k+1 on the side stream
-                self._apply_panel(k, buf, c0, c0 + NB, self._Wm)
-                if k + 1 >= nbuf:
-                    main.wait_event(ev_rest[k + 1 - nbuf])  # its buffer slot is free again
-                self._pack(k + 1, B[(k + 1) % nbuf])
+                self._apply_panel(k, xb, db, c0, c0 + NB, self._Wm)
             if nxt:
-                if o1 != r and k + 1 >= nbuf:
-                    main.wait_event(ev_rest[k + 1 - nbuf])
-                handles[k + 1] = comm.broadcast_async(B[(k + 1) % nbuf][:self._bsize(k + 1)], src=o1)
+                if k + 1 >= nbuf:
+                    main.wait_event(ev_rest[k + 1 - nbuf])  # the buffer slots of k+1 are free again
+                ship(k + 1)
         main.wait_event(ev_rest[nb - 1])
 
     # -- solves ----------------------------------------------------------------

@@ -51,11 +51,6 @@ from pathlib import Path
 
 ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
-# 8 hardware queues per process (gelim sets the same default on import; here it
-# is set before torch can initialise the HIP runtime): with HIP's 4, a plan's
-# side stream can share the caller's queue and serialise with it
-# (profiles/hw_queues_r4.txt)
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
 
 BASELINE_GAUSS_S = 0.509428  # OpenMP best, 2048^2 (OpenMP_and_MPI/Report.pdf p.4)
 BASELINE_MATMUL_S = 0.114906  # CUDA V2 end-to-end, 2048^2 (CUDA_and_OpenMP/Report.pdf p.2)

@@ -420,7 +420,14 @@ __global__ void fold_info_kernel(int* __restrict__ info, const int* __restrict__
 
 }  // namespace
 
-size_t workspace_bytes() { return leafk::kKeyBytes + leafk::kRowBytes; }
+namespace sleaf {  // leaf_stream.hip
+size_t scratch_bytes();
+int factor(double* A, int64_t lda, int64_t m, int64_t c0, int mode, int* ipiv, int* pairs, int* info,
+           void* scratch, hipStream_t s);
+}  // namespace sleaf
+
+// the register leaf's exchange areas, then the streamed leaf's scratch
+size_t workspace_bytes() { return leafk::kKeyBytes + leafk::kRowBytes + sleaf::scratch_bytes(); }
 int leaf_width() { return LW; }
 
 // Waves per leaf participant: GELIM_LEAF_WAVES = 1 | 4 (default 1), raised
@@ -437,7 +444,19 @@ int leaf_waves(int64_t m) {
   }();
   return (env == 1 && m > (int64_t)leafk::kMaxP * leafk::kRowsPerWave) ? 4 : env;
 }
-int64_t max_rows() { return (int64_t)leafk::kMaxP * 4 * leafk::kRowsPerWave; }
+// Rows the register-resident leaf holds (256 participants x 4 waves x 256
+// rows: the chip's register file); taller panels take the streamed leaf
+// (leaf_stream.hip, HBM-resident, same results bit for bit), so the leaf
+// itself no longer caps the order -- memory does.
+int64_t reg_max_rows() { return (int64_t)leafk::kMaxP * 4 * leafk::kRowsPerWave; }
+int64_t max_rows() { return (int64_t)1 << 26; }
+// GELIM_LEAF_STREAM=1: the streamed leaf at every m (tests compare the two);
+// read per call
+bool leaf_streamed(int64_t m) {
+  if (m > reg_max_rows()) return true;
+  const char* e = std::getenv("GELIM_LEAF_STREAM");
+  return e != nullptr && std::atoi(e) == 1;
+}
 int leaf_participants(int64_t m) {
   const int64_t rows = (int64_t)leaf_waves(m) * leafk::kRowsPerWave;
   return (int)((m + rows - 1) / rows);
@@ -445,6 +464,7 @@ int leaf_participants(int64_t m) {
 // CUs a leaf of m rows needs at once (its waves take a whole SIMD's registers:
 // four single-wave participants or one 4-wave participant per CU)
 int leaf_cus(int64_t m) {
+  if (m > reg_max_rows()) return 0;  // the streamed leaf: ordinary launches, no residency
   const int P = leaf_participants(m);
   return leaf_waves(m) == 4 ? P : (P + 3) / 4;
 }
@@ -458,6 +478,9 @@ int leaf_factor(double* A, int64_t lda, int64_t m, int64_t c0, int mode, int* ip
   if (m < LW || m > max_rows()) return GELIM_FAIL(GELIM_E_ARG, "leaf: m out of range");
   if ((reinterpret_cast<uintptr_t>(A) & 15) || (lda & 1)) return GELIM_FAIL(GELIM_E_ARG, "leaf: alignment");
   if (leaf < 0 || leaf >= (1 << 25)) return GELIM_FAIL(GELIM_E_ARG, "leaf: counter out of range");
+  if (leaf_streamed(m))
+    return sleaf::factor(A, lda, m, c0, mode, ipiv, pairs, info,
+                         static_cast<char*>(ws) + leafk::kKeyBytes + leafk::kRowBytes, s);
   const int nwv = leaf_waves(m);
   leafk::LeafArgs a{};
   a.A = A;

@@ -944,11 +944,11 @@ extern "C" gelim_mixed_plan* gelim_mixed_plan_create2(int64_t n, const double* u
     int reserve = 0;
     if (const char* e = std::getenv("GELIM_RBT_RESERVE")) reserve = std::max(0, std::atoi(e));
     p->cap = reserve == 0 ? 0 : ncu > reserve + 8 ? ncu - reserve : std::max(8, ncu / 2);
-    if (hipStreamCreateWithFlags(&p->side, hipStreamNonBlocking) != hipSuccess) return fail("side stream");
+    if (gelim::side_stream_create(&p->side) != GELIM_OK) return fail("side stream");
     if (hipEventCreateWithFlags(&p->e0, hipEventDisableTiming) != hipSuccess) return fail("event");
     if (hipEventCreateWithFlags(&p->e1, hipEventDisableTiming) != hipSuccess) return fail("event");
     if (p->pairs && p->aux_on) {
-      if (hipStreamCreateWithFlags(&p->aux, hipStreamNonBlocking) != hipSuccess) return fail("aux stream");
+      if (gelim::side_stream_create(&p->aux) != GELIM_OK) return fail("aux stream");
       if (hipEventCreateWithFlags(&p->ea, hipEventDisableTiming) != hipSuccess) return fail("event");
       if (hipEventCreateWithFlags(&p->eb, hipEventDisableTiming) != hipSuccess) return fail("event");
     }

@@ -557,7 +557,7 @@ extern "C" gelim_gauss_plan* gelim_gauss_plan_create(int64_t n, int algo, int pi
       // whose participants cannot all be resident would spin into its timeout
       reserve = std::max(reserve, gelim::big::leaf_cus(n) + 8);
       p->big_cap = ncu > reserve + 8 ? ncu - reserve : std::max(8, ncu / 2);
-      if (hipStreamCreateWithFlags(&p->big_side, hipStreamNonBlocking) != hipSuccess) return fail("side stream");
+      if (gelim::side_stream_create(&p->big_side) != GELIM_OK) return fail("side stream");
       if (std::getenv("GELIM_BIG_NET") == nullptr || std::atoi(std::getenv("GELIM_BIG_NET")) != 0)
         if (hipMalloc((void**)&p->big_net, sizeof(int) * (1 + 2 * (size_t)gelim::big::laswp_net_max())) != hipSuccess)
           return fail("net movement");
@@ -628,7 +628,7 @@ extern "C" gelim_gauss_plan* gelim_gauss_plan_create(int64_t n, int algo, int pi
         }
     }
     const size_t S = p->step_k.size();
-    if (hipStreamCreateWithFlags(&p->side, hipStreamNonBlocking) != hipSuccess) return fail("side");
+    if (gelim::side_stream_create(&p->side) != GELIM_OK) return fail("side");
     p->ev_panel.assign(S, nullptr);
     p->ev_wide.assign(S + 1, nullptr);
     for (auto* v : {&p->ev_panel, &p->ev_wide})

@@ -4,6 +4,8 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <mutex>
+#include <vector>
 
 #include "device_common.h"
 #include "gelim/internal.h"
@@ -173,7 +175,141 @@ int init_synthetic_f32(float* A, int64_t lda, int64_t n, hipStream_t s) {
   return GELIM_OK;
 }
 
+// ---- side streams on a hardware queue of their own ---------------------------
+// HIP maps streams onto at most GPU_MAX_HW_QUEUES hardware queues per process
+// and shares queues once they run out.  A lookahead side stream that shares
+// the caller's queue runs AFTER the caller's work instead of beside it: the
+// 8192 solve took 49.4 instead of 33.9 ms, the distributed 2048 solve 16 instead
+// of 8 ms, depending on how many streams the process had created before
+// (profiles/hw_queues_r4.txt).  So a side stream is probed when it is made:
+// a kernel on the default stream waits (bounded, 5 ms) for a flag that a
+// kernel on the new stream sets -- it sees the flag only if the two run
+// concurrently.  A stream that failed is parked (kept alive, so the runtime
+// does not hand its queue out again) and another one is made, up to 8 times.
+namespace {
+constexpr unsigned long long kProbeTicks = 500000ull;  // 5 ms at 100 MHz
+
+__global__ void probe_wait_kernel(int* w, unsigned long long ticks) {
+  if (threadIdx.x != 0) return;
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  int seen = 0;
+  for (;;) {
+    if (__hip_atomic_load(&w[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) {
+      seen = 1;
+      break;
+    }
+    if (__builtin_amdgcn_s_memrealtime() - t0 > ticks) break;
+    __builtin_amdgcn_s_sleep(2);
+  }
+  __hip_atomic_store(&w[1], seen ? 1 : 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__global__ void probe_set_kernel(int* w) {
+  if (threadIdx.x == 0) __hip_atomic_store(&w[0], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+std::mutex g_park_mu;
+std::vector<hipStream_t> g_parked;  // streams that shared the default stream's queue
+int g_side_stats[2] = {0, 0};       // {probed streams, parked streams} (diagnostics)
+
+// 1: side runs concurrently with the default stream, 0: it does not, < 0: error
+int probe_concurrent(hipStream_t side, int* w) {
+  int h[2] = {0, 0};
+  HIP_TRY(hipMemsetAsync(w, 0, 2 * sizeof(int), nullptr));
+  HIP_TRY(hipStreamSynchronize(nullptr));
+  hipLaunchKernelGGL(probe_wait_kernel, dim3(1), dim3(64), 0, nullptr, w, kProbeTicks);
+  hipLaunchKernelGGL(probe_set_kernel, dim3(1), dim3(64), 0, side, w);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipStreamSynchronize(side));
+  HIP_TRY(hipStreamSynchronize(nullptr));
+  HIP_TRY(hipMemcpy(h, w, sizeof(h), hipMemcpyDeviceToHost));
+  return h[1] == 1 ? 1 : 0;
+}
+}  // namespace
+
+bool probe_enabled() {
+  const char* e = std::getenv("GELIM_SIDE_PROBE");  // 0: plain streams, no probe
+  return !(e && std::atoi(e) == 0);
+}
+
+// one probe word pair per device for the process (no hipFree: it would
+// synchronise the whole device under other threads' work); call under g_park_mu
+int probe_words(int** w) {
+  static int* words[64] = {};
+  int dev = 0;
+  HIP_TRY(hipGetDevice(&dev));
+  if (dev < 0 || dev >= 64) return GELIM_FAIL(GELIM_E_ARG, "side stream: device index");
+  if (!words[dev]) HIP_TRY(hipMalloc((void**)&words[dev], 2 * sizeof(int)));
+  *w = words[dev];
+  return GELIM_OK;
+}
+
+int side_stream_create(hipStream_t* out) {
+  *out = nullptr;
+  if (!probe_enabled()) {
+    HIP_TRY(hipStreamCreateWithFlags(out, hipStreamNonBlocking));
+    return GELIM_OK;
+  }
+  std::lock_guard<std::mutex> lk(g_park_mu);  // one probe at a time (shared words)
+  int* w = nullptr;
+  GELIM_TRY(probe_words(&w));
+  hipStream_t s = nullptr;
+  int rc = GELIM_OK;
+  for (int attempt = 0; attempt < 8; ++attempt) {
+    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) {
+      rc = GELIM_FAIL(GELIM_E_HIP, "side stream");
+      s = nullptr;
+      break;
+    }
+    const int ok = probe_concurrent(s, w);
+    ++g_side_stats[0];
+    if (ok != 0 || attempt == 7) break;  // concurrent, an error (keep the stream), or out of tries
+    ++g_side_stats[1];
+    g_parked.push_back(s);
+    s = nullptr;
+  }
+  *out = s;
+  return s ? GELIM_OK : rc;
+}
+
 }  // namespace gelim
+
+// A non-blocking stream that runs concurrently with the default stream
+// (probed; see side_stream_create).  Destroy with gelim_gpu_stream_destroy.
+extern "C" int gelim_gpu_side_stream_create(void** out) {
+  hipStream_t s = nullptr;
+  GELIM_TRY(gelim::side_stream_create(&s));
+  *out = (void*)s;
+  return GELIM_OK;
+}
+
+extern "C" int gelim_gpu_stream_destroy(void* s) {
+  if (s) HIP_TRY(hipStreamDestroy((hipStream_t)s));
+  return GELIM_OK;
+}
+
+// 1 when `stream` (an existing stream, e.g. one of torch's pool) runs
+// concurrently with the default stream, 0 when it shares its hardware queue
+// (always 1 with GELIM_SIDE_PROBE=0), < 0 on errors.
+extern "C" int gelim_gpu_stream_probe(void* stream) {
+  if (!gelim::probe_enabled()) return 1;
+  std::lock_guard<std::mutex> lk(gelim::g_park_mu);
+  int* w = nullptr;
+  GELIM_TRY(gelim::probe_words(&w));
+  const int ok = gelim::probe_concurrent((hipStream_t)stream, w);
+  if (ok >= 0) {
+    ++gelim::g_side_stats[0];
+    if (ok == 0) ++gelim::g_side_stats[1];
+  }
+  return ok;
+}
+
+// {streams probed, streams that shared the default stream's queue}
+extern "C" void gelim_gpu_side_stream_stats(int32_t* out) {
+  std::lock_guard<std::mutex> lk(gelim::g_park_mu);
+  out[0] = gelim::g_side_stats[0];
+  out[1] = gelim::g_side_stats[1];
+}
 
 extern "C" int gelim_gpu_device_count(void) {
   int n = 0;

@@ -17,6 +17,9 @@ int fail(int code, const char* file, int line, const std::string& msg);
 // nodes of captured graphs were the part of a graph that plan lifecycle
 // operations corrupted on ROCm 7.2 (profiles/graph_recapture.txt).
 int zero_async(void* p, size_t bytes, struct ihipStream_t* s);
+// A non-blocking stream probed to run concurrently with the default stream
+// (runtime.hip: streams sharing its hardware queue are parked, up to 8 tries).
+int side_stream_create(struct ihipStream_t** out);
 // Co-residency guard of the persistent (flag hand-off) kernels: true when
 // `grid` workgroups of a kernel that the occupancy API admits `per_cu` times
 // per CU all fit at once (one block of margin per CU above one, as the API

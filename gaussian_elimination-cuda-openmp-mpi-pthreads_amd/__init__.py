@@ -16,18 +16,6 @@ Layers: `_native` (ctypes over libgelim.so: C++17 + HIP), `ops` (tensor-level
 kernels), `models` (GaussSolver, MatMul), `parallel` (communicator,
 distributed solvers), `utils` (IO, timers, reports).  Import as `gelim`.
 """
-import os as _os
-
-# Hardware queues per process: HIP's default of 4 lets a plan's side stream
-# (the wide-panel engine's capped trailing GEMMs, the randomised engines'
-# lookahead) land on the SAME hardware queue as the caller's stream once a
-# process has created enough streams, and then the two serialise: the 8192
-# solve measured 49.4 vs 33.9 ms depending on the process's stream history,
-# 34.5 ms either way with 8 queues (profiles/hw_queues_r4.txt).  Effective
-# only if the HIP runtime is not initialised yet (set it in the environment
-# to override).
-_os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
-
 from . import _native  # noqa: F401,E402
 from . import utils  # noqa: F401,E402
 from . import ops  # noqa: F401,E402

@@ -71,7 +71,7 @@ import torch
 from .. import _native
 from ..ops import lu
 from ..utils.checkpoint import Checkpointer, maybe_inject_fault
-from ..utils.tensors import padded_ld, ptr, stream_handle
+from ..utils.tensors import padded_ld, ptr, side_stream, stream_handle
 from .comm import Communicator
 
 
@@ -163,7 +163,7 @@ class DistributedGauss:
             self._npd = -(-(nl * self._slot + self._nnet + 2) // 2)
             self._bufs = [torch.empty(self.n_pad * D + self._npd, dtype=torch.float64, device=self.device)
                           for _ in range(NBUF)]
-            self._side = torch.cuda.Stream(self.device)
+            self._side = side_stream(self.device)  # probed: never on the default stream's queue
             self._cap = int(lib.gelim_dist_side_cap(self.n_pad))
             self._tail_solver = None
             self._pairs = torch.zeros(nl * self._slot, dtype=torch.int32, device=self.device)

@@ -63,7 +63,7 @@ import numpy as np
 import torch
 
 from .. import _native
-from ..utils.tensors import ptr, stream_handle
+from ..utils.tensors import ptr, side_stream, stream_handle
 from .comm import Communicator
 
 NB = 128  # block width (= the single-GPU engine's)
@@ -151,7 +151,7 @@ class DistributedRBT:
         self._Ws = torch.zeros((NB, self.nloc), **f64)
         self._info = torch.full((1,), 0x7F7F7F7F, dtype=torch.int32, device=dev)
         if self.gpu:
-            self._side = torch.cuda.Stream(dev)
+            self._side = side_stream(dev)  # probed: never on the default stream's queue
         else:
             self._Wu = butterfly_dense(self._ud, self.np)
             Wv = butterfly_dense(self._vd, self.np)

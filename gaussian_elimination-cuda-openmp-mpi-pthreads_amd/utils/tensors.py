@@ -24,6 +24,43 @@ def stream_handle(device: torch.device | None = None) -> int | None:
     return torch.cuda.current_stream(device).cuda_stream
 
 
+def side_stream(device: torch.device) -> torch.cuda.Stream:
+    """A torch stream that runs BESIDE the default stream.  HIP shares
+    hardware queues between streams once a process has created
+    GPU_MAX_HW_QUEUES of them, and a lookahead stream on the default
+    stream's queue silently serialises behind it (the distributed 2048 solve
+    took 16 instead of 8 ms, profiles/hw_queues_r4.txt).  So torch's pool
+    streams are probed (runtime.hip gelim_gpu_stream_probe: a bounded wait on
+    the default stream for a flag the candidate sets) and the first one that
+    runs concurrently is returned -- a pool stream, so its lifetime is
+    torch's."""
+    from .. import _native
+
+    lib = _native.lib()
+    s = None
+    with torch.cuda.device(device):
+        for _ in range(33):  # torch's pool holds 32 streams per priority
+            s = torch.cuda.Stream(device)
+            rc = int(lib.gelim_gpu_stream_probe(s.cuda_stream))
+            if rc < 0:
+                _native.check(rc, "stream_probe")
+            if rc == 1:
+                break
+    return s
+
+
+def side_stream_stats() -> tuple[int, int]:
+    """(streams probed, streams found sharing the default stream's hardware
+    queue) in this process."""
+    from .. import _native
+
+    import ctypes
+
+    out = (ctypes.c_int32 * 2)()
+    _native.lib().gelim_gpu_side_stream_stats(out)
+    return int(out[0]), int(out[1])
+
+
 def is_gpu(t: torch.Tensor) -> bool:
     return t.device.type == "cuda"
 

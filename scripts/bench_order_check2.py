@@ -50,5 +50,16 @@ for sec in sys.argv[1:]:
         for k in keep:
             k.solve(gelim.random_system(64, seed=1, device=dev))
         torch.cuda.synchronize()
-t = bench.bench_single(comm, gelim, torch, 8192, seed=77)["time_s"]
-print(f"{' '.join(sys.argv[1:]) or '(none)'} -> single 8192 {t * 1e3:.2f} ms", flush=True)
+import os  # noqa: E402
+
+q = os.environ.get("GPU_MAX_HW_QUEUES")
+if os.environ.get("FINAL") == "t0":  # the dist 2048 panels (tail=0) solve, 4 fresh timings
+    ts = [bench.bench_dist_gauss(comm, gelim, torch, 2048, tail=0)["time_s"] * 1e3 for _ in range(4)]
+    print(f"Q={q} {' '.join(sys.argv[1:]) or '(none)'} -> dist 2048 tail=0 " + " ".join(f"{t:.2f}" for t in ts)
+          + " ms", flush=True)
+else:
+    t = bench.bench_single(comm, gelim, torch, 8192, seed=77)["time_s"]
+    print(f"Q={q} {' '.join(sys.argv[1:]) or '(none)'} -> single 8192 {t * 1e3:.2f} ms", flush=True)
+from gelim.utils.tensors import side_stream_stats  # noqa: E402
+
+print(f"   side streams probed / parked: {side_stream_stats()}", flush=True)

@@ -351,3 +351,109 @@ def test_big_solver_past_old_leaf_cap(gelim, cuda):
     assert ((x - ref).abs().max() / ref.abs().max()).item() < 1e-7
     del aug, ref
     torch.cuda.empty_cache()
+
+
+def _leaf_run(gelim, cuda, P, mode, monkeypatch, streamed):
+    from gelim import _native
+    from gelim.utils.tensors import ptr, stream_handle
+
+    if streamed:
+        monkeypatch.setenv("GELIM_LEAF_STREAM", "1")
+    else:
+        monkeypatch.delenv("GELIM_LEAF_STREAM", raising=False)
+    Pg = P.to(cuda)
+    m, ld = P.shape
+    ipiv = torch.full((32,), -7, dtype=torch.int32, device=cuda)
+    pairs = torch.full((1 + 4 * 32,), -7, dtype=torch.int32, device=cuda)
+    info = torch.zeros(4, dtype=torch.int32, device=cuda)
+    rc = _native.lib().gelim_gpu_leaf_factor(ptr(Pg), ld, m, 0, mode, ptr(ipiv), ptr(pairs), ptr(info),
+                                             stream_handle(cuda))
+    _native.check(rc, "leaf_factor")
+    torch.cuda.synchronize()
+    monkeypatch.delenv("GELIM_LEAF_STREAM", raising=False)
+    npairs = int(pairs[0].item())
+    return Pg.cpu(), ipiv.cpu(), pairs.cpu()[:1 + 2 * npairs], info.cpu()
+
+
+@pytest.mark.parametrize("m,kind,mode", [(32, "randn", 1), (1025, "randn", 1), (8192, "randn", 1),
+                                         (70000, "randn", 1), (5000, "ties", 1), (3000, "zeros", 0),
+                                         (2100, "zeros", 1), (600, "singular", 1)])
+def test_streamed_leaf_matches_register_leaf_bitwise(gelim, cuda, monkeypatch, m, kind, mode):
+    """The HBM-streamed leaf (leaf_stream.hip, the leaf of panels taller than
+    the register file holds) against the register-resident leaf on the same
+    panel: identical bits in the factors, ipiv, the net row movement and
+    info -- random panels, integer panels full of |a| ties across
+    workgroups, panels with exact zeros (the ZERO rule's position keys and
+    partial pivoting), and a panel with a zero column (info)."""
+    g = torch.Generator().manual_seed(m + mode)
+    ld = 34
+    if kind == "randn":
+        P = torch.randn(m, ld, generator=g, dtype=torch.float64)
+    elif kind == "ties":
+        P = torch.randint(-3, 4, (m, ld), generator=g).double()
+    else:
+        P = torch.randn(m, ld, generator=g, dtype=torch.float64)
+        P[torch.rand(m, ld, generator=g) < 0.5] = 0.0
+        if kind == "singular":
+            P[:, 5] = 0.0
+    reg = _leaf_run(gelim, cuda, P, mode, monkeypatch, streamed=False)
+    st = _leaf_run(gelim, cuda, P, mode, monkeypatch, streamed=True)
+    names = ("factors", "ipiv", "pairs", "info")
+    for name, a, b in zip(names, reg, st):
+        assert torch.equal(a, b), name
+    if kind == "singular":
+        assert reg[3][0].item() == 6
+
+
+def test_streamed_leaf_past_register_capacity(gelim, cuda):
+    """m = 300000 rows (> 262144, the register leaf's capacity; 82 MB):
+    LAPACK's getrf pivots, factors to rounding, the pair list reproduces its
+    row order."""
+    from gelim import _native
+
+    assert _native.lib().gelim_gpu_leaf_max_rows() >= 540000
+    m = 300000
+    g = torch.Generator().manual_seed(3)
+    P = torch.randn(m, 34, generator=g, dtype=torch.float64)
+    from gelim.utils.tensors import ptr, stream_handle
+
+    Pg = P.to(cuda)
+    ipiv = torch.zeros(32, dtype=torch.int32, device=cuda)
+    pairs = torch.zeros(1 + 4 * 32, dtype=torch.int32, device=cuda)
+    info = torch.zeros(4, dtype=torch.int32, device=cuda)
+    rc = _native.lib().gelim_gpu_leaf_factor(ptr(Pg), 34, m, 0, 1, ptr(ipiv), ptr(pairs), ptr(info),
+                                             stream_handle(cuda))
+    _native.check(rc, "leaf_factor")
+    torch.cuda.synchronize()
+    assert info.cpu()[:2].tolist() == [0, 0]
+    lu_, piv_ref = torch.linalg.lu_factor(P[:, :32])
+    assert torch.equal(ipiv.cpu().long() + 1, piv_ref.long())
+    out = Pg.cpu()
+    assert torch.allclose(out[:, :32], lu_, rtol=1e-10, atol=1e-10)
+    assert torch.equal(out[:, 32:], P[:, 32:])
+    pr = pairs.cpu().tolist()
+    moved = {pr[1 + 2 * e]: pr[2 + 2 * e] for e in range(pr[0])}
+    perm = list(range(m))
+    for j, pj in enumerate(piv_ref.tolist()):
+        perm[j], perm[pj - 1] = perm[pj - 1], perm[j]
+    assert all(moved.get(d, d) == perm[d] for d in set(moved) | set(range(64)))
+    del Pg, out
+    torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("pivot", ["partial", "zero"])
+def test_streamed_leaf_inside_wide_panel_solve(gelim, cuda, monkeypatch, pivot):
+    """The whole wide-panel solve with every leaf streamed (GELIM_LEAF_STREAM=1)
+    gives the same bits as with the register leaves."""
+    n = 3000
+    aug = gelim.random_system(n, seed=8, device=cuda) if pivot == "partial" else gelim.synthetic_system(
+        n, device=cuda)
+    monkeypatch.delenv("GELIM_LEAF_STREAM", raising=False)
+    s = gelim.GaussSolver(n, backend="hip", pivot=pivot, device=cuda)
+    x0 = s.solve(aug.clone()).cpu()
+    s.close()
+    monkeypatch.setenv("GELIM_LEAF_STREAM", "1")
+    s = gelim.GaussSolver(n, backend="hip", pivot=pivot, device=cuda)
+    x1 = s.solve(aug.clone()).cpu()
+    s.close()
+    assert torch.equal(x0, x1)

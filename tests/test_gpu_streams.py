@@ -1,0 +1,51 @@
+"""Lookahead side streams and the hardware queues behind them (runtime.hip
+side_stream_create / gelim_gpu_stream_probe, utils/tensors.py side_stream):
+a side stream must run concurrently with the default stream, and the probe
+must tell a stream that shares the default stream's queue from one that
+does not (profiles/hw_queues_r4.txt)."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def test_probe_detects_a_shared_queue(gelim, cuda):
+    """The default stream probed against itself is the shared-queue case
+    (the waiting kernel times out before the flag is set): 0."""
+    from gelim import _native
+
+    with torch.cuda.device(cuda):
+        assert _native.lib().gelim_gpu_stream_probe(torch.cuda.default_stream(cuda).cuda_stream) == 0
+
+
+def test_side_stream_runs_beside_default(gelim, cuda):
+    from gelim import _native
+    from gelim.utils.tensors import side_stream, side_stream_stats
+
+    before = side_stream_stats()
+    s = side_stream(cuda)
+    assert s.cuda_stream != torch.cuda.default_stream(cuda).cuda_stream
+    with torch.cuda.device(cuda):
+        assert _native.lib().gelim_gpu_stream_probe(s.cuda_stream) == 1
+    after = side_stream_stats()
+    assert after[0] >= before[0] + 2
+    # work on it is ordinary stream work
+    with torch.cuda.stream(s):
+        x = torch.arange(1000, dtype=torch.float64, device=cuda).mul_(2)
+    s.synchronize()
+    assert x.sum().item() == 999000.0
+
+
+def test_unprobed_side_streams_still_solve(gelim, cuda, monkeypatch):
+    """GELIM_SIDE_PROBE=0 (plain streams): the plans' lookahead schedules
+    give the same bits, only the concurrency guarantee is gone."""
+    n = 3000
+    aug = gelim.random_system(n, seed=12, device=cuda)
+    s = gelim.GaussSolver(n, backend="hip", device=cuda)
+    x0 = s.solve(aug.clone()).cpu()
+    s.close()
+    monkeypatch.setenv("GELIM_SIDE_PROBE", "0")
+    s = gelim.GaussSolver(n, backend="hip", device=cuda)
+    x1 = s.solve(aug.clone()).cpu()
+    s.close()
+    assert torch.equal(x0, x1)

@@ -1153,6 +1153,33 @@ extern "C" int gelim_rbt_block_inverse(const double* Ablk, int64_t lda, int64_t 
   return gelim::block_inv(Ablk, lda, col, Dinv, info, (hipStream_t)stream);
 }
 
+// x = T^-1 rhs for the block-unit-lower (upper = 0; ysave, may be null,
+// gets y_b = rhs_b - sum_{j<b} F_bj x_j) or the block-upper (upper = 1) part
+// of an (nblk * 128)-square block-LDU factor F (leading dimension ldf) whose
+// diagonal blocks' inverses are Dinv (nblk x 128 x 128): the persistent block
+// solve of the randomised engine above (blk_trsv_kernel, one workgroup per
+// block row, chain order = dispatch order, so no co-residency is needed).
+// The distributed engine's super-block solves (parallel/dist_rbt.py) use it.
+// err: a device int, 3 on a hand-off timeout (left as is otherwise).
+extern "C" int gelim_rbt_block_solve(const double* F, int64_t ldf, const double* Dinv, int nblk, const double* rhs,
+                                     double* x, double* ysave, int upper, int* err, void* stream) {
+  using namespace gelim;
+  if (!F || !Dinv || !rhs || !x || !err || nblk < 1 || nblk > kMaxBlocks || ldf < (int64_t)nblk * NB || x == rhs)
+    return GELIM_FAIL(GELIM_E_ARG, "rbt_block_solve: bad argument");
+  hipStream_t s = (hipStream_t)stream;
+  const int n = nblk * NB;
+  hipLaunchKernelGGL(fill_sentinel_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s,
+                     reinterpret_cast<unsigned long long*>(x), n);
+  if (upper)
+    hipLaunchKernelGGL((blk_trsv_kernel<double, true>), dim3((unsigned)nblk), dim3(kDT), 0, s, F, ldf, Dinv, rhs, x,
+                       (double*)nullptr, nblk, err, (unsigned long long*)nullptr, 0);
+  else
+    hipLaunchKernelGGL((blk_trsv_kernel<double, false>), dim3((unsigned)nblk), dim3(kDT), 0, s, F, ldf, Dinv, rhs, x,
+                       ysave, nblk, err, (unsigned long long*)nullptr, 0);
+  HIP_TRY(hipGetLastError());
+  return GELIM_OK;
+}
+
 // out = U^T [b; 0] (transpose = 1) or out = V y (transpose = 0) for the
 // butterfly with diagonals d (8 x np/4, device), b / y of n entries (stride
 // incb), out of nout entries -- replicated vectors of the distributed solve.

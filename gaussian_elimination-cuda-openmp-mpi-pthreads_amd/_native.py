@@ -89,6 +89,7 @@ _PROTOS = {
     "gelim_rbt_vec": (_int, [_vp, _i64, _i64, _i64, _vp, _int, _vp, _i64, _vp]),
     "gelim_drbt_transform": (_int, [_vp, _i64, _vp, _i64, _i64, _i64, _int, _int, _vp, _vp, _vp]),
     "gelim_drbt_super_solve": (_int, [_vp, _i64, _vp, _int, _vp, _vp, _vp, _int, _vp]),
+    "gelim_rbt_block_solve": (_int, [_vp, _i64, _vp, _int, _vp, _vp, _vp, _int, _vp, _vp]),
     "gelim_drbt_gemv": (_int, [_vp, _i64, _i64, _i64, _vp, _vp, _dbl, _vp]),
     "gelim_drbt_matvec_abs": (_int, [_vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp]),
     "gelim_gpu_dgemm_thin": (_int, [_vp, _i64, _vp, _i64, _vp, _i64, _i64, _i64, _i64, _dbl, _int, _int, _vp]),

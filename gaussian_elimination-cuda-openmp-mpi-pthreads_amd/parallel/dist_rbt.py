@@ -151,6 +151,7 @@ class DistributedRBT:
         self._Ws = torch.zeros((NB, self.nloc), **f64)
         self._info = torch.full((1,), 0x7F7F7F7F, dtype=torch.int32, device=dev)
         if self.gpu:
+            self._serr = torch.zeros(1, dtype=torch.int32, device=dev)  # block solves: hand-off timeout word
             self._side = side_stream(dev)  # probed: never on the default stream's queue
         else:
             self._Wu = butterfly_dense(self._ud, self.np)
@@ -387,9 +388,13 @@ class DistributedRBT:
                      upper: bool) -> None:
         P = self.P
         if self.gpu:
-            _native.check(_native.lib().gelim_drbt_super_solve(ptr(self._Fs[s]), NB * P, ptr(self._Ds[s]), P,
-                                                               ptr(rhs), ptr(x), ptr(ysave), int(upper), self._sh()),
-                          "drbt_super_solve")
+            # the single-GPU engine's persistent block solve (one workgroup per
+            # 128-row block, hand-offs through sentinel-filled x): 12 us at
+            # P = 8 against 190 us for the one-workgroup super_solve kernel
+            # (profiles/dist_rbt_8rank_critical_path.md)
+            _native.check(_native.lib().gelim_rbt_block_solve(ptr(self._Fs[s]), NB * P, ptr(self._Ds[s]), P, ptr(rhs),
+                                                              ptr(x), ptr(ysave), int(upper), ptr(self._serr),
+                                                              self._sh()), "rbt_block_solve")
             return
         F, D = self._Fs[s], self._Ds[s]
         order = reversed(range(P)) if upper else range(P)
@@ -449,6 +454,9 @@ class DistributedRBT:
                 self._gemv(self.M[:s * S, s * NB:(s + 1) * NB], xb, acc[:s * S])
         out = torch.empty_like(c)
         self._rbt_vec(xs, self.vd if self.gpu else None, False, out)
+        if self.gpu and int(self._serr.item()) != 0:
+            self._serr.zero_()
+            raise _native.GelimError("distributed RBT: block-solve hand-off timed out")
         return out
 
     def _residual(self, loc: torch.Tensor, x: torch.Tensor) -> tuple[torch.Tensor, float]:

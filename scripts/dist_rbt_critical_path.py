@@ -1,86 +1,81 @@
-"""Critical-path estimate of the distributed randomised solver
-(parallel/dist_rbt.py) at P ranks, from a one-rank kernel trace of its
-distributed schedule (scripts/dist_rbt_prof.py under rocprofv3
---kernel-trace; one rank owns every block, so its main stream runs the whole
-chain and its side stream all trailing updates).
+"""Critical-path model of the distributed randomised solver
+(parallel/dist_rbt.py) at P ranks, from measured one-GPU kernel times
+(scripts/dist_rbt_prof.py --micro, profiles/dgemm_thin_r4.txt) and an RCCL
+model bcast(bytes) = latency + bytes / bandwidth.
 
-Per block k the owner of k+1 (main stream) needs panel k -- the column
-broadcast X_k and the inverse broadcast D_k -- and then updates block k+1 and
-ships it.  D_k leaves after the inverse, X_k before it, so
+Factorisation, per 128-column block k (m = rows below block k):
+  the owner of block k+1 (main stream), once panel k has arrived:
+    W = Dinv_k A[k, k+1]  +  column update of block k+1  +  pack of column k+1
+  then the column broadcast X_{k+1} leaves, the inverse of block k+1 runs
+  under it, and its 128 x 128 broadcast D_{k+1} follows:
+    chain_k = t_W + t_upd(m) + t_pack(m) + max(bcast(X), t_inv + bcast(D))
+  every rank's side stream applies panel k to its own columns (~1/P of the
+  trailing update); a block costs max(chain_k, side_k).
+Solves (per apply): ns = np / (128 P) super-blocks per direction, each one
+all_reduce (latency + S doubles) + the persistent block solve of P blocks +
+one local GEMV; refinement = 1 + corrections applies, each followed by a
+residual (local |A||x| mat-vec + an all_reduce of 2 np doubles).
+Setup: the butterfly transform (local) and the all_gather of the super-blocks
+(np x 128 P doubles) and of the inverses (np x 128).
 
-  chain_k = max(bcast(X_k), inv_k + bcast(D_k)) + [W + column update of k+1 + pack]
-
-with the kernel times measured here and an RCCL broadcast model
-bcast(bytes) = latency + bytes / bandwidth.  Every rank's side stream applies
-panel k to ITS columns, ~1/P of the one-rank side work per block; a block
-costs max(chain_k, side_k / P).  Solves: per direction np / (128 P)
-super-blocks of one all_reduce (latency) + a super-block solve + a GEMV.
-
-  python scripts/dist_rbt_critical_path.py gpurun_out/drbt/run_results.db 8192
+  python scripts/dist_rbt_critical_path.py [n]
 """
-import sqlite3
 import sys
 
+# measured on one MI355X (us); profiles/dist_rbt_8rank_critical_path.md
+T_INV = 58.3                       # 128 x 128 Gauss-Jordan inverse (one workgroup)
+T_SS = {1: 8.3, 2: 12.1, 4: 19.2, 8: 34.4}   # persistent block solve of P blocks
+T_GEMV = 4.6                       # 8192 x 128 local GEMV
+T_PACK_8192 = 8.1                  # column pack, 8192 x 128 (8.4 MB)
+T_TRANSFORM_8192 = 120.0           # one-rank butterfly transform, 8192^2 (scales 1/P)
 
-def load(path: str):
-    con = sqlite3.connect(path)
-    return con.execute("select name, start, end, stream_id, grid_x from kernels order by start").fetchall()
+
+def t_gemm_thin(m: int) -> float:
+    """m x 128 x 128 fp64 GEMM (dgemm.hip LDS kernel): 9.5 us at m = 1024, 11.5
+    at 8064 (profiles/dgemm_thin_r4.txt)."""
+    return 9.5 + 2.0 * max(0, m - 1024) / 7040
+
+
+def model(n: int, P: int, lat: float, bw: float, corrections: int = 2) -> dict:
+    NB = 128
+    np_ = -(-n // (512 * P)) * 512 * P
+    nb = np_ // NB
+    us_per_byte = 1.0 / (bw * 1e3)    # GB/s -> bytes per us
+    chain = side = fac = 0.0
+    for k in range(nb - 1):
+        m = np_ - NB * (k + 1)
+        xb = m * NB * 8
+        c = t_gemm_thin(NB) + t_gemm_thin(m) + T_PACK_8192 * m / 8192 + 2.0 + max(
+            lat + xb * us_per_byte, T_INV + lat + NB * NB * 8 * us_per_byte)
+        # side: panel k on this rank's ~(np - 128 k) / P trailing columns: a W
+        # GEMM and an m x cols x 128 GEMM at ~40 TF/s
+        cols = (np_ - NB * (k + 1)) / P
+        s = 2 * t_gemm_thin(NB) + 2.0 * m * cols * NB / 40e6
+        chain += c
+        side += s
+        fac += max(c, s)
+    fac += T_INV
+    S = NB * P
+    ns = np_ // S
+    t_ss = T_SS.get(P, T_SS[8] * P / 8)
+    per_apply = 2 * ns * (lat + S * 8 * us_per_byte + t_ss + T_GEMV)
+    resid = lat + 2 * np_ * 8 * us_per_byte + 10.0
+    solves = (1 + corrections) * (per_apply + resid)
+    gather = (np_ * S * 8 + np_ * NB * 8) * us_per_byte * (P - 1) / P + 2 * lat
+    setup = T_TRANSFORM_8192 * (np_ / 8192) ** 2 / P + gather
+    return {"np": np_, "chain": chain, "side": side, "factor": fac, "solves": solves, "setup": setup,
+            "total": fac + solves + setup}
 
 
 def main():
-    path = sys.argv[1]
-    n = int(sys.argv[2]) if len(sys.argv) > 2 else 8192
-    ks = load(path)
-    inv = [k for k in ks if "diag_inv_kernel" in k[0]]
-    nb = n // 128
-    if len(inv) < nb:
-        raise SystemExit(f"only {len(inv)} inverse dispatches in the trace")
-    last = inv[-nb:]  # the last distributed-schedule solve
-    t0, t1 = last[0][1], last[-1][2]
-    # the solve's window: from its first inverse back to its transform, forward to the last kernel
-    win = [k for k in ks if k[1] >= t0 - 2_000_000 and k[2] <= t1 + 50_000_000]
-    main_stream = last[0][3]
-    inv_us = [(k[2] - k[1]) / 1e3 for k in last]
-    # per-block main-stream work between consecutive inverses (W, block update, packs)
-    chain_other = []
-    side_work = []
-    for i in range(nb - 1):
-        a, b = last[i][2], last[i + 1][1]
-        seg = [k for k in win if k[1] >= a and k[2] <= b + 1]
-        chain_other.append(sum((k[2] - k[1]) / 1e3 for k in seg if k[3] == main_stream))
-        side_work.append(sum((k[2] - k[1]) / 1e3 for k in seg if k[3] != main_stream))
-    chain_other.append(0.0)
-    side_work.append(0.0)
-    span_1rank = (win[-1][2] - win[0][1]) / 1e3
-    solve_k = [k for k in win if k[1] > t1]
-    ss = [(k[2] - k[1]) / 1e3 for k in solve_k if "super_solve" in k[0]]
-    gv = [(k[2] - k[1]) / 1e3 for k in solve_k if "gemv_acc" in k[0]]
-    mean = lambda v: sum(v) / len(v) if v else 0.0  # noqa: E731
-    print(f"# one-rank trace: {len(win)} kernels in the last schedule solve, span {span_1rank / 1e3:.2f} ms")
-    print(f"# inverse: mean {mean(inv_us):.1f} us, min {min(inv_us):.1f}, max {max(inv_us):.1f} (x{nb})")
-    print(f"# main-stream work between inverses (W, block update, packs): mean {mean(chain_other):.1f} us")
-    print(f"# side-stream work per block at one rank: mean {mean(side_work):.1f} us, total "
-          f"{sum(side_work) / 1e3:.2f} ms")
-    print(f"# super-block solve {mean(ss):.1f} us, gemv {mean(gv):.1f} us (one rank: S = 128)")
-    print()
-    print("P  bcast-lat(us) bcast-BW(GB/s)  chain(ms)  side-bound(ms)  factor(ms)  solves(ms)  total(ms)")
+    n = int(sys.argv[1]) if len(sys.argv) > 1 else 8192
+    print(f"# n = {n}; inverse {T_INV} us, block solves {T_SS} us, GEMV {T_GEMV} us, pack {T_PACK_8192} us/8.4 MB")
+    print("P  lat(us) BW(GB/s)  chain  side-bound  factor  solves  setup   total (ms)")
     for P in (2, 4, 8):
         for lat, bw in ((15.0, 100.0), (25.0, 50.0)):
-            chain = side = fac = 0.0
-            for k in range(nb):
-                xbytes = (n - 128 * k) * 128 * 8
-                bx = lat + xbytes / (bw * 1e3)  # us
-                bd = lat + 128 * 128 * 8 / (bw * 1e3)
-                c = max(bx, inv_us[k] + bd) + chain_other[k]
-                s = side_work[k] / P
-                chain += c
-                side += s
-                fac += max(c, s)
-            ns = n // (128 * P)
-            # forward + backward per apply, one apply + one correction typical
-            solves = 2 * 2 * ns * (lat + mean(ss) * P + mean(gv))
-            print(f"{P}  {lat:12.0f} {bw:14.0f} {chain / 1e3:10.2f} {side / 1e3:14.2f} {fac / 1e3:11.2f} "
-                  f"{solves / 1e3:11.2f} {(fac + solves) / 1e3:10.2f}")
+            r = model(n, P, lat, bw)
+            print(f"{P}  {lat:6.0f} {bw:8.0f} {r['chain'] / 1e3:7.2f} {r['side'] / 1e3:10.2f} {r['factor'] / 1e3:7.2f} "
+                  f"{r['solves'] / 1e3:7.2f} {r['setup'] / 1e3:6.2f} {r['total'] / 1e3:7.2f}")
 
 
 if __name__ == "__main__":

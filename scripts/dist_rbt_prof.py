@@ -55,7 +55,11 @@ def micro():
         x = torch.empty(S, dtype=torch.float64, device=dev)
         y = torch.empty(S, dtype=torch.float64, device=dev)
         t = timed(lambda: lib.gelim_drbt_super_solve(ptr(Fs), S, ptr(Ds), P, ptr(rhs), ptr(x), ptr(y), 0, sh))
-        print(f"super-block solve, P = {P} (S = {S}): {t:.1f} us", flush=True)
+        err = torch.zeros(1, dtype=torch.int32, device=dev)
+        t2 = timed(lambda: lib.gelim_rbt_block_solve(ptr(Fs), S, ptr(Ds), P, ptr(rhs), ptr(x), ptr(y), 0, ptr(err), sh))
+        t3 = timed(lambda: lib.gelim_rbt_block_solve(ptr(Fs), S, ptr(Ds), P, ptr(rhs), ptr(x), None, 1, ptr(err), sh))
+        print(f"super-block solve, P = {P} (S = {S}): one-workgroup kernel {t:.1f} us, persistent block solve "
+              f"lower {t2:.1f} / upper {t3:.1f} us (err {int(err.item())})", flush=True)
     A = torch.randn(8192, 130, dtype=torch.float64, device=dev, generator=g)[:, :128]
     xv = torch.randn(128, dtype=torch.float64, device=dev, generator=g)
     yv = torch.zeros(8192, dtype=torch.float64, device=dev)

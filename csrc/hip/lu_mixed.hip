@@ -306,6 +306,161 @@ __global__ __launch_bounds__(16 * NB / TR) void diag_inv_kernel(const T* __restr
   if (!fin) atomicMin(info, k0 + 1);
 }
 
+// ---- blocked Gauss-Jordan inverse on the matrix cores ------------------------
+// The same inverse, blocked: four block steps of 32 pivots.  The 128 x 128
+// block lives in LDS (133 KB of the CU's 160 KB); per block step b (rows /
+// columns kb = 32 b ..):
+//  1. wave 0 inverts the 32 x 32 pivot block in place by the unblocked
+//     Gauss-Jordan step above (the uniform rank-1 form; lane l holds row
+//     l / 2, half l % 2 of the columns; the pivot row goes through a
+//     wave-private LDS line, the pivot column through one DPP lane swap);
+//  2. the pivot rows: A[kb, j] = P^-1 A[kb, j] for j outside kb;
+//  3. every other row: A[i, j] -= A[i, kb] A[kb, j] (j outside kb) and
+//     A[i, kb] = -A[i, kb] P^-1 -- one GEMM with the pivot block columns of
+//     the right operand = P^-1 and of the start value = 0.
+// Steps 2 and 3 run on v_mfma_f64_16x16x4f64 (16 x 16 tiles, K = 32, every
+// wave one column tile of 6 row tiles in step 3), results held in registers
+// across a barrier, then stored (the GEMMs read what they overwrite).  The
+// 2.1 M FMAs of the inverse move from 128 barrier-separated VALU rank-1
+// steps to 8 MFMA phases + 128 single-wave steps on 32 x 32.
+constexpr int kBjLd = NB + 2;  // LDS row stride (doubles): 16 rows of an operand load hit distinct banks
+constexpr int kBjB = 32;       // pivot block
+constexpr int kBjThreads = 512;
+
+struct BjLds {
+  double a[NB * kBjLd];
+  double rowb[2][kBjB];
+};
+
+__device__ __forceinline__ double lane_swap1(double x) {  // the value of lane l ^ 1 (DPP quad_perm [1,0,3,2])
+  const unsigned lo = (unsigned)__builtin_amdgcn_mov_dpp((int)(unsigned)__double_as_longlong(x), 0xB1, 0xf, 0xf,
+                                                         false);
+  const unsigned hi = (unsigned)__builtin_amdgcn_mov_dpp(
+      (int)(unsigned)((uint64_t)__double_as_longlong(x) >> 32), 0xB1, 0xf, 0xf, false);
+  return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+
+// step 1: wave 0, the pivot block at (kb, kb) inverted in place
+__device__ __forceinline__ void bj_leaf(BjLds& sh, int kb, int lane) {
+  const int r = lane >> 1, ch = lane & 1;
+  double* prow = &sh.a[(kb + r) * kBjLd + kb + 16 * ch];
+  double p[16];
+#pragma unroll
+  for (int j = 0; j < 16; j += 2) {
+    const double2 v = *reinterpret_cast<const double2*>(prow + j);
+    p[j] = v.x;
+    p[j + 1] = v.y;
+  }
+#pragma unroll
+  for (int k = 0; k < kBjB; ++k) {
+    double* rb = sh.rowb[k & 1];
+    if (r == k) {
+#pragma unroll
+      for (int j = 0; j < 16; j += 2) *reinterpret_cast<double2*>(rb + 16 * ch + j) = make_double2(p[j], p[j + 1]);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // wave-private line: in-order LDS
+    double v[16];
+#pragma unroll
+    for (int j = 0; j < 16; j += 2) {
+      const double2 w = *reinterpret_cast<const double2*>(rb + 16 * ch + j);
+      v[j] = w.x;
+      v[j + 1] = w.y;
+    }
+    const double akk = rb[k];
+    const double own = p[k & 15];
+    const double oth = lane_swap1(own);
+    const double g = ((ch == (k >> 4)) ? own : oth) - (r == k ? 1.0 : 0.0);
+    const double pk = gj_recip(akk);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const double u = (16 * ch + j == k) ? 1.0 + pk : v[j] * pk;
+      p[j] = fma(-g, u, p[j]);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 16; j += 2) *reinterpret_cast<double2*>(prow + j) = make_double2(p[j], p[j + 1]);
+}
+
+// the c-th 16-column (or row) tile outside the pivot block kb
+__device__ __forceinline__ int bj_outside(int c, int kb) { return 16 * c < kb ? 16 * c : 16 * c + kBjB; }
+
+__global__ __launch_bounds__(kBjThreads) void bj_inv_kernel(const double* __restrict__ Ablk, int64_t lda, int k0,
+                                                            double* __restrict__ Dinv, int* __restrict__ info) {
+  __shared__ BjLds sh;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int m = lane & 15, q = lane >> 4;
+  {  // lanes along a row: coalesced
+    const int c = t & (NB - 1);
+#pragma unroll 8
+    for (int r = t >> 7; r < NB; r += kBjThreads / NB) sh.a[r * kBjLd + c] = Ablk[(int64_t)r * lda + c];
+  }
+  __syncthreads();
+  for (int kb = 0; kb < NB; kb += kBjB) {
+    if (wave == 0) bj_leaf(sh, kb, lane);
+    __syncthreads();
+    // step 2: 2 x 6 tiles of the pivot rows, waves 0..7 then 0..3
+    dev::d4 acc2[2];
+    int nt2 = 0;
+    for (int ti = wave; ti < 12; ti += 8, ++nt2) {
+      const int r0 = kb + 16 * (ti / 6), c0 = bj_outside(ti % 6, kb);
+      dev::d4 acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int kk = 0; kk < kBjB; kk += 4) {
+        const double av = sh.a[(r0 + m) * kBjLd + kb + kk + q];   // P^-1 (row r0 + m, col kb + k)
+        const double bv = sh.a[(kb + kk + q) * kBjLd + c0 + m];   // A[kb + k, c0 + n]
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
+      }
+      acc2[nt2] = acc;
+    }
+    __syncthreads();
+    nt2 = 0;
+    for (int ti = wave; ti < 12; ti += 8, ++nt2) {
+      const int r0 = kb + 16 * (ti / 6), c0 = bj_outside(ti % 6, kb);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) sh.a[(r0 + q + 4 * i) * kBjLd + c0 + m] = acc2[nt2][i];
+    }
+    __syncthreads();
+    // step 3: column tile `wave` of the 6 row tiles outside kb
+    const int c0 = 16 * wave;
+    const bool pcol = c0 >= kb && c0 < kb + kBjB;
+    dev::d4 acc3[6];
+#pragma unroll
+    for (int s = 0; s < 6; ++s) {
+      const int r0 = bj_outside(s, kb);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc3[s][i] = pcol ? 0.0 : sh.a[(r0 + q + 4 * i) * kBjLd + c0 + m];
+    }
+#pragma unroll
+    for (int kk = 0; kk < kBjB; kk += 4) {
+      const double bv = sh.a[(kb + kk + q) * kBjLd + c0 + m];
+#pragma unroll
+      for (int s = 0; s < 6; ++s) {
+        const double av = sh.a[(bj_outside(s, kb) + m) * kBjLd + kb + kk + q];
+        acc3[s] = __builtin_amdgcn_mfma_f64_16x16x4f64(-av, bv, acc3[s], 0, 0, 0);
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < 6; ++s) {
+      const int r0 = bj_outside(s, kb);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) sh.a[(r0 + q + 4 * i) * kBjLd + c0 + m] = acc3[s][i];
+    }
+    __syncthreads();
+  }
+  bool fin = true;
+  {
+    const int c = t & (NB - 1);
+#pragma unroll 8
+    for (int r = t >> 7; r < NB; r += kBjThreads / NB) {
+      const double v = sh.a[r * kBjLd + c];
+      fin = fin && isfinite(v);
+      Dinv[r * NB + c] = v;
+    }
+  }
+  if (!fin) atomicMin(info, k0 + 1);
+}
+
 // Launch of the diagonal inverse: GELIM_GJ_TR = 4 (default: 512 threads, two
 // waves per SIMD), 8 (256 threads) or 2 (1024 threads: 2048 1.52 ms, slower).  With the padded LDS chunks 4 x 8 tiles
 // are the faster shape (hip-rbt factor 2048 1.43 vs 1.52 ms, 4096 3.85 vs
@@ -315,6 +470,12 @@ __global__ __launch_bounds__(16 * NB / TR) void diag_inv_kernel(const T* __restr
 // The inverse of the NB x NB block at Ablk; `col` (its first global column)
 // only labels a non-finite result in info.
 int block_inv(const double* Ablk, int64_t lda, int64_t col, double* Di, int* info, hipStream_t s) {
+  const char* eb = std::getenv("GELIM_GJ_BLOCKED");  // 1: the blocked MFMA form (read per launch)
+  if (eb && std::atoi(eb) == 1) {
+    hipLaunchKernelGGL(bj_inv_kernel, dim3(1), dim3(kBjThreads), 0, s, Ablk, lda, (int)col, Di, info);
+    HIP_TRY(hipGetLastError());
+    return GELIM_OK;
+  }
   const char* e = std::getenv("GELIM_GJ_TR");  // read per launch (tests switch it)
   const int tr = e && (std::atoi(e) == 8 || std::atoi(e) == 2) ? std::atoi(e) : 4;
   if (tr == 2)

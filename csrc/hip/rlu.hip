@@ -49,8 +49,11 @@ namespace gelim {
 namespace rlu {
 namespace {
 
-constexpr int NT = 512;          // threads per workgroup: 8 wave64s, 2 per SIMD
-constexpr int kWaves = NT / 64;
+// Threads per workgroup NT (a template parameter): 512 = 8 wave64s, 2 per
+// SIMD (R <= 4 row slots), or 1024 = 16 wave64s (R <= 2: the n <= 2048
+// engine on the 2-slot register budget, 128 VGPRs, where 512 threads need 4
+// slots and spill).
+constexpr int kWavesMax = 16;
 constexpr int kW = 16;           // panel / strip width
 constexpr int kAuxSc1 = 16;      // buffer-op aux: sc1 (write-through store, L1-bypass load)
 constexpr unsigned long long kSpinTicks = 20000000ull;  // 200 ms at 100 MHz
@@ -78,12 +81,12 @@ struct Args {
 };
 
 struct alignas(16) Shared {
-  double cand[2][kWaves][18];  // each wave's winning row (16 values) + 1/pivot
-  u32x4 ckey[2][kWaves];       // {key hi, key lo, row, -}
+  double cand[2][kWavesMax][18];  // each wave's winning row (16 values) + 1/pivot
+  u32x4 ckey[2][kWavesMax];       // {key hi, key lo, row, -}
   double prow[kW][kW];         // this panel's pivot rows (engine) / L11 (updaters)
   double xs[kW][kW];           // TRSM right-hand sides (updaters)
   int sel[kW];                 // physical pivot row of each panel column
-  unsigned fb[kWaves];         // singular fallback: lowest live row per wave
+  unsigned fb[kWavesMax];         // singular fallback: lowest live row per wave
   int ok[2];                   // poll results (parity-buffered)
 };
 
@@ -314,8 +317,9 @@ __device__ __forceinline__ double recip(double p) {
 
 // ---- the engine: panel factorisation in registers ------------------------
 
-template <int R, int MODE>
+template <int NT, int R, int MODE>
 struct Engine {
+  static constexpr int kWaves = NT / 64;
   // One column J (compile time) of the panel whose first column is k0.
   template <int J>
   static __device__ __forceinline__ void col(double (&a)[R][kW], bool (&live)[R], int (&pos)[R], Shared& sh,
@@ -431,6 +435,7 @@ struct Engine {
     gm = max(gm, dpp<0x111>(0u, gm));
     gm = max(gm, dpp<0x112>(0u, gm));
     gm = max(gm, dpp<0x114>(0u, gm));
+    if constexpr (kWaves > 8) gm = max(gm, dpp<0x118>(0u, gm));
     const unsigned gh = (unsigned)__builtin_amdgcn_readlane((int)gm, kWaves - 1);
     int q = 0;
     unsigned p = 0;
@@ -526,7 +531,7 @@ struct Engine {
   }
 };
 
-template <int R, int MODE>
+template <int NT, int R, int MODE>
 __device__ __forceinline__ void engine(const Args& g, Shared& sh) {
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int vo = tvo<R>(t);  // this thread's voffset in the thread-major buffers
@@ -558,7 +563,8 @@ __device__ __forceinline__ void engine(const Args& g, Shared& sh) {
     unsigned pre = 1;
     if (more && t == 0) pre = __hip_atomic_load(&g.flags[np + j + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     unsigned long long* cs = (g.stamps != nullptr && j == 10) ? g.stamps + 8 * np + 2 * (np + 1) * np : nullptr;
-    Engine<R, MODE>::factor(a, live, pos, sh, t, lane, wave, w, k0, g.info, cs, std::make_integer_sequence<int, kW>{});
+    Engine<NT, R, MODE>::factor(a, live, pos, sh, t, lane, wave, w, k0, g.info, cs,
+                                std::make_integer_sequence<int, kW>{});
     if (more && t == 0) {
       int ok = 1;
       if (pre == 0) {  // not published yet: bounded poll
@@ -683,7 +689,7 @@ __device__ __forceinline__ void engine(const Args& g, Shared& sh) {
 
 // ---- updaters: one register-resident strip each --------------------------
 
-template <int R>
+template <int NT, int R>
 __device__ __forceinline__ void updater(const Args& g, Shared& sh, int s) {
   const int t = threadIdx.x, lane = t & 63;
   const int vo = tvo<R>(t);
@@ -785,25 +791,26 @@ __device__ __forceinline__ void updater(const Args& g, Shared& sh, int s) {
 // n <= 1536 / 2048 engines: np + 1 <= 129 workgroups, one per CU) get the
 // whole 256-VGPR budget -- with (NT, 2) the 4-slot engine spilled 137 VGPRs
 // to scratch (profiles/graph_recapture.txt: resident 2048 5.6 ms).
-template <int R, int MODE>
-__global__ __launch_bounds__(NT, R <= 2 ? 2 : 1) void rlu_kernel(Args g) {
+template <int NT, int R, int MODE>
+__global__ __launch_bounds__(NT, NT == 512 && R <= 2 ? 2 : 1) void rlu_kernel(Args g) {
   __shared__ Shared sh;
   if (blockIdx.x == 0)
-    engine<R, MODE>(g, sh);
+    engine<NT, R, MODE>(g, sh);
   else
-    updater<R>(g, sh, (int)blockIdx.x);
+    updater<NT, R>(g, sh, (int)blockIdx.x);
 }
 
 // Workspace of the resident LU for order n (bytes, 256-aligned pieces).
 struct Layout {
-  int R = 0, np = 0;
+  int NT = 0, R = 0, np = 0;
   size_t flags = 0, lbuf = 0, pbuf = 0, ubuf = 0, hbuf = 0, pslot = 0, total = 0;
 };
 
-Layout layout(int64_t n) {
+Layout layout(int64_t n, int NT) {
   Layout L;
-  L.R = n <= 512 ? 1 : n <= 1024 ? 2 : n <= 1536 ? 3 : n <= 2048 ? 4 : 0;
-  if (!L.R || n < 1) return Layout{};
+  if (n < 1 || n > 2048 || (NT != 512 && NT != 1024)) return Layout{};
+  L.NT = NT;
+  L.R = (int)((n + NT - 1) / NT);
   L.np = (int)((n + kW - 1) / kW);
   auto up = [](size_t b) { return (b + 255) & ~size_t(255); };
   const size_t panel = (size_t)L.R * 8 * NT * 16;
@@ -831,20 +838,32 @@ int64_t rlu_max_n() { return 2048; }
 
 // The np + 1 workgroups of the resident LU hand panels and strips to each
 // other through flags: they must all be resident at once.
+// Workgroup size of the resident LU for order n: 512 threads (1..4 register
+// slots) by default; GELIM_RLU_NT=1024 takes 1024 threads for n > 1024 (2
+// slots instead of 3-4; read per call).
+int rlu_threads(int64_t n) {
+  const char* e = std::getenv("GELIM_RLU_NT");
+  return (e && std::atoi(e) == 1024 && n > 1024) ? 1024 : 512;
+}
+
 bool rlu_coresident(int64_t n) {
   using namespace rlu;
-  const Layout L = layout(n);
+  const Layout L = layout(n, rlu_threads(n));
   if (!L.R) return false;
   int per = 0;
   hipError_t e = hipSuccess;
-  if (L.R == 1) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, rlu_kernel<1, 1>, NT, 0);
-  else if (L.R == 2) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, rlu_kernel<2, 1>, NT, 0);
-  else if (L.R == 3) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, rlu_kernel<3, 1>, NT, 0);
-  else e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, rlu_kernel<4, 1>, NT, 0);
+  if (L.NT == 1024) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, rlu_kernel<1024, 2, 1>, 1024, 0);
+  else if (L.R == 1) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, rlu_kernel<512, 1, 1>, 512, 0);
+  else if (L.R == 2) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, rlu_kernel<512, 2, 1>, 512, 0);
+  else if (L.R == 3) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, rlu_kernel<512, 3, 1>, 512, 0);
+  else e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, rlu_kernel<512, 4, 1>, 512, 0);
   return e == hipSuccess && coresident(per, L.np + 1);
 }
 
-size_t rlu_workspace_bytes(int64_t n) { return rlu::layout(n).total; }
+size_t rlu_workspace_bytes(int64_t n) {
+  // the larger of the two shapes, so a plan's workspace fits either
+  return std::max(rlu::layout(n, 512).total, rlu::layout(n, 1024).total);
+}
 
 // Factor the augmented system src (n x (n+1), ld lds; NULL = work already
 // holds it) into work (U rows at their physical positions, y in column n),
@@ -853,7 +872,7 @@ size_t rlu_workspace_bytes(int64_t n) { return rlu::layout(n).total; }
 int rlu_factor(const double* src, int64_t lds, double* work, int64_t ldw, int64_t n, int mode,
                int* piv, int* info, void* ws, hipStream_t s, unsigned long long* stamps) {
   using namespace rlu;
-  const Layout L = layout(n);
+  const Layout L = layout(n, rlu_threads(n));
   if (!L.R) return GELIM_FAIL(GELIM_E_ARG, "rlu: n out of range (1..2048)");
   char* base = static_cast<char*>(ws);
   Args a{};
@@ -877,20 +896,23 @@ int rlu_factor(const double* src, int64_t lds, double* work, int64_t ldw, int64_
   }
   a.stamps = stamps;
   GELIM_TRY(zero_async(a.flags, L.lbuf - L.flags, s));
-  const dim3 grid((unsigned)(L.np + 1)), block(NT);
+  const dim3 grid((unsigned)(L.np + 1)), block((unsigned)L.NT);
   const bool part = mode == GELIM_PIVOT_PARTIAL;
-  if (L.R == 1) {
-    if (part) hipLaunchKernelGGL((rlu_kernel<1, 1>), grid, block, 0, s, a);
-    else hipLaunchKernelGGL((rlu_kernel<1, 0>), grid, block, 0, s, a);
+  if (L.NT == 1024) {
+    if (part) hipLaunchKernelGGL((rlu_kernel<1024, 2, 1>), grid, block, 0, s, a);
+    else hipLaunchKernelGGL((rlu_kernel<1024, 2, 0>), grid, block, 0, s, a);
+  } else if (L.R == 1) {
+    if (part) hipLaunchKernelGGL((rlu_kernel<512, 1, 1>), grid, block, 0, s, a);
+    else hipLaunchKernelGGL((rlu_kernel<512, 1, 0>), grid, block, 0, s, a);
   } else if (L.R == 2) {
-    if (part) hipLaunchKernelGGL((rlu_kernel<2, 1>), grid, block, 0, s, a);
-    else hipLaunchKernelGGL((rlu_kernel<2, 0>), grid, block, 0, s, a);
+    if (part) hipLaunchKernelGGL((rlu_kernel<512, 2, 1>), grid, block, 0, s, a);
+    else hipLaunchKernelGGL((rlu_kernel<512, 2, 0>), grid, block, 0, s, a);
   } else if (L.R == 3) {
-    if (part) hipLaunchKernelGGL((rlu_kernel<3, 1>), grid, block, 0, s, a);
-    else hipLaunchKernelGGL((rlu_kernel<3, 0>), grid, block, 0, s, a);
+    if (part) hipLaunchKernelGGL((rlu_kernel<512, 3, 1>), grid, block, 0, s, a);
+    else hipLaunchKernelGGL((rlu_kernel<512, 3, 0>), grid, block, 0, s, a);
   } else {
-    if (part) hipLaunchKernelGGL((rlu_kernel<4, 1>), grid, block, 0, s, a);
-    else hipLaunchKernelGGL((rlu_kernel<4, 0>), grid, block, 0, s, a);
+    if (part) hipLaunchKernelGGL((rlu_kernel<512, 4, 1>), grid, block, 0, s, a);
+    else hipLaunchKernelGGL((rlu_kernel<512, 4, 0>), grid, block, 0, s, a);
   }
   HIP_TRY(hipGetLastError());
   return GELIM_OK;

@@ -91,16 +91,21 @@ def test_mixed_singular_raises(gelim, cuda):
     assert s.last_fallback is not None
 
 
-@pytest.mark.parametrize("tr", ["2", "4", "8"])
+@pytest.mark.parametrize("tr", ["2", "4", "8", "blocked"])
 @pytest.mark.parametrize("backend", ["hip-mixed", "hip-rbt"])
 @pytest.mark.parametrize("n", [130, 1000])
 def test_diag_inverses_and_factor(gelim, cuda, backend, n, tr, monkeypatch):
     """Every stored diagonal-block inverse (Gauss-Jordan, fp64; 2 x 8, 4 x 8
-    or 8 x 8 tiles on 1024 / 512 / 256 threads, GELIM_GJ_TR) inverts the Schur diagonal
-    block the block-LDU factor left in place; fp64 oracle."""
+    or 8 x 8 tiles on 1024 / 512 / 256 threads, GELIM_GJ_TR, or the blocked
+    MFMA form, GELIM_GJ_BLOCKED=1) inverts the Schur diagonal block the
+    block-LDU factor left in place; fp64 oracle."""
     import ctypes
 
-    monkeypatch.setenv("GELIM_GJ_TR", tr)
+    if tr == "blocked":
+        monkeypatch.setenv("GELIM_GJ_BLOCKED", "1")
+    else:
+        monkeypatch.setenv("GELIM_GJ_BLOCKED", "0")
+        monkeypatch.setenv("GELIM_GJ_TR", tr)
 
     aug = gelim.random_system(n, seed=3, device=cuda)
     s = gelim.GaussSolver(n, backend=backend, device=cuda)
@@ -233,4 +238,64 @@ def test_not_coresident_falls_back(gelim, cuda, backend, monkeypatch):
     assert s.last_fallback is not None
     ref = torch.linalg.solve(aug[:, :n], aug[:, n])
     assert ((x - ref).abs().max() / ref.abs().max()).item() < 1e-9
+    s.close()
+
+
+@pytest.mark.parametrize("kind", ["dominant", "randn", "rbt_like"])
+def test_block_inverse_forms_match_torch(gelim, cuda, monkeypatch, kind):
+    """gelim_rbt_block_inverse, unblocked (one barrier per pivot) and blocked
+    (32-pivot blocks, MFMA updates), against torch.linalg.inv in fp64, on a
+    strided 128 x 128 block; a zero pivot block is reported through info."""
+    from gelim.utils.tensors import ptr, stream_handle
+
+    lib = gelim._native.lib()
+    g = torch.Generator(device="cpu").manual_seed(len(kind))
+    A = torch.randn(128, 128, generator=g, dtype=torch.float64)
+    if kind == "dominant":
+        A += 64 * torch.eye(128, dtype=torch.float64)
+    elif kind == "rbt_like":  # a Schur block after a butterfly: no small leading minors by construction
+        Q, _ = torch.linalg.qr(torch.randn(128, 128, generator=g, dtype=torch.float64))
+        A = Q @ torch.diag(torch.logspace(0, 4, 128, dtype=torch.float64)) @ Q.T + 0.1 * A
+    ref = torch.linalg.inv(A)
+    big = torch.zeros(200, 134, dtype=torch.float64)
+    big[30:158, 4:132] = A
+    bg = big.to(cuda)
+    outs = {}
+    for blocked in ("0", "1"):
+        monkeypatch.setenv("GELIM_GJ_BLOCKED", blocked)
+        D = torch.full((128, 128), float("nan"), dtype=torch.float64, device=cuda)
+        info = torch.full((1,), 0x7F7F7F7F, dtype=torch.int32, device=cuda)
+        blk = bg[30:158, 4:132]
+        gelim._native.check(lib.gelim_rbt_block_inverse(ptr(blk), bg.stride(0), 256, ptr(D), ptr(info),
+                                                        stream_handle(cuda)), "block_inverse")
+        torch.cuda.synchronize()
+        assert info.item() == 0x7F7F7F7F
+        outs[blocked] = D.cpu()
+        resid = (D.cpu() @ A - torch.eye(128, dtype=torch.float64)).abs().max().item()
+        cond = torch.linalg.cond(A).item()
+        assert resid < 64 * cond * 2.2e-16, (blocked, resid, cond)
+        assert ((D.cpu() - ref).abs().max() / ref.abs().max()).item() < 64 * cond * 2.2e-16
+    assert torch.equal(bg.cpu(), big.to(torch.float64))  # the block is read, not written
+    # a singular pivot block: info = 1 + the block's first column
+    monkeypatch.setenv("GELIM_GJ_BLOCKED", "1")
+    Z = torch.zeros(128, 128, dtype=torch.float64, device=cuda)
+    D = torch.empty(128, 128, dtype=torch.float64, device=cuda)
+    info = torch.full((1,), 0x7F7F7F7F, dtype=torch.int32, device=cuda)
+    gelim._native.check(lib.gelim_rbt_block_inverse(ptr(Z), 128, 384, ptr(D), ptr(info), stream_handle(cuda)),
+                        "block_inverse")
+    torch.cuda.synchronize()
+    assert info.item() == 385
+
+
+@pytest.mark.parametrize("n", [1000, 2048, 4200, 8192])
+def test_rbt_with_blocked_inverse(gelim, cuda, monkeypatch, n):
+    """The whole hip-rbt solve on the blocked MFMA inverse: no fallback, the
+    fp64 error class, at most as many corrections as a few."""
+    monkeypatch.setenv("GELIM_GJ_BLOCKED", "1")
+    aug = gelim.random_system(n, seed=n + 5, device=cuda)
+    s = gelim.GaussSolver(n, backend="hip-rbt", device=cuda)
+    x = s.solve(aug, check=True)
+    assert s.last_fallback is None, s.last_fallback
+    assert s.last_steps <= 4
+    assert gelim.ops.gauss.error_metric(x) < 1e-8
     s.close()

@@ -1,4 +1,5 @@
 #!/usr/bin/env bash
+# (GELIM_DGEMM_STAGGER was removed after this A/B: profiles/dgemm_r3_lds.txt has the result)
 # dgemm change check: its numerics tests, then the f64 GEMM shapes and the
 # solvers that use it under each C schedule (GELIM_DGEMM_STAGGER)
 set -u

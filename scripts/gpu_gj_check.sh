@@ -1,4 +1,5 @@
 #!/usr/bin/env bash
+# (GELIM_GJ_SCALED was removed after this A/B: profiles/rbt_engine_round3.txt has the result)
 # Gauss-Jordan diagonal-inverse change check: the randomised engines' tests,
 # the hip-rbt breakdown, one PMC pass over the factor kernels
 set -u

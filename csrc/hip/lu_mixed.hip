@@ -307,7 +307,7 @@ __global__ __launch_bounds__(16 * NB / TR) void diag_inv_kernel(const T* __restr
 }
 
 // ---- blocked Gauss-Jordan inverse on the matrix cores ------------------------
-// The same inverse, blocked: four block steps of 32 pivots.  The 128 x 128
+// The same inverse, blocked: block steps of KB = 32 (or 16) pivots.  The 128 x 128
 // block lives in LDS (133 KB of the CU's 160 KB); per block step b (rows /
 // columns kb = 32 b ..):
 //  1. wave 0 inverts the 32 x 32 pivot block in place by the unblocked
@@ -324,68 +324,95 @@ __global__ __launch_bounds__(16 * NB / TR) void diag_inv_kernel(const T* __restr
 // 2.1 M FMAs of the inverse move from 128 barrier-separated VALU rank-1
 // steps to 8 MFMA phases + 128 single-wave steps on 32 x 32.
 constexpr int kBjLd = NB + 2;  // LDS row stride (doubles): 16 rows of an operand load hit distinct banks
-constexpr int kBjB = 32;       // pivot block
 constexpr int kBjThreads = 512;
 
 struct BjLds {
   double a[NB * kBjLd];
-  double rowb[2][kBjB];
+  double rowb[2][32];
 };
 
-__device__ __forceinline__ double lane_swap1(double x) {  // the value of lane l ^ 1 (DPP quad_perm [1,0,3,2])
-  const unsigned lo = (unsigned)__builtin_amdgcn_mov_dpp((int)(unsigned)__double_as_longlong(x), 0xB1, 0xf, 0xf,
+template <int CTRL>
+__device__ __forceinline__ double mov_dpp_f64(double x) {
+  const unsigned lo = (unsigned)__builtin_amdgcn_mov_dpp((int)(unsigned)__double_as_longlong(x), CTRL, 0xf, 0xf,
                                                          false);
   const unsigned hi = (unsigned)__builtin_amdgcn_mov_dpp(
-      (int)(unsigned)((uint64_t)__double_as_longlong(x) >> 32), 0xB1, 0xf, 0xf, false);
+      (int)(unsigned)((uint64_t)__double_as_longlong(x) >> 32), CTRL, 0xf, 0xf, false);
   return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
 }
 
-// step 1: wave 0, the pivot block at (kb, kb) inverted in place
-__device__ __forceinline__ void bj_leaf(BjLds& sh, int kb, int lane) {
-  const int r = lane >> 1, ch = lane & 1;
-  double* prow = &sh.a[(kb + r) * kBjLd + kb + 16 * ch];
-  double p[16];
+// step 1: wave 0 inverts the KB x KB pivot block at (kb, kb) in place.  Lane
+// l holds row l / LPR, columns VPL (l % LPR) .. of it (LPR = 64 / KB lanes per
+// row, VPL = KB / LPR values each): the pivot row goes through a
+// wave-private LDS line, the pivot column's entry of a row through one DPP
+// move inside the row's lane group.  Step K (compile time) of it:
+template <int KB, int K>
+__device__ __forceinline__ void bj_leaf_step(BjLds& sh, double (&p)[KB * KB / 64], int r, int cg) {
+  constexpr int LPR = 64 / KB, VPL = KB / LPR;
+  double* rb = sh.rowb[K & 1];
+  if (r == K) {
 #pragma unroll
-  for (int j = 0; j < 16; j += 2) {
+    for (int j = 0; j < VPL; j += 2) *reinterpret_cast<double2*>(rb + VPL * cg + j) = make_double2(p[j], p[j + 1]);
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // wave-private line: in-order LDS
+  double v[VPL];
+#pragma unroll
+  for (int j = 0; j < VPL; j += 2) {
+    const double2 w = *reinterpret_cast<const double2*>(rb + VPL * cg + j);
+    v[j] = w.x;
+    v[j + 1] = w.y;
+  }
+  const double akk = rb[K];
+  // my row's entry in column K: lane-group member K / VPL, register K % VPL
+  double gk;
+  if constexpr (LPR == 2) {
+    const double own = p[K % VPL];
+    const double oth = mov_dpp_f64<0xB1>(own);  // quad_perm [1,0,3,2]: the other lane of the pair
+    gk = (cg == K / VPL) ? own : oth;
+  } else {  // LPR == 4: the quad is the row's lane group
+    constexpr int src = K / VPL;
+    gk = mov_dpp_f64<src | (src << 2) | (src << 4) | (src << 6)>(p[K % VPL]);
+  }
+  const double g = gk - (r == K ? 1.0 : 0.0);
+  const double pk = gj_recip(akk);
+#pragma unroll
+  for (int j = 0; j < VPL; ++j) {
+    const double u = (VPL * cg + j == K) ? 1.0 + pk : v[j] * pk;
+    p[j] = fma(-g, u, p[j]);
+  }
+}
+
+template <int KB, int... K>
+__device__ __forceinline__ void bj_leaf_steps(BjLds& sh, double (&p)[KB * KB / 64], int r, int cg,
+                                              std::integer_sequence<int, K...>) {
+  (bj_leaf_step<KB, K>(sh, p, r, cg), ...);
+}
+
+template <int KB>
+__device__ __forceinline__ void bj_leaf(BjLds& sh, int kb, int lane) {
+  constexpr int LPR = 64 / KB, VPL = KB / LPR;
+  const int r = lane / LPR, cg = lane % LPR;
+  double* prow = &sh.a[(kb + r) * kBjLd + kb + VPL * cg];
+  double p[VPL];
+#pragma unroll
+  for (int j = 0; j < VPL; j += 2) {
     const double2 v = *reinterpret_cast<const double2*>(prow + j);
     p[j] = v.x;
     p[j + 1] = v.y;
   }
+  bj_leaf_steps<KB>(sh, p, r, cg, std::make_integer_sequence<int, KB>{});
 #pragma unroll
-  for (int k = 0; k < kBjB; ++k) {
-    double* rb = sh.rowb[k & 1];
-    if (r == k) {
-#pragma unroll
-      for (int j = 0; j < 16; j += 2) *reinterpret_cast<double2*>(rb + 16 * ch + j) = make_double2(p[j], p[j + 1]);
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // wave-private line: in-order LDS
-    double v[16];
-#pragma unroll
-    for (int j = 0; j < 16; j += 2) {
-      const double2 w = *reinterpret_cast<const double2*>(rb + 16 * ch + j);
-      v[j] = w.x;
-      v[j + 1] = w.y;
-    }
-    const double akk = rb[k];
-    const double own = p[k & 15];
-    const double oth = lane_swap1(own);
-    const double g = ((ch == (k >> 4)) ? own : oth) - (r == k ? 1.0 : 0.0);
-    const double pk = gj_recip(akk);
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      const double u = (16 * ch + j == k) ? 1.0 + pk : v[j] * pk;
-      p[j] = fma(-g, u, p[j]);
-    }
-  }
-#pragma unroll
-  for (int j = 0; j < 16; j += 2) *reinterpret_cast<double2*>(prow + j) = make_double2(p[j], p[j + 1]);
+  for (int j = 0; j < VPL; j += 2) *reinterpret_cast<double2*>(prow + j) = make_double2(p[j], p[j + 1]);
 }
 
-// the c-th 16-column (or row) tile outside the pivot block kb
-__device__ __forceinline__ int bj_outside(int c, int kb) { return 16 * c < kb ? 16 * c : 16 * c + kBjB; }
+// the c-th 16-row / column tile outside the pivot block [kb, kb + KB)
+template <int KB>
+__device__ __forceinline__ int bj_outside(int c, int kb) { return 16 * c < kb ? 16 * c : 16 * c + KB; }
 
+template <int KB>
 __global__ __launch_bounds__(kBjThreads) void bj_inv_kernel(const double* __restrict__ Ablk, int64_t lda, int k0,
                                                             double* __restrict__ Dinv, int* __restrict__ info) {
+  constexpr int RT = KB / 16;          // row tiles of the pivot rows
+  constexpr int OT = (NB - KB) / 16;   // tiles outside the pivot block
   __shared__ BjLds sh;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int m = lane & 15, q = lane >> 4;
@@ -395,54 +422,61 @@ __global__ __launch_bounds__(kBjThreads) void bj_inv_kernel(const double* __rest
     for (int r = t >> 7; r < NB; r += kBjThreads / NB) sh.a[r * kBjLd + c] = Ablk[(int64_t)r * lda + c];
   }
   __syncthreads();
-  for (int kb = 0; kb < NB; kb += kBjB) {
-    if (wave == 0) bj_leaf(sh, kb, lane);
+  for (int kb = 0; kb < NB; kb += KB) {
+    if (wave == 0) bj_leaf<KB>(sh, kb, lane);
     __syncthreads();
-    // step 2: 2 x 6 tiles of the pivot rows, waves 0..7 then 0..3
-    dev::d4 acc2[2];
-    int nt2 = 0;
-    for (int ti = wave; ti < 12; ti += 8, ++nt2) {
-      const int r0 = kb + 16 * (ti / 6), c0 = bj_outside(ti % 6, kb);
-      dev::d4 acc = {0.0, 0.0, 0.0, 0.0};
+    // step 2: RT x OT tiles of the pivot rows, dealt to the waves
+    constexpr int N2 = (RT * OT + 7) / 8;
+    dev::d4 acc2[N2];
 #pragma unroll
-      for (int kk = 0; kk < kBjB; kk += 4) {
-        const double av = sh.a[(r0 + m) * kBjLd + kb + kk + q];   // P^-1 (row r0 + m, col kb + k)
-        const double bv = sh.a[(kb + kk + q) * kBjLd + c0 + m];   // A[kb + k, c0 + n]
-        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
+    for (int u = 0; u < N2; ++u) {
+      const int ti = wave + 8 * u;
+      if (ti < RT * OT) {
+        const int r0 = kb + 16 * (ti / OT), c0 = bj_outside<KB>(ti % OT, kb);
+        dev::d4 acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int kk = 0; kk < KB; kk += 4) {
+          const double av = sh.a[(r0 + m) * kBjLd + kb + kk + q];   // P^-1 (row r0 + m, col kb + k)
+          const double bv = sh.a[(kb + kk + q) * kBjLd + c0 + m];   // A[kb + k, c0 + n]
+          acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
+        }
+        acc2[u] = acc;
       }
-      acc2[nt2] = acc;
     }
     __syncthreads();
-    nt2 = 0;
-    for (int ti = wave; ti < 12; ti += 8, ++nt2) {
-      const int r0 = kb + 16 * (ti / 6), c0 = bj_outside(ti % 6, kb);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) sh.a[(r0 + q + 4 * i) * kBjLd + c0 + m] = acc2[nt2][i];
+    for (int u = 0; u < N2; ++u) {
+      const int ti = wave + 8 * u;
+      if (ti < RT * OT) {
+        const int r0 = kb + 16 * (ti / OT), c0 = bj_outside<KB>(ti % OT, kb);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) sh.a[(r0 + q + 4 * i) * kBjLd + c0 + m] = acc2[u][i];
+      }
     }
     __syncthreads();
-    // step 3: column tile `wave` of the 6 row tiles outside kb
+    // step 3: column tile `wave` of the OT row tiles outside the pivot block
     const int c0 = 16 * wave;
-    const bool pcol = c0 >= kb && c0 < kb + kBjB;
-    dev::d4 acc3[6];
+    const bool pcol = c0 >= kb && c0 < kb + KB;
+    dev::d4 acc3[OT];
 #pragma unroll
-    for (int s = 0; s < 6; ++s) {
-      const int r0 = bj_outside(s, kb);
+    for (int s = 0; s < OT; ++s) {
+      const int r0 = bj_outside<KB>(s, kb);
 #pragma unroll
       for (int i = 0; i < 4; ++i) acc3[s][i] = pcol ? 0.0 : sh.a[(r0 + q + 4 * i) * kBjLd + c0 + m];
     }
 #pragma unroll
-    for (int kk = 0; kk < kBjB; kk += 4) {
+    for (int kk = 0; kk < KB; kk += 4) {
       const double bv = sh.a[(kb + kk + q) * kBjLd + c0 + m];
 #pragma unroll
-      for (int s = 0; s < 6; ++s) {
-        const double av = sh.a[(bj_outside(s, kb) + m) * kBjLd + kb + kk + q];
+      for (int s = 0; s < OT; ++s) {
+        const double av = sh.a[(bj_outside<KB>(s, kb) + m) * kBjLd + kb + kk + q];
         acc3[s] = __builtin_amdgcn_mfma_f64_16x16x4f64(-av, bv, acc3[s], 0, 0, 0);
       }
     }
     __syncthreads();
 #pragma unroll
-    for (int s = 0; s < 6; ++s) {
-      const int r0 = bj_outside(s, kb);
+    for (int s = 0; s < OT; ++s) {
+      const int r0 = bj_outside<KB>(s, kb);
 #pragma unroll
       for (int i = 0; i < 4; ++i) sh.a[(r0 + q + 4 * i) * kBjLd + c0 + m] = acc3[s][i];
     }
@@ -470,9 +504,13 @@ __global__ __launch_bounds__(kBjThreads) void bj_inv_kernel(const double* __rest
 // The inverse of the NB x NB block at Ablk; `col` (its first global column)
 // only labels a non-finite result in info.
 int block_inv(const double* Ablk, int64_t lda, int64_t col, double* Di, int* info, hipStream_t s) {
-  const char* eb = std::getenv("GELIM_GJ_BLOCKED");  // 1: the blocked MFMA form (read per launch)
-  if (eb && std::atoi(eb) == 1) {
-    hipLaunchKernelGGL(bj_inv_kernel, dim3(1), dim3(kBjThreads), 0, s, Ablk, lda, (int)col, Di, info);
+  // GELIM_GJ_BLOCKED: 1 = the blocked MFMA form with 32-pivot blocks, 2 = with
+  // 16-pivot blocks (read per launch)
+  const char* eb = std::getenv("GELIM_GJ_BLOCKED");
+  const int bj = eb ? std::atoi(eb) : 0;
+  if (bj == 1 || bj == 2) {
+    if (bj == 1) hipLaunchKernelGGL(bj_inv_kernel<32>, dim3(1), dim3(kBjThreads), 0, s, Ablk, lda, (int)col, Di, info);
+    else hipLaunchKernelGGL(bj_inv_kernel<16>, dim3(1), dim3(kBjThreads), 0, s, Ablk, lda, (int)col, Di, info);
     HIP_TRY(hipGetLastError());
     return GELIM_OK;
   }

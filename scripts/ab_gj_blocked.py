@@ -1,5 +1,5 @@
 """A/B of the diagonal-block inverse forms (GELIM_GJ_BLOCKED=0: one barrier
-per pivot; 1: 32-pivot blocks with MFMA updates): the kernel alone, and the
+per pivot; 1 / 2: 32- / 16-pivot blocks with MFMA updates): the kernel alone, and the
 hip-rbt solves at 2048 and 8192 (time, corrections, backward error).
 
   python scripts/ab_gj_blocked.py
@@ -19,11 +19,12 @@ from gelim.utils.tensors import ptr, stream_handle  # noqa: E402
 dev = torch.device("cuda:0")
 lib = gelim._native.lib()
 sh = stream_handle(dev)
-A = torch.randn(128, 130, dtype=torch.float64, device=dev)[:, :128] + 16 * torch.eye(128, dtype=torch.float64,
-                                                                                   device=dev)
+Af = torch.randn(128, 130, dtype=torch.float64, device=dev)
+Af[:, :128] += 16 * torch.eye(128, dtype=torch.float64, device=dev)
+A = Af[:, :128]  # a strided block, leading dimension 130
 D = torch.empty(128, 128, dtype=torch.float64, device=dev)
 info = torch.full((1,), 0x7F7F7F7F, dtype=torch.int32, device=dev)
-for form in ("0", "1"):
+for form in ("0", "1", "2"):
     os.environ["GELIM_GJ_BLOCKED"] = form
     for _ in range(3):
         lib.gelim_rbt_block_inverse(ptr(A), 130, 0, ptr(D), ptr(info), sh)
@@ -39,7 +40,7 @@ for form in ("0", "1"):
           f"max rel diff vs torch {((D - ref).abs().max() / ref.abs().max()).item():.2e}", flush=True)
 for n in (2048, 8192):
     aug = gelim.random_system(n, seed=31 + n, device=dev)
-    for form in ("0", "1"):
+    for form in ("0", "1", "2"):
         os.environ["GELIM_GJ_BLOCKED"] = form
         s = gelim.GaussSolver(n, backend="hip-rbt", device=dev)
         s.solve(aug)

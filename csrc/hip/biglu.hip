@@ -25,6 +25,7 @@
 #include <algorithm>
 #include <cstdint>
 #include <cstdlib>
+#include <string>
 #include <utility>
 
 #include "device_common.h"
@@ -420,6 +421,10 @@ __global__ void fold_info_kernel(int* __restrict__ info, const int* __restrict__
 
 }  // namespace
 
+struct LeafShape {
+  int nwv, rw;  // waves per participant, rows per lane
+};
+
 namespace sleaf {  // leaf_stream.hip
 size_t scratch_bytes();
 int factor(double* A, int64_t lda, int64_t m, int64_t c0, int mode, int* ipiv, int* pairs, int* info,
@@ -430,20 +435,39 @@ int factor(double* A, int64_t lda, int64_t m, int64_t c0, int mode, int* ipiv, i
 size_t workspace_bytes() { return leafk::kKeyBytes + leafk::kRowBytes + sleaf::scratch_bytes(); }
 int leaf_width() { return LW; }
 
-// Waves per leaf participant: GELIM_LEAF_WAVES = 1 | 4 (default 1), raised
-// to 4 when m needs more than kMaxP single-wave participants (m > 65536).
-// Measured (profiles/leaf_waves_ab.txt): merging 4 waves per participant in
-// LDS first does not shorten the column (4.7 vs 4.5 us at m = 8192, 5.4 vs
-// 4.5 at 32768; 8192 solve 37.4 vs 34.9 ms) -- the exchange costs the same
-// with 8 or 32 parties -- so it is kept only for the rows past 65536.
-int leaf_waves(int64_t m) {
-  static const int env = [] {
-    const char* e = std::getenv("GELIM_LEAF_WAVES");
-    const int v = e ? std::atoi(e) : 0;
-    return (v == 1 || v == 4) ? v : 1;
+// Leaf participant shape (waves x rows per lane), GELIM_LEAF_SHAPE = 1x4 |
+// 2x2 | 4x1 | 4x4 (read once; default 2x2), every shape but 4x4 a 256-row
+// participant; past kMaxP such participants (m > 65536) 4x4 (1024 rows).
+// Measured (profiles/leaf_shape_r4.txt): 2x2 -- two waves of 128 rows, the
+// 128-VGPR panel in architectural registers (1x4 keeps half of its 256-VGPR
+// panel in AGPRs: every update of it is accvgpr read + FMA + accvgpr write)
+// and half the per-column update per wave, the two candidates merged in LDS
+// behind one barrier -- m = 8192: 2.93 vs 3.90 us per column, the 8192
+// solve 31.6 vs 33.8 ms; 4x4 (round 3) was slower than 1x4 where both fit
+// (profiles/leaf_waves_ab.txt).  GELIM_LEAF_WAVES = 1 | 2 | 4 (older knob)
+// maps to 1x4 | 2x2 | 4x4.
+LeafShape leaf_shape(int64_t m) {
+  static const LeafShape env = [] {
+    if (const char* e = std::getenv("GELIM_LEAF_SHAPE")) {
+      const std::string v(e);
+      if (v == "1x4") return LeafShape{1, 4};
+      if (v == "4x1") return LeafShape{4, 1};
+      if (v == "4x4") return LeafShape{4, 4};
+      return LeafShape{2, 2};
+    }
+    if (const char* e = std::getenv("GELIM_LEAF_WAVES")) {
+      const int v = std::atoi(e);
+      if (v == 1) return LeafShape{1, 4};
+      if (v == 4) return LeafShape{4, 4};
+    }
+    return LeafShape{2, 2};
   }();
-  return (env == 1 && m > (int64_t)leafk::kMaxP * leafk::kRowsPerWave) ? 4 : env;
+  if (env.nwv * env.rw == 4 && m > (int64_t)leafk::kMaxP * leafk::kRowsPerWave) return LeafShape{4, 4};
+  return env;
 }
+int leaf_waves(int64_t m) { return leaf_shape(m).nwv; }
+// rows of one participant
+int64_t participant_rows(LeafShape sh) { return (int64_t)sh.nwv * 64 * sh.rw; }
 // Rows the register-resident leaf holds (256 participants x 4 waves x 256
 // rows: the chip's register file); taller panels take the streamed leaf
 // (leaf_stream.hip, HBM-resident, same results bit for bit), so the leaf
@@ -458,7 +482,7 @@ bool leaf_streamed(int64_t m) {
   return e != nullptr && std::atoi(e) == 1;
 }
 int leaf_participants(int64_t m) {
-  const int64_t rows = (int64_t)leaf_waves(m) * leafk::kRowsPerWave;
+  const int64_t rows = participant_rows(leaf_shape(m));
   return (int)((m + rows - 1) / rows);
 }
 // CUs a leaf of m rows needs at once (its waves take a whole SIMD's registers:
@@ -466,7 +490,8 @@ int leaf_participants(int64_t m) {
 int leaf_cus(int64_t m) {
   if (m > reg_max_rows()) return 0;  // the streamed leaf: ordinary launches, no residency
   const int P = leaf_participants(m);
-  return leaf_waves(m) == 4 ? P : (P + 3) / 4;
+  const int nwv = leaf_waves(m);
+  return nwv == 4 ? P : nwv == 2 ? (P + 1) / 2 : (P + 3) / 4;  // a CU holds 4 waves of a full SIMD each
 }
 // the composed row movement keeps one int per row of the panel in LDS
 int64_t compose_max_rows() { return 160 * 1024 / (int64_t)sizeof(int) - 1; }
@@ -481,7 +506,7 @@ int leaf_factor(double* A, int64_t lda, int64_t m, int64_t c0, int mode, int* ip
   if (leaf_streamed(m))
     return sleaf::factor(A, lda, m, c0, mode, ipiv, pairs, info,
                          static_cast<char*>(ws) + leafk::kKeyBytes + leafk::kRowBytes, s);
-  const int nwv = leaf_waves(m);
+  const LeafShape shp = leaf_shape(m);
   leafk::LeafArgs a{};
   a.A = A;
   a.lda = lda;
@@ -500,12 +525,18 @@ int leaf_factor(double* A, int64_t lda, int64_t m, int64_t c0, int mode, int* ip
   // single-wave participants (profiles/leaf_fused_vs_2hop.txt)
   static const bool fused = std::getenv("GELIM_LEAF_2HOP") == nullptr;
   const bool zero = mode != GELIM_PIVOT_PARTIAL;
-  if (nwv == 1) {
-    if (zero) leafk::launch_leaf_nwv<1, 0>(a, fused, s);
-    else leafk::launch_leaf_nwv<1, 1>(a, fused, s);
+  if (shp.nwv == 1) {
+    if (zero) leafk::launch_leaf_shape<1, 4, 0>(a, fused, s);
+    else leafk::launch_leaf_shape<1, 4, 1>(a, fused, s);
+  } else if (shp.nwv == 2) {
+    if (zero) leafk::launch_leaf_shape<2, 2, 0>(a, fused, s);
+    else leafk::launch_leaf_shape<2, 2, 1>(a, fused, s);
+  } else if (shp.rw == 1) {
+    if (zero) leafk::launch_leaf_shape<4, 1, 0>(a, fused, s);
+    else leafk::launch_leaf_shape<4, 1, 1>(a, fused, s);
   } else {
-    if (zero) leafk::launch_leaf_nwv<4, 0>(a, fused, s);
-    else leafk::launch_leaf_nwv<4, 1>(a, fused, s);
+    if (zero) leafk::launch_leaf_shape<4, 4, 0>(a, fused, s);
+    else leafk::launch_leaf_shape<4, 4, 1>(a, fused, s);
   }
   HIP_TRY(hipGetLastError());
   return GELIM_OK;

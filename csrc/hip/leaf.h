@@ -9,9 +9,11 @@
 // '>' of Pthreads/Version-1/gauss_external_input.c:130-134 = ties to the
 // lowest row) on 32 columns, LAPACK row order.
 //
-// Layout: participant p = blockIdx.x owns rows [p * NWV * 256, +NWV * 256);
-// wave w of it the 256 rows from (p * NWV + w) * 256, lane l the rows
-// base + l + 64 i (i < R = 4) -- 32 columns each, register resident.
+// Layout: participant p = blockIdx.x owns rows [p * NWV * 64 R, +NWV * 64 R);
+// wave w of it the 64 R rows from (p * NWV + w) * 64 R, lane l the rows
+// base + l + 64 i (i < R) -- 32 columns each, register resident.  Shapes
+// (NWV x R): 2 x 2 by default, 1 x 4, 4 x 1, and 4 x 4 past 65536 rows
+// (biglu.hip leaf_shape).
 //
 // Per column J:
 //  1. every lane's best live row, the wave's arg-max (DPP, one ballot);
@@ -48,7 +50,7 @@ namespace big {
 namespace leafk {
 
 constexpr int LW = 32;             // leaf width
-constexpr int R = 4;               // rows per lane
+constexpr int R = 4;               // rows per lane of the default shape (template parameter RW)
 constexpr int kRowsPerWave = 64 * R;
 constexpr int kMaxP = 256;         // participating workgroups
 constexpr int kAuxSc1 = 16;        // buffer-op aux: sc1
@@ -122,12 +124,12 @@ __device__ __forceinline__ void lstamp(const LeafArgs& g, int J, int k, unsigned
   if (g.stamps != nullptr && threadIdx.x == 0) g.stamps[((int64_t)blockIdx.x * LW + J) * 8 + k] = v;
 }
 
-template <int NWV>
+template <int NWV, int RW>
 struct alignas(16) LeafLds {
   double prow[NWV][2][LW];      // per wave: the pivot rows of the last two columns (parity)
   double cand[2][NWV][LW];      // per parity and wave: the wave's candidate row (NWV > 1)
   u32x4 wkey[2][NWV];           // per parity and wave: {key lo, key hi, row, -} (NWV > 1)
-  int dest[NWV][kRowsPerWave];  // final row of a moved local row (-1: unmoved)
+  int dest[NWV][64 * RW];       // final row of a moved local row (-1: unmoved)
 };
 
 // ---- the LAPACK interchange replay, in the lanes of the wave -----------------
@@ -188,9 +190,9 @@ __device__ __forceinline__ int live_granule(int g) {
   return (g % LW) < kLive<J> ? g - (g % LW) + kLive<J> : g;
 }
 
-template <int MODE, int NKK, int NR, int NWV>
+template <int MODE, int NKK, int NR, int NWV, int R = leafk::R>
 struct Leaf {
-  using Lds = LeafLds<NWV>;
+  using Lds = LeafLds<NWV, R>;
   // one column J of the leaf (compile time); false: hand-off aborted
   template <int J>
   static __device__ __forceinline__ bool col(double (&a)[R][LW], bool (&live)[R], int (&pos)[R], double (&lp)[R],
@@ -446,9 +448,10 @@ struct Leaf {
   }
 };
 
-template <int MODE, int NKK, int NR, int NWV>
+template <int MODE, int NKK, int NR, int NWV, int R>
 __global__ __launch_bounds__(64 * NWV, 1) void leaf_kernel(LeafArgs g) {
-  __shared__ LeafLds<NWV> sh;
+  constexpr int kRowsPerWave = 64 * R;
+  __shared__ LeafLds<NWV, R> sh;
   const int lane = threadIdx.x & 63;
   const int wave = NWV > 1 ? __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) : 0;
   const int base = (blockIdx.x * NWV + wave) * kRowsPerWave;
@@ -471,7 +474,7 @@ __global__ __launch_bounds__(64 * NWV, 1) void leaf_kernel(LeafArgs g) {
 #pragma unroll
   for (int i = 0; i < R; ++i) sh.dest[wave][lane + 64 * i] = -1;
   Table tb{0, 0, 0};
-  if (!Leaf<MODE, NKK, NR, NWV>::factor(a, live, pos, sh, tb, g, lane, wave, base,
+  if (!Leaf<MODE, NKK, NR, NWV, R>::factor(a, live, pos, sh, tb, g, lane, wave, base,
                                         std::make_integer_sequence<int, LW>{}))
     return;
 
@@ -498,25 +501,26 @@ __global__ __launch_bounds__(64 * NWV, 1) void leaf_kernel(LeafArgs g) {
   }
 }
 
-// launcher of one instantiation (leaf_w*.hip)
-template <int MODE, int NKK, int NR, int NWV>
+// launcher of one instantiation (leaf_w*.hip): NWV waves of RW rows per
+// lane per participant
+template <int MODE, int NKK, int NR, int NWV, int RW>
 void launch_leaf(const LeafArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL((leaf_kernel<MODE, NKK, NR, NWV>), dim3((unsigned)a.P), dim3(64 * NWV), 0, s, a);
+  hipLaunchKernelGGL((leaf_kernel<MODE, NKK, NR, NWV, RW>), dim3((unsigned)a.P), dim3(64 * NWV), 0, s, a);
 }
 
-// host dispatch by participant count, one (NWV, MODE) per instantiation unit
-template <int NWV, int MODE>
-void launch_leaf_nwv(const LeafArgs& a, bool fused, hipStream_t s);
+// host dispatch by participant count, one (NWV, RW, MODE) per instantiation unit
+template <int NWV, int RW, int MODE>
+void launch_leaf_shape(const LeafArgs& a, bool fused, hipStream_t s);
 
-#define GELIM_LEAF_NWV_DEFINE(NWV, MODE)                                                        \
+#define GELIM_LEAF_SHAPE_DEFINE(NWV, RW, MODE)                                                  \
   template <>                                                                                   \
-  void launch_leaf_nwv<NWV, MODE>(const LeafArgs& a, bool fused, hipStream_t s) {               \
-    if (fused && a.P <= 8) launch_leaf<MODE, 1, 4, NWV>(a, s);                                  \
-    else if (fused && a.P <= 16) launch_leaf<MODE, 1, 8, NWV>(a, s);                            \
-    else if (fused && a.P <= 32) launch_leaf<MODE, 1, 16, NWV>(a, s);                           \
-    else if (a.P <= 64) launch_leaf<MODE, 1, 0, NWV>(a, s);                                     \
-    else if (a.P <= 128) launch_leaf<MODE, 2, 0, NWV>(a, s);                                    \
-    else launch_leaf<MODE, 4, 0, NWV>(a, s);                                                    \
+  void launch_leaf_shape<NWV, RW, MODE>(const LeafArgs& a, bool fused, hipStream_t s) {         \
+    if (fused && a.P <= 8) launch_leaf<MODE, 1, 4, NWV, RW>(a, s);                              \
+    else if (fused && a.P <= 16) launch_leaf<MODE, 1, 8, NWV, RW>(a, s);                        \
+    else if (fused && a.P <= 32) launch_leaf<MODE, 1, 16, NWV, RW>(a, s);                       \
+    else if (a.P <= 64) launch_leaf<MODE, 1, 0, NWV, RW>(a, s);                                 \
+    else if (a.P <= 128) launch_leaf<MODE, 2, 0, NWV, RW>(a, s);                                \
+    else launch_leaf<MODE, 4, 0, NWV, RW>(a, s);                                                \
   }
 
 }  // namespace leafk

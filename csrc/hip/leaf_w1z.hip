@@ -7,7 +7,7 @@
 namespace gelim {
 namespace big {
 namespace leafk {
-GELIM_LEAF_NWV_DEFINE(1, 0)
+GELIM_LEAF_SHAPE_DEFINE(1, 4, 0)
 }  // namespace leafk
 }  // namespace big
 }  // namespace gelim

@@ -1,4 +1,4 @@
-// Leaf instantiations: 4 wave(s) per participant, partial pivoting
+// Leaf instantiations: 4 waves of 1 row per lane per participant, partial pivoting
 // (csrc/hip/leaf.h; split per variant so they compile in parallel).
 #include "leaf.h"
 
@@ -7,7 +7,7 @@
 namespace gelim {
 namespace big {
 namespace leafk {
-GELIM_LEAF_SHAPE_DEFINE(4, 4, 1)
+GELIM_LEAF_SHAPE_DEFINE(4, 1, 1)
 }  // namespace leafk
 }  // namespace big
 }  // namespace gelim

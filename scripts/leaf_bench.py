@@ -49,7 +49,7 @@ def main() -> None:
 
     t_leaf = timeit(leaf) - timeit(copy_only)
     import os
-    print(f"leaf m={m} (GELIM_LEAF_WAVES={os.environ.get('GELIM_LEAF_WAVES', 'default')}, "
+    print(f"leaf m={m} (GELIM_LEAF_SHAPE={os.environ.get('GELIM_LEAF_SHAPE', 'default')}, "
           f"{lib.gelim_gpu_leaf_participants(m)} participants): {t_leaf:.1f} us ({t_leaf / 32:.2f} us/column)")
     if "--time-only" in sys.argv:
         return

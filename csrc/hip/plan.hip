@@ -129,6 +129,15 @@ struct gelim_gauss_plan {
   int* big_net = nullptr;                // an outer panel's composed row movement (side stream)
   hipStream_t big_side = nullptr;
   std::vector<hipEvent_t> big_ev;        // fork, fact[T], next[T], join
+  // GELIM_BIG_SPLIT=1 (lookahead only, default off): after each leaf only the
+  // NEXT leaf's 32 columns are updated on the caller's stream; the rest of the
+  // leaf's update (the panel's L part, the other columns of P_j / P_j+1) runs
+  // on big_rest beside the next leaf.  Measured slower (8192: 34.0 vs 31.6 ms,
+  // profiles/leaf_shape_r4.txt): the rest work beside the leaf delays it more
+  // than the shorter critical update saves
+  bool big_split = false;
+  hipStream_t big_rest = nullptr;
+  std::vector<hipEvent_t> big_rev;       // per leaf: critical part done (leaf_ev) / rest done
   hipGraphExec_t exec = nullptr;
   hipGraph_t tpl = nullptr;              // template of exec (GELIM_GRAPH_KEEPTPL=1 keeps it alive)
   // the graph is captured ONCE on plan-owned buffers: the input is staged
@@ -280,6 +289,8 @@ int enqueue_big(gelim_gauss_plan* p, double* A, double* x, double* bnorm, hipStr
     HIP_TRY(hipStreamWaitEvent(side, *ev_fork, 0));
   }
   int leaf = 0;
+  const bool split = la && p->big_split;
+  bool rest_pending = false;  // big_rest has work the caller's stream has not waited for
   for (int64_t j = 0; j < T; ++j) {
     const int64_t k = kb(j), kend = kb(j + 1);
     const int64_t cend = la ? kb(j + 2) : n + 1;  // columns the leaves update: P_j (+ P_j+1)
@@ -290,6 +301,32 @@ int enqueue_big(gelim_gauss_plan* p, double* A, double* x, double* bnorm, hipStr
                                  leaf, s));
       // P_j+1 is side j-1's until next[j-1]
       if (la && c0 == k && j > 0 && cend > kend) HIP_TRY(hipStreamWaitEvent(s, ev_next[j - 1], 0));
+      if (split) {
+        // critical: the next leaf's columns [c1, nx) only (swaps, TRSM of
+        // the leaf's U rows, rank-32 GEMM); they may still carry the previous
+        // leaf's rest update, so wait for it first
+        const int64_t c1 = c0 + LW, nx = std::min(c1 + LW, cend);
+        if (rest_pending) HIP_TRY(hipStreamWaitEvent(s, p->big_rev[2 * (leaf - 1) + 1], 0));
+        rest_pending = false;
+        if (nx > c1) {
+          GELIM_TRY(big::laswp_trsm(A + c0 * lda, lda, c0, 0, 0, c1, nx, nx, n - c0, pr, s));
+          GELIM_TRY(dgemm(A + c1 * lda + c1, lda, A + c1 * lda + c0, lda, A + c0 * lda + c1, lda, n - c1, nx - c1, LW,
+                          -1.0, s));
+        }
+        // the rest on big_rest, beside the next leaf: the panel's L part
+        // (swaps) and the columns [nx, cend) (swaps, TRSM, GEMM)
+        if (nx < cend || c0 > k) {
+          HIP_TRY(hipEventRecord(p->big_rev[2 * leaf], s));
+          HIP_TRY(hipStreamWaitEvent(p->big_rest, p->big_rev[2 * leaf], 0));
+          GELIM_TRY(big::laswp_trsm(A + c0 * lda, lda, c0, k, c0, nx, cend, cend, n - c0, pr, p->big_rest));
+          if (nx < cend)
+            GELIM_TRY(dgemm(A + c1 * lda + nx, lda, A + c1 * lda + c0, lda, A + c0 * lda + nx, lda, n - c1, cend - nx,
+                            LW, -1.0, p->big_rest));
+          HIP_TRY(hipEventRecord(p->big_rev[2 * leaf + 1], p->big_rest));
+          rest_pending = true;
+        }
+        continue;
+      }
       // serial: interchanges on every other column (L part, rest of the
       // panel, trailing columns, b), TRSM inside the panel; lookahead: the
       // panel's own L part and P_j, P_j+1 (swaps + TRSM)
@@ -309,6 +346,10 @@ int enqueue_big(gelim_gauss_plan* p, double* A, double* x, double* bnorm, hipStr
     }
     const int nl = leaf - first_leaf;
     const int* pr0 = p->big_pairs + first_leaf * kBigPairSlot;
+    if (rest_pending) {  // the panel is complete only with its last leaf's rest update
+      HIP_TRY(hipStreamWaitEvent(s, p->big_rev[2 * (leaf - 1) + 1], 0));
+      rest_pending = false;
+    }
     HIP_TRY(hipEventRecord(ev_fact[j], s));
     HIP_TRY(hipStreamWaitEvent(side, ev_fact[j], 0));
     // the panel's row movement composed into one permutation (<= 64 rows per
@@ -565,6 +606,14 @@ extern "C" gelim_gauss_plan* gelim_gauss_plan_create(int64_t n, int algo, int pi
       p->big_ev.assign((size_t)(2 * T + 2), nullptr);
       for (auto& e : p->big_ev)
         if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return fail("event");
+      const char* es = std::getenv("GELIM_BIG_SPLIT");
+      p->big_split = es ? std::atoi(es) != 0 : false;
+      if (p->big_split) {
+        if (gelim::side_stream_create(&p->big_rest) != GELIM_OK) return fail("rest stream");
+        p->big_rev.assign((size_t)(2 * nleaves), nullptr);
+        for (auto& e : p->big_rev)
+          if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return fail("event");
+      }
     }
     p->tail = gelim_gauss_plan_create(n - big_k, algo, pivot, dtype_bytes, 0);
     if (!p->tail) {
@@ -659,6 +708,9 @@ extern "C" void gelim_gauss_plan_destroy(gelim_gauss_plan* p) {
   if (p->side) (void)hipStreamDestroy(p->side);
   if (p->big_side) (void)hipStreamDestroy(p->big_side);
   for (auto& e : p->big_ev)
+    if (e) (void)hipEventDestroy(e);
+  if (p->big_rest) (void)hipStreamDestroy(p->big_rest);
+  for (auto& e : p->big_rev)
     if (e) (void)hipEventDestroy(e);
   for (auto* v : {&p->ev_panel, &p->ev_wide})
     for (auto& e : *v)

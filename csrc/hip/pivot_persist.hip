@@ -364,7 +364,12 @@ int pivot_persistent(T* A, int64_t lda, int64_t n, int mode, int* info, int* ipi
     return e ? std::atoi(e) : 1;
   }();
   if (!on || n > 2048 || n < 1) return 1;
-  // 8 rows x 9 column slots per thread (256 threads): 2048 x 2049 on 256 CUs
+  // GELIM_PIVOT_SHAPE (read per call): 1 (default) = 256 threads x 8 rows x 9
+  // column slots per thread, 2048 x 2049 on 256 CUs; 2 = 512 threads x 16 rows
+  // x 5 slots on 128 CUs (half the workgroups: half the candidate sweep and
+  // half the pivot-row broadcast traffic per step)
+  const char* e = std::getenv("GELIM_PIVOT_SHAPE");
+  if (e && std::atoi(e) == 2) return launch_pp<T, 512, 16, 5>(A, lda, n, mode, info, ipiv, diag, ws, s);
   return launch_pp<T, 256, 8, 9>(A, lda, n, mode, info, ipiv, diag, ws, s);
 }
 

@@ -180,16 +180,13 @@ __global__ __launch_bounds__(NT) void pivot_persist_kernel(PpArgs g) {
           bp = v.z;
         }
       }
-      // wave arg-max: largest key, lowest position
-#pragma unroll
-      for (int off = 32; off >= 1; off >>= 1) {
-        const unsigned kh = __shfl_xor((unsigned)(bk >> 32), off), kl = __shfl_xor((unsigned)bk, off);
-        const unsigned op = __shfl_xor(bp, off);
-        const uint64_t ok2 = ((uint64_t)kh << 32) | kl;
-        if (ok2 > bk || (ok2 == bk && op < bp)) {
-          bk = ok2;
-          bp = op;
-        }
+      // wave arg-max: largest key, lowest position -- two DPP ladders (the
+      // 64-bit max, then the min position among its holders) instead of six
+      // ds_bpermute round trips per value
+      {
+        const uint64_t km = dev::wave_max_u64(bk);
+        bp = dev::wave_min_u32(bk == km ? bp : 0xffffffffu);
+        bk = km;
       }
       const bool all_good = __ballot(!good) == 0 &&
                             __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0;
@@ -368,6 +365,7 @@ int pivot_persistent(T* A, int64_t lda, int64_t n, int mode, int* info, int* ipi
   // column slots per thread, 2048 x 2049 on 256 CUs; 2 = 512 threads x 16 rows
   // x 5 slots on 128 CUs (half the workgroups: half the candidate sweep and
   // half the pivot-row broadcast traffic per step)
+  // (measured slower: 2048 fp64 14.0 vs 13.5 ms)
   const char* e = std::getenv("GELIM_PIVOT_SHAPE");
   if (e && std::atoi(e) == 2) return launch_pp<T, 512, 16, 5>(A, lda, n, mode, info, ipiv, diag, ws, s);
   return launch_pp<T, 256, 8, 9>(A, lda, n, mode, info, ipiv, diag, ws, s);

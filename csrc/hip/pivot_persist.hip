@@ -96,6 +96,27 @@ struct PpArgs {
   unsigned char* rowb;  // [2][n+1] 16-byte pivot-row granules
 };
 
+// out[r] = a[r][kc] for a thread-uniform kc, by a branch to the one
+// compile-time slot (a select chain costs R x KC x 2 v_cndmask)
+template <int K, int KC, typename T, int R>
+__device__ __forceinline__ void column_of_k(const T (&a)[R][KC], int kc, T (&out)[R]) {
+  if constexpr (K < KC) {
+    if (kc == K) {
+#pragma unroll
+      for (int r = 0; r < R; ++r) out[r] = a[r][K];
+    } else {
+      column_of_k<K + 1, KC>(a, kc, out);
+    }
+  } else {
+#pragma unroll
+    for (int r = 0; r < R; ++r) out[r] = T(0);
+  }
+}
+template <int KC, typename T, int R>
+__device__ __forceinline__ void column_of(const T (&a)[R][KC], int kc, T (&out)[R]) {
+  column_of_k<0, KC>(a, kc, out);
+}
+
 template <typename T, int NT, int R, int KC>
 __global__ __launch_bounds__(NT) void pivot_persist_kernel(PpArgs g) {
   extern __shared__ int rowat[];  // [n] position -> physical row; then scalars
@@ -135,11 +156,11 @@ __global__ __launch_bounds__(NT) void pivot_persist_kernel(PpArgs g) {
     uint64_t best = 0;
     int bpos = 0x7fffffff;
     T bval = T(0);
+    T cv[R];  // column kc of every row: one uniform branch instead of a select chain per slot
+    column_of<KC>(a, kc, cv);
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-      T v = T(0);
-#pragma unroll
-      for (int k = 0; k < KC; ++k) v = (k == kc) ? a[r][k] : v;
+      const T v = cv[r];
       s_m[(col & 1) * R + r] = v;
       if (live >> r & 1u) {
         const uint64_t key = cand_key<T>(v, pos[r] == col, g.mode);

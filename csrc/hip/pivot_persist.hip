@@ -186,19 +186,33 @@ __global__ __launch_bounds__(NT) void pivot_persist_kernel(PpArgs g) {
       unsigned bp = 0xffffffffu;
       bool good = true;
       const unsigned long long t0 = rtc();
-      for (int q = lane; q < G; q += 64) {
-        u32x4 v = get16(crs, (uint32_t)((par * G + q) * 16));
-        while (v.w != (unsigned)(i + 1)) {
-          if (rtc() - t0 > kSpinTicks || __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) {
-            good = false;
-            break;
-          }
-          v = get16(crs, (uint32_t)((par * G + q) * 16));
+      // every lane's (up to) 4 granules in flight at once -- lanes past G
+      // read a clamped duplicate, which never changes the arg-max -- then
+      // only the stale ones are re-read: one round trip per column when the
+      // candidates are out, instead of one per granule
+      constexpr int kQ = 4;  // G <= 256
+      u32x4 v[kQ];
+#pragma unroll
+      for (int j = 0; j < kQ; ++j) v[j] = get16(crs, (uint32_t)((par * G + min(lane + 64 * j, G - 1)) * 16));
+      for (;;) {
+        bool ready = true;
+#pragma unroll
+        for (int j = 0; j < kQ; ++j) ready = ready && v[j].w == (unsigned)(i + 1);
+        if (__ballot(!ready) == 0) break;
+        if (rtc() - t0 > kSpinTicks || __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) {
+          good = false;
+          break;
         }
-        const uint64_t k = ((uint64_t)v.y << 32) | v.x;
-        if (k > bk || (k == bk && v.z < bp)) {
+#pragma unroll
+        for (int j = 0; j < kQ; ++j)
+          if (v[j].w != (unsigned)(i + 1)) v[j] = get16(crs, (uint32_t)((par * G + min(lane + 64 * j, G - 1)) * 16));
+      }
+#pragma unroll
+      for (int j = 0; j < kQ; ++j) {
+        const uint64_t k = ((uint64_t)v[j].y << 32) | v[j].x;
+        if (k > bk || (k == bk && v[j].z < bp)) {
           bk = k;
-          bp = v.z;
+          bp = v[j].z;
         }
       }
       // wave arg-max: largest key, lowest position -- two DPP ladders (the
@@ -345,6 +359,7 @@ template <typename T, int NT, int R, int KC>
 int launch_pp(void* A, int64_t lda, int64_t n, int mode, int* info, int* ipiv, double* diag, void* ws,
               hipStream_t s) {
   const int G = (int)((n + R - 1) / R);
+  if (G > 256) return 1;  // the candidate sweep reads at most 4 granules per lane
   const size_t lds = sizeof(int) * (((size_t)n + 8 + 3) & ~(size_t)3) + sizeof(T) * (2 * R + 2);
   static const bool attr = hipFuncSetAttribute((const void*)pivot_persist_kernel<T, NT, R, KC>,
                                                hipFuncAttributeMaxDynamicSharedMemorySize, 64 * 1024) == hipSuccess;

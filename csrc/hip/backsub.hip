@@ -107,7 +107,7 @@ __device__ __forceinline__ bool poll_flag(unsigned* flags, int c, int* err, bool
       }
     }
   }
-  return __shfl(good, 0) != 0;
+  return __builtin_amdgcn_readfirstlane(good) != 0;  // lane 0's verdict (no ds_bpermute round trip)
 }
 
 // acc -= U[rows of this block, block c] . x_c, row = lane: the U block was

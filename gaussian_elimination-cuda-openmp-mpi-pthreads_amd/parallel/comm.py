@@ -182,8 +182,12 @@ def init_from_env(backend: str | None = None, device: str | None = None,
     gloo has no device path (Communicator.staged)."""
     rank, world, local = env_world()
     use_gpu = device != "cpu" and (device is not None or torch.cuda.is_available())
+    want = backend or os.environ.get("GELIM_DIST_BACKEND")
     if use_gpu:
-        dev = torch.device(device) if device not in (None, "cuda") else torch.device("cuda", local)
+        # one rank per GPU; over gloo, more ranks than GPUs share them round-robin
+        ndev = max(1, torch.cuda.device_count())
+        idx = local % ndev if want == "gloo" else local
+        dev = torch.device(device) if device not in (None, "cuda") else torch.device("cuda", idx)
         torch.cuda.set_device(dev)
     else:
         dev = torch.device("cpu")

@@ -435,35 +435,41 @@ int factor(double* A, int64_t lda, int64_t m, int64_t c0, int mode, int* ipiv, i
 size_t workspace_bytes() { return leafk::kKeyBytes + leafk::kRowBytes + sleaf::scratch_bytes(); }
 int leaf_width() { return LW; }
 
-// Leaf participant shape (waves x rows per lane), GELIM_LEAF_SHAPE = 1x4 |
-// 2x2 | 4x1 | 4x4 (read once; default 2x2), every shape but 4x4 a 256-row
-// participant; past kMaxP such participants (m > 65536) 4x4 (1024 rows).
-// Measured (profiles/leaf_shape_r4.txt): 2x2 -- two waves of 128 rows, the
-// 128-VGPR panel in architectural registers (1x4 keeps half of its 256-VGPR
-// panel in AGPRs: every update of it is accvgpr read + FMA + accvgpr write)
-// and half the per-column update per wave, the two candidates merged in LDS
-// behind one barrier -- m = 8192: 2.93 vs 3.90 us per column, the 8192
-// solve 31.6 vs 33.8 ms; 4x4 (round 3) was slower than 1x4 where both fit
-// (profiles/leaf_waves_ab.txt).  GELIM_LEAF_WAVES = 1 | 2 | 4 (older knob)
-// maps to 1x4 | 2x2 | 4x4.
+// Leaf participant shape (waves x rows per lane), GELIM_LEAF_SHAPE = 1x1 |
+// 1x2 | 1x4 | 2x2 | 4x1 | 4x4 (read once; default 1x2: one wave of 128
+// rows, 2 per lane, the 32-column panel in 128 architectural VGPRs); a shape
+// that would need more than kMaxP participants falls back to 1x2 (m <= 32768),
+// 2x2 (m <= 65536), then 4x4.  Measured (profiles/leaf_shape_r4.txt), whole
+// solves 3072 / 4096 / 8192 / 16384: 1x2 7.7 / 11.5 / 31.3 / 125.4 ms, 2x2
+// 7.9 / 12.0 / 31.8 / 127.0, 1x4 (round 3: half of its 256-VGPR panel in
+// AGPRs, every update of it accvgpr read + FMA + accvgpr write) 8.2 / 12.5 /
+// 33.8 / 129.1, 1x1 7.8 / 11.8 / 31.8 / 131.1, 4x1 8.6 / 13.6 / 34.6 / 132.7.
+// GELIM_LEAF_WAVES = 1 | 2 | 4 (older knob) maps to 1x4 | 2x2 | 4x4.
 LeafShape leaf_shape(int64_t m) {
   static const LeafShape env = [] {
     if (const char* e = std::getenv("GELIM_LEAF_SHAPE")) {
       const std::string v(e);
       if (v == "1x4") return LeafShape{1, 4};
+      if (v == "1x2") return LeafShape{1, 2};
+      if (v == "1x1") return LeafShape{1, 1};
+      if (v == "2x2") return LeafShape{2, 2};
       if (v == "4x1") return LeafShape{4, 1};
       if (v == "4x4") return LeafShape{4, 4};
-      return LeafShape{2, 2};
+      return LeafShape{1, 2};
     }
     if (const char* e = std::getenv("GELIM_LEAF_WAVES")) {
       const int v = std::atoi(e);
       if (v == 1) return LeafShape{1, 4};
+      if (v == 2) return LeafShape{2, 2};
       if (v == 4) return LeafShape{4, 4};
     }
-    return LeafShape{2, 2};
+    return LeafShape{1, 2};
   }();
-  if (env.nwv * env.rw == 4 && m > (int64_t)leafk::kMaxP * leafk::kRowsPerWave) return LeafShape{4, 4};
-  return env;
+  auto fits = [&](LeafShape sh) { return m <= (int64_t)leafk::kMaxP * 64 * sh.nwv * sh.rw; };  // <= kMaxP participants
+  if (fits(env)) return env;
+  for (LeafShape sh : {LeafShape{1, 2}, LeafShape{2, 2}})
+    if (sh.nwv * sh.rw > env.nwv * env.rw && fits(sh)) return sh;
+  return LeafShape{4, 4};
 }
 int leaf_waves(int64_t m) { return leaf_shape(m).nwv; }
 // rows of one participant
@@ -525,9 +531,15 @@ int leaf_factor(double* A, int64_t lda, int64_t m, int64_t c0, int mode, int* ip
   // single-wave participants (profiles/leaf_fused_vs_2hop.txt)
   static const bool fused = std::getenv("GELIM_LEAF_2HOP") == nullptr;
   const bool zero = mode != GELIM_PIVOT_PARTIAL;
-  if (shp.nwv == 1) {
+  if (shp.nwv == 1 && shp.rw == 4) {
     if (zero) leafk::launch_leaf_shape<1, 4, 0>(a, fused, s);
     else leafk::launch_leaf_shape<1, 4, 1>(a, fused, s);
+  } else if (shp.nwv == 1 && shp.rw == 1) {
+    if (zero) leafk::launch_leaf_shape<1, 1, 0>(a, fused, s);
+    else leafk::launch_leaf_shape<1, 1, 1>(a, fused, s);
+  } else if (shp.nwv == 1 && shp.rw == 2) {
+    if (zero) leafk::launch_leaf_shape<1, 2, 0>(a, fused, s);
+    else leafk::launch_leaf_shape<1, 2, 1>(a, fused, s);
   } else if (shp.nwv == 2) {
     if (zero) leafk::launch_leaf_shape<2, 2, 0>(a, fused, s);
     else leafk::launch_leaf_shape<2, 2, 1>(a, fused, s);

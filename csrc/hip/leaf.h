@@ -12,7 +12,7 @@
 // Layout: participant p = blockIdx.x owns rows [p * NWV * 64 R, +NWV * 64 R);
 // wave w of it the 64 R rows from (p * NWV + w) * 64 R, lane l the rows
 // base + l + 64 i (i < R) -- 32 columns each, register resident.  Shapes
-// (NWV x R): 2 x 2 by default, 1 x 4, 4 x 1, and 4 x 4 past 65536 rows
+// (NWV x R): 1 x 2 by default, 1 x 1, 1 x 4, 2 x 2, 4 x 1, 4 x 4
 // (biglu.hip leaf_shape).
 //
 // Per column J:

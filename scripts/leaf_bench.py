@@ -39,10 +39,16 @@ def main() -> None:
     pairs = torch.zeros(256, dtype=torch.int32, device=dev)
     info = torch.zeros(4, dtype=torch.int32, device=dev)
 
+    counter = [0]
+
     def leaf():
+        # a fresh leaf counter per call, as in a solve: granules are tagged with
+        # it, so a rerun can never read the previous run's (identical) granules
+        # as current and skip the exchange waits
         A.copy_(A0)
-        _native.check(lib.gelim_gpu_leaf_factor_ws(ptr(A), lda, m, 0, 1, ptr(ipiv), ptr(pairs), ptr(info), ptr(ws), 0,
-                                                   sh), "leaf")
+        counter[0] += 1
+        _native.check(lib.gelim_gpu_leaf_factor_ws(ptr(A), lda, m, 0, 1, ptr(ipiv), ptr(pairs), ptr(info), ptr(ws),
+                                                   counter[0], sh), "leaf")
 
     def copy_only():
         A.copy_(A0)

@@ -1077,6 +1077,8 @@ struct gelim_mixed_plan {
   int aux_on = 0;              // pairs: updates the next inverse does not read on a third stream (factor_la3)
   hipStream_t aux = nullptr;
   hipEvent_t ea = nullptr, eb = nullptr;
+  hipStream_t crit = nullptr;  // GELIM_CRIT_PRIO set: the factorisation's chain on a stream of that priority
+  hipEvent_t ef = nullptr, ej = nullptr;
 };
 
 extern "C" int64_t gelim_mixed_max_n(void) { return (int64_t)gelim::kMaxBlocks * gelim::NB; }
@@ -1093,6 +1095,9 @@ extern "C" void gelim_mixed_plan_destroy(gelim_mixed_plan* p) {
   if (p->e0) (void)hipEventDestroy(p->e0);
   if (p->e1) (void)hipEventDestroy(p->e1);
   if (p->side) (void)hipStreamDestroy(p->side);
+  if (p->ef) (void)hipEventDestroy(p->ef);
+  if (p->ej) (void)hipEventDestroy(p->ej);
+  if (p->crit) (void)hipStreamDestroy(p->crit);
   delete p;
 }
 
@@ -1144,6 +1149,11 @@ extern "C" gelim_mixed_plan* gelim_mixed_plan_create2(int64_t n, const double* u
     if (const char* e = std::getenv("GELIM_RBT_RESERVE")) reserve = std::max(0, std::atoi(e));
     p->cap = reserve == 0 ? 0 : ncu > reserve + 8 ? ncu - reserve : std::max(8, ncu / 2);
     if (gelim::side_stream_create(&p->side) != GELIM_OK) return fail("side stream");
+    if (std::getenv("GELIM_CRIT_PRIO")) {
+      if (gelim::side_stream_create(&p->crit, 1) != GELIM_OK) return fail("critical stream");
+      if (hipEventCreateWithFlags(&p->ef, hipEventDisableTiming) != hipSuccess) return fail("event");
+      if (hipEventCreateWithFlags(&p->ej, hipEventDisableTiming) != hipSuccess) return fail("event");
+    }
     if (hipEventCreateWithFlags(&p->e0, hipEventDisableTiming) != hipSuccess) return fail("event");
     if (hipEventCreateWithFlags(&p->e1, hipEventDisableTiming) != hipSuccess) return fail("event");
     if (p->pairs && p->aux_on) {
@@ -1185,6 +1195,12 @@ extern "C" int gelim_mixed_factor(gelim_mixed_plan* p, const double* aug, int64_
   hipStream_t s = (hipStream_t)stream;
   const int64_t np = p->np, h = np / 4, ldm = p->ldm;
   HIP_TRY(hipMemsetAsync(p->info, 0x7f, 4, s));  // INT_MAX-ish: atomicMin keeps the first bad column
+  hipStream_t caller = s;
+  if (p->crit) {  // fork onto the critical-priority stream; joined below
+    HIP_TRY(hipEventRecord(p->ef, s));
+    HIP_TRY(hipStreamWaitEvent(p->crit, p->ef, 0));
+    s = p->crit;
+  }
   const dim3 grid((unsigned)((h + 255) / 256), (unsigned)h);
   hipLaunchKernelGGL(rbt_matrix_kernel<double>, grid, dim3(256), 0, s, aug, ld, (int)p->n, (int)np, p->ud, p->vd,
                      p->M, ldm);
@@ -1199,6 +1215,11 @@ extern "C" int gelim_mixed_factor(gelim_mixed_plan* p, const double* aug, int64_
   else
     GELIM_TRY(factor_impl(p->M, ldm, np, p->Dinv, p->W, p->fp64 ? nullptr : p->A21f, p->fp64 ? nullptr : p->Wf,
                           p->info, s));
+  if (p->crit) {
+    HIP_TRY(hipEventRecord(p->ej, s));
+    HIP_TRY(hipStreamWaitEvent(caller, p->ej, 0));
+    s = caller;
+  }
   int h_info = 0;
   HIP_TRY(hipMemcpyAsync(&h_info, p->info, 4, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));

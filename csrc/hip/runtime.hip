@@ -244,10 +244,23 @@ int probe_words(int** w) {
   return GELIM_OK;
 }
 
-int side_stream_create(hipStream_t* out) {
+// Stream priority of kind 0 (side streams: GELIM_SIDE_PRIO) or 1 (a
+// critical-chain stream: GELIM_CRIT_PRIO), clamped to the device's range
+// (HIP: lower numbers are higher priorities).  The queue arbiter hands CUs
+// that free up to the higher-priority queue's workgroups first.
+int stream_priority(int kind) {
+  const char* e = std::getenv(kind ? "GELIM_CRIT_PRIO" : "GELIM_SIDE_PRIO");
+  int v = e ? std::atoi(e) : 0;
+  int least = 0, greatest = 0;
+  if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) return 0;
+  return std::max(greatest, std::min(least, v));
+}
+
+int side_stream_create(hipStream_t* out, int kind) {
   *out = nullptr;
+  const int prio = stream_priority(kind);
   if (!probe_enabled()) {
-    HIP_TRY(hipStreamCreateWithFlags(out, hipStreamNonBlocking));
+    HIP_TRY(hipStreamCreateWithPriority(out, hipStreamNonBlocking, prio));
     return GELIM_OK;
   }
   std::lock_guard<std::mutex> lk(g_park_mu);  // one probe at a time (shared words)
@@ -256,7 +269,7 @@ int side_stream_create(hipStream_t* out) {
   hipStream_t s = nullptr;
   int rc = GELIM_OK;
   for (int attempt = 0; attempt < 8; ++attempt) {
-    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) {
+    if (hipStreamCreateWithPriority(&s, hipStreamNonBlocking, prio) != hipSuccess) {
       rc = GELIM_FAIL(GELIM_E_HIP, "side stream");
       s = nullptr;
       break;
@@ -280,6 +293,15 @@ extern "C" int gelim_gpu_side_stream_create(void** out) {
   hipStream_t s = nullptr;
   GELIM_TRY(gelim::side_stream_create(&s));
   *out = (void*)s;
+  return GELIM_OK;
+}
+
+// {least, greatest} stream priority of the current device
+extern "C" int gelim_gpu_stream_priority_range(int32_t* out) {
+  int least = 0, greatest = 0;
+  HIP_TRY(hipDeviceGetStreamPriorityRange(&least, &greatest));
+  out[0] = least;
+  out[1] = greatest;
   return GELIM_OK;
 }
 

@@ -146,6 +146,14 @@ __device__ __forceinline__ void store_buf(__amdgpu_buffer_rsrc_t r, uint32_t vof
   __builtin_amdgcn_raw_buffer_store_b64(x, r, (int)voff, (int)soff, 0);
 }
 
+// The same with sc1 (write-through): for payloads another workgroup of the
+// same launch reads (lu_panel.hip fused narrow update).
+__device__ __forceinline__ void store_buf_wt(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff, double v) {
+  const uint64_t b = (uint64_t)__double_as_longlong(v);
+  const wt_u32x2 x = {(unsigned)b, (unsigned)(b >> 32)};
+  __builtin_amdgcn_raw_buffer_store_b64(x, r, (int)voff, (int)soff, 16 /* sc1 */);
+}
+
 // Masked load without control flow: p must be a valid address (callers
 // clamp their indices), the value is selected afterwards.  Written as
 // `ok ? p[i] : 0`, LLVM turns each masked load into an exec-masked branch

@@ -363,7 +363,7 @@ struct Panel {
     if (Lout != nullptr) {
 #pragma unroll
       for (int i = 0; i < R; ++i)
-        dev::store_buf(lrs, (uint32_t)t * 8u, (uint32_t)(J * ldL + i * NT) * 8u, a[i][J]);
+        dev::store_buf_wt(lrs, (uint32_t)t * 8u, (uint32_t)(J * ldL + i * NT) * 8u, a[i][J]);
     }
     // 6. wave 0: step J of the LAPACK interchange replay (compact ids: rows
     //    < w keep their index, the row chosen at step j >= w is w + j; lane x
@@ -648,11 +648,13 @@ __device__ __forceinline__ void panel_body(double* __restrict__ P, int64_t ldp, 
       const bool emit = lane < 2 * w && !(lane >= w && selx < w) && ap != ar;
       const uint64_t mask = __ballot(emit);
       const int k = __popcll(mask & ((1ull << lane) - 1ull));
+      // agent-scope (sc1) stores: the fused narrow update reads them in the
+      // same launch, possibly from another XCD
       if (emit) {
-        pairs[1 + 2 * k] = ap;
-        pairs[2 + 2 * k] = ar;
+        __hip_atomic_store(pairs + 1 + 2 * k, ap, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(pairs + 2 + 2 * k, ar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
-      if (lane == 0) pairs[0] = __popcll(mask);
+      if (lane == 0) __hip_atomic_store(pairs, (int)__popcll(mask), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
   unsigned long long tr = 0;
@@ -693,7 +695,7 @@ __device__ __forceinline__ void panel_body(double* __restrict__ P, int64_t ldp, 
       if (lr < m && dest[i] != lr) {
 #pragma unroll
         for (int c = 0; c < W; ++c)
-          if (c < w) dev::store_buf(lrs, (uint32_t)dest[i] * 8u, (uint32_t)(c * ldL) * 8u, a[i][c]);
+          if (c < w) dev::store_buf_wt(lrs, (uint32_t)dest[i] * 8u, (uint32_t)(c * ldL) * 8u, a[i][c]);
       }
       if (lr < m && dest[i] < w) {
         const uint32_t ro = (uint32_t)((int64_t)dest[i] * ldp * 8);
@@ -758,6 +760,19 @@ __global__ __launch_bounds__(NT) void panel_kernel(double* __restrict__ P, int64
 constexpr int kStripCols = 16;
 constexpr int kStripMaxW = 16;
 
+struct NarrowArgs {
+  const double* C;  // strip: A + kp*lda + k (rows relative to kp)
+  int64_t ldc;
+  int ncols;        // strip width (next panel's w)
+  const double* L;  // step-j panel, column-major (ld ldl)
+  int64_t ldl;
+  int wp;           // step-j panel width
+  int m;            // n - kp
+  const int* pairs; // step-j row movement
+  double* out;      // buffer, column-major (rows relative to kp), ld ldo
+  int64_t ldo;
+};
+
 struct StepArgs {
   double* A;
   int64_t lda;
@@ -776,6 +791,13 @@ struct StepArgs {
   const double* lprev;         // the previous step's, same layout
   int ldL;                     // >= NT * R of every step (padding rows absorb the
                                // unconditional early stores)
+  // fused narrow update (nflags != null): nnar trailing workgroups apply
+  // THIS step to the next panel's strip (nar, as lu_narrow would) once the
+  // first wide workgroup has updated that strip (nflags[0]) and workgroup 0
+  // has factored the panel (nflags[1]) -- no separate narrow launch
+  unsigned* nflags;
+  int nwide, nnar;
+  NarrowArgs nar;
 };
 
 
@@ -941,6 +963,180 @@ __device__ __forceinline__ void strip_update(double* __restrict__ C, int64_t ldc
   mark(5);
 }
 
+// ---- narrow kernel ------------------------------------------------------------
+// Step j applied to the NEXT panel's column strip, spread over ceil(m/64)
+// workgroups (one 64-row slice each: 2048: 3.96 ms vs 3.99 with 128 and 4.03
+// with 256-row slices) instead of serialising it on the panel
+// workgroup.  A is only read; the updated strip (rows relative to the step-j
+// panel top, U12 rows first) goes to a side buffer that the next panel loads
+// directly, so the row interchanges need no cross-workgroup ordering.
+constexpr int kNarrowRows = 64;
+
+
+// Coherent loads for the fused narrow update (StepArgs::nflags): the strip,
+// the panel and its row movement were written by other workgroups of the
+// same launch (possibly on other XCDs) with write-through stores, so they are
+// read with agent-scope (sc1) loads; the narrow kernel reads plain.
+template <bool COH, typename T>
+__device__ __forceinline__ T ldc(const T* p) {
+  if constexpr (COH) {
+    if constexpr (sizeof(T) == 8) {
+      const unsigned long long v =
+          __hip_atomic_load(reinterpret_cast<const unsigned long long*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return __builtin_bit_cast(T, v);
+    } else {
+      const unsigned v = __hip_atomic_load(reinterpret_cast<const unsigned*>(p), __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+      return __builtin_bit_cast(T, v);
+    }
+  } else {
+    return *p;
+  }
+}
+template <bool COH, typename T>
+__device__ __forceinline__ T ldc_sel(const T* p, bool ok) {
+  const T v = ldc<COH>(p);
+  return ok ? v : T(0);
+}
+
+constexpr int kNarrowMaxRows = 128;
+struct alignas(16) NarrowLds {
+  double x[kStripMaxW][kStripCols];
+  double l11[kStripMaxW][kStripMaxW];
+  int pr[1 + 4 * kStripMaxW];
+  int srcmap[kNarrowMaxRows];
+};
+
+// Rows [r0, r0 + 16 * NT / 64) of the narrow update (one 16-row MFMA block
+// per wave), NT threads.
+template <int NT, bool COH>
+__device__ __forceinline__ void narrow_body(const NarrowArgs& g, int r0, NarrowLds& sh) {
+  constexpr int kRows = 16 * (NT / 64);
+  static_assert(kRows <= kNarrowMaxRows, "narrow slice");
+  const int t = threadIdx.x;
+  const __amdgpu_buffer_rsrc_t ors = dev::buffer_rsrc(g.out, (uint64_t)kStripCols * g.ldo * 8);
+  const int r1 = min(r0 + kRows, g.m);
+  const int wp = g.wp, ncols = g.ncols;
+  const int lane = t & 63, wave = t >> 6;
+  const int r16 = lane & 15, q = lane >> 4;
+  const bool ccol = r16 < ncols;
+  const int a0 = max(r0, wp);
+  const int nblk = (r1 - a0 + 15) >> 4;  // <= NT / 64
+  // Round trip 1 — everything that does not depend on the row movement is in
+  // flight together: pairs, L11, the top rows, this slice's multipliers and
+  // its strip rows at their own positions (unmoved rows: all but <= 2w).
+  dev::d4 acc;
+  double la[4];
+  if (t < 256) {
+    const int rr = t >> 4, cc = t & 15;
+    if (t < 1 + 4 * kStripMaxW) {
+      const int np = ldc<COH>(g.pairs);
+      sh.pr[t] = ldc_sel<COH>(g.pairs + t, t == 0 || t <= 2 * np);
+    }
+    sh.l11[rr][cc] = ldc_sel<COH>(g.L + (int64_t)min(cc, wp - 1) * g.ldl + min(rr, wp - 1), cc < rr && rr < wp);
+    sh.x[rr][cc] = ldc_sel<COH>(g.C + (int64_t)min(rr, wp - 1) * g.ldc + min(cc, ncols - 1), rr < wp && cc < ncols);
+  }
+  if (t < kRows) sh.srcmap[t] = r0 + t;
+  const int rbase = a0 + 16 * wave;
+  {
+    const int lrow = rbase + r16;
+    const bool okb = wave < nblk && lrow < r1;
+    const double* lp = g.L + min(lrow, r1 - 1);  // column-major L
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      la[e] = ldc_sel<COH>(lp + (int64_t)min(4 * q + e, wp - 1) * g.ldl, okb && 4 * q + e < wp);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = rbase + q + 4 * r;
+      const int rowc = min(max(row, r0), r1 - 1);
+      acc[r] = ldc_sel<COH>(g.C + (int64_t)rowc * g.ldc + min(r16, ncols - 1), wave < nblk && row < r1 && ccol);
+    }
+  }
+  __syncthreads();
+  const int np = sh.pr[0];
+  // round trip 2: post-swap top rows; source rows of this slice's permuted rows
+  for (int idx = t; idx < np * kStripCols; idx += NT) {
+    const int e = idx >> 4, cc = idx & 15;
+    const int d = sh.pr[1 + 2 * e];
+    if (d < wp) sh.x[d][cc] = ldc_sel<COH>(g.C + (int64_t)sh.pr[2 + 2 * e] * g.ldc + min(cc, ncols - 1), cc < ncols);
+  }
+  if (t < np) {
+    const int d = sh.pr[1 + 2 * t];
+    if (d >= r0 && d < r1) sh.srcmap[d - r0] = sh.pr[2 + 2 * t];
+  }
+  __syncthreads();
+  // the moved rows of this slice re-read their source (in flight under the TRSM)
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int row = rbase + q + 4 * r;
+    const int rowc = min(max(row, r0), r1 - 1);
+    const int src = sh.srcmap[rowc - r0];
+    if (src != rowc && wave < nblk && row < r1 && ccol) acc[r] = ldc<COH>(g.C + (int64_t)src * g.ldc + r16);
+  }
+  if (t < 256) {  // U12 = L11^-1 x: DPP row = one column
+    const int cc = t >> 4, j = t & 15;
+    double xv = sh.x[j][cc];
+    double lrow[kStripMaxW];
+#pragma unroll
+    for (int i = 0; i < kStripMaxW; ++i) lrow[i] = sh.l11[j][i];
+    trsm_dpp_steps(xv, lrow, j, std::make_integer_sequence<int, kStripMaxW>{});
+    sh.x[j][cc] = xv;
+    if (r0 == 0 && j < wp) dev::store_wt(ors, (uint32_t)(((int64_t)cc * g.ldo + j) * 8), xv);
+  }
+  __syncthreads();
+  // rows [max(r0, wp), r1): out[r] = A[src(r)] - L[r] U12 (MFMA, K permuted)
+  double b[4];
+#pragma unroll
+  for (int kk = 0; kk < 4; ++kk) b[kk] = sh.x[4 * q + kk][r16];
+#pragma unroll
+  for (int kk = 0; kk < 4; ++kk) {
+    const double a = (4 * q + kk < wp) ? -la[kk] : 0.0;
+    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b[kk], acc, 0, 0, 0);
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int row = rbase + q + 4 * r;
+    if (wave < nblk && row < r1) dev::store_wt(ors, (uint32_t)(((int64_t)r16 * g.ldo + row) * 8), acc[r]);
+  }
+}
+
+__global__ __launch_bounds__(256) void narrow_kernel(NarrowArgs g) {
+  __shared__ NarrowLds sh;
+  narrow_body<256, false>(g, blockIdx.x * kNarrowRows, sh);
+}
+
+// Hand-off inside one step launch (write-through recipe, rlu.hip): every
+// wave's stores drain, barrier, one lane sets the flag; the waiting workgroup
+// polls it relaxed (bounded: 200 ms, then code 11 in info[1]) and reads the
+// payload with sc1 loads.
+__device__ __forceinline__ void publish_flag(unsigned* f) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_store(f, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ bool wait_flags(unsigned* f, bool strip, int* info, NarrowLds& sh) {
+  if (threadIdx.x == 0) {
+    int ok = 1;
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    for (int i = strip ? 0 : 1; i < 2 && ok; ++i) {
+      while (__hip_atomic_load(f + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
+        if (__builtin_amdgcn_s_memrealtime() - t0 > 20000000ull) {  // 200 ms at 100 MHz
+          __hip_atomic_store(info + 1, 11, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          ok = 0;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+    }
+    sh.srcmap[0] = ok;
+  }
+  __syncthreads();
+  const bool ok = sh.srcmap[0] != 0;
+  __syncthreads();  // srcmap is reused by the slice
+  return ok;
+}
+
 template <int NT, int R, int W, int MODE, bool STAMP = false>
 __global__ __launch_bounds__(NT) void step_kernel(StepArgs g) {
   __shared__ PanelLds<W> sh;
@@ -962,6 +1158,7 @@ __global__ __launch_bounds__(NT) void step_kernel(StepArgs g) {
     panel_body<NT, R, W, MODE, STAMP>(g.A + (int64_t)g.k * lda + g.k, lda, g.n - g.k, g.w, g.k,
                                       g.piv + g.k, g.info, STAMP ? g.stamps + 700 : nullptr,
                                       g.pairs, sh, g.io, g.buf + g.wp, g.ldL, g.lout, g.ldL, true);
+    if (g.nflags) publish_flag(g.nflags + 1);
     if constexpr (STAMP) {
       __syncthreads();
       if (threadIdx.x == 0) {
@@ -982,6 +1179,7 @@ __global__ __launch_bounds__(NT) void step_kernel(StepArgs g) {
     panel_body<NT, R, W, MODE, false>(g.A + (int64_t)g.k * lda + g.k, lda, g.n - g.k, g.w, g.k,
                                       g.piv + g.k, g.info, nullptr, g.pairs, sh, g.io, nullptr, 0,
                                       g.lout, g.ldL);
+    if (g.nflags) publish_flag(g.nflags + 1);
     if constexpr (STAMP) {
       __syncthreads();
       if (threadIdx.x == 0) {
@@ -994,149 +1192,23 @@ __global__ __launch_bounds__(NT) void step_kernel(StepArgs g) {
     return;
   }
   const int wb = (int)(blockIdx.x - (has_panel ? 1 : 0));
+  if (g.nflags && wb >= g.nwide) {  // fused narrow slice
+    NarrowLds& nl = *reinterpret_cast<NarrowLds*>(g_panel_dyn_lds);
+    if (!wait_flags(g.nflags, g.wp > 0, g.info, nl)) return;
+    narrow_body<NT, true>(g.nar, (wb - g.nwide) * 16 * (NT / 64), nl);
+    return;
+  }
   const int c0 = g.wide_c0 + kStripCols * wb;
   const int ncols = min(kStripCols, g.n + 1 - c0);
   if (ncols <= 0) return;
   strip_update<NT>(g.A + (int64_t)g.kp * lda + c0, lda, ncols, g.lprev, g.ldL, g.wp, g.n - g.kp,
                    g.pairs_prev, ss);
+  if (g.nflags && wb == 0) publish_flag(g.nflags);  // the next panel's strip is up to date
   if constexpr (STAMP) {
     __syncthreads();
     if (threadIdx.x == 0) {
       g.stamps[8 + 2 * wb] = t0;
       g.stamps[9 + 2 * wb] = realtime_now();
-    }
-  }
-}
-
-// ---- narrow kernel ------------------------------------------------------------
-// Step j applied to the NEXT panel's column strip, spread over ceil(m/64)
-// workgroups (one 64-row slice each: 2048: 3.96 ms vs 3.99 with 128 and 4.03
-// with 256-row slices) instead of serialising it on the panel
-// workgroup.  A is only read; the updated strip (rows relative to the step-j
-// panel top, U12 rows first) goes to a side buffer that the next panel loads
-// directly, so the row interchanges need no cross-workgroup ordering.
-constexpr int kNarrowRows = 64;
-
-struct NarrowArgs {
-  const double* C;  // strip: A + kp*lda + k (rows relative to kp)
-  int64_t ldc;
-  int ncols;        // strip width (next panel's w)
-  const double* L;  // step-j panel, column-major (ld ldl)
-  int64_t ldl;
-  int wp;           // step-j panel width
-  int m;            // n - kp
-  const int* pairs; // step-j row movement
-  double* out;      // buffer, column-major (rows relative to kp), ld ldo
-  int64_t ldo;
-};
-
-__global__ __launch_bounds__(256) void narrow_kernel(NarrowArgs g) {
-  __shared__ double x[kStripMaxW][kStripCols];
-  __shared__ double l11[kStripMaxW][kStripMaxW];
-  __shared__ int pr[1 + 4 * kStripMaxW];
-  __shared__ int srcmap[kNarrowRows];
-  const int t = threadIdx.x;
-  const int r0 = blockIdx.x * kNarrowRows;
-  const __amdgpu_buffer_rsrc_t ors = dev::buffer_rsrc(g.out, (uint64_t)kStripCols * g.ldo * 8);
-  const int r1 = min(r0 + kNarrowRows, g.m);
-  const int wp = g.wp, ncols = g.ncols;
-  const int lane = t & 63, wave = t >> 6;
-  const int r16 = lane & 15, q = lane >> 4;
-  const bool ccol = r16 < ncols;
-  const int a0 = max(r0, wp);
-  const int nblk = (r1 - a0 + 15) >> 4;  // <= 16
-  // Round trip 1 — everything that does not depend on the row movement is in
-  // flight together: pairs, L11, the top rows, this slice's multipliers and
-  // its strip rows at their own positions (unmoved rows: all but <= 2w).
-  dev::d4 acc[4];
-  double la[4][4];
-  {
-    const int rr = t >> 4, cc = t & 15;
-    if (t < 1 + 4 * kStripMaxW) {
-      const int np = g.pairs[0];
-      pr[t] = dev::load_sel(g.pairs + t, t == 0 || t <= 2 * np);
-    }
-    l11[rr][cc] = dev::load_sel(g.L + (int64_t)min(cc, wp - 1) * g.ldl + min(rr, wp - 1),
-                                cc < rr && rr < wp);
-    x[rr][cc] = dev::load_sel(g.C + (int64_t)min(rr, wp - 1) * g.ldc + min(cc, ncols - 1),
-                              rr < wp && cc < ncols);
-    if (t < kNarrowRows) srcmap[t] = r0 + t;
-  }
-#pragma unroll
-  for (int s = 0; s < 4; ++s) {
-    const int blk = wave + 4 * s;
-    const int rbase = a0 + 16 * blk;
-    const int lrow = rbase + r16;
-    const bool okb = blk < nblk && lrow < r1;
-    const double* lp = g.L + min(lrow, r1 - 1);  // column-major L
-#pragma unroll
-    for (int e = 0; e < 4; ++e)
-      la[s][e] = dev::load_sel(lp + (int64_t)min(4 * q + e, wp - 1) * g.ldl, okb && 4 * q + e < wp);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int row = rbase + q + 4 * r;
-      const int rowc = min(max(row, r0), r1 - 1);
-      acc[s][r] = dev::load_sel(g.C + (int64_t)rowc * g.ldc + min(r16, ncols - 1),
-                                blk < nblk && row < r1 && ccol);
-    }
-  }
-  __syncthreads();
-  const int np = pr[0];
-  // round trip 2: post-swap top rows; source rows of this slice's permuted rows
-  for (int idx = t; idx < np * kStripCols; idx += 256) {
-    const int e = idx >> 4, cc = idx & 15;
-    const int d = pr[1 + 2 * e];
-    if (d < wp) x[d][cc] = dev::load_sel(g.C + (int64_t)pr[2 + 2 * e] * g.ldc + min(cc, ncols - 1), cc < ncols);
-  }
-  if (t < np) {
-    const int d = pr[1 + 2 * t];
-    if (d >= r0 && d < r1) srcmap[d - r0] = pr[2 + 2 * t];
-  }
-  __syncthreads();
-  // the moved rows of this slice re-read their source (in flight under the TRSM)
-#pragma unroll
-  for (int s = 0; s < 4; ++s) {
-    const int blk = wave + 4 * s;
-    const int rbase = a0 + 16 * blk;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int row = rbase + q + 4 * r;
-      const int rowc = min(max(row, r0), r1 - 1);
-      const int src = srcmap[rowc - r0];
-      if (src != rowc && blk < nblk && row < r1 && ccol)
-        acc[s][r] = g.C[(int64_t)src * g.ldc + r16];
-    }
-  }
-  {  // U12 = L11^-1 x: DPP row = one column
-    const int cc = t >> 4, j = t & 15;
-    double xv = x[j][cc];
-    double lrow[kStripMaxW];
-#pragma unroll
-    for (int i = 0; i < kStripMaxW; ++i) lrow[i] = l11[j][i];
-    trsm_dpp_steps(xv, lrow, j, std::make_integer_sequence<int, kStripMaxW>{});
-    x[j][cc] = xv;
-    if (r0 == 0 && j < wp) dev::store_wt(ors, (uint32_t)(((int64_t)cc * g.ldo + j) * 8), xv);
-  }
-  __syncthreads();
-  // rows [max(r0, wp), r1): out[r] = A[src(r)] - L[r] U12 (MFMA, K permuted)
-  double b[4];
-#pragma unroll
-  for (int kk = 0; kk < 4; ++kk) b[kk] = x[4 * q + kk][r16];
-#pragma unroll
-  for (int s = 0; s < 4; ++s)
-#pragma unroll
-    for (int kk = 0; kk < 4; ++kk) {
-      const double a = (4 * q + kk < wp) ? -la[s][kk] : 0.0;
-      acc[s] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b[kk], acc[s], 0, 0, 0);
-    }
-#pragma unroll
-  for (int s = 0; s < 4; ++s) {
-    const int blk = wave + 4 * s;
-    const int rbase = a0 + 16 * blk;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int row = rbase + q + 4 * r;
-      if (blk < nblk && row < r1) dev::store_wt(ors, (uint32_t)(((int64_t)r16 * g.ldo + row) * 8), acc[s][r]);
     }
   }
 }
@@ -1205,7 +1277,8 @@ int64_t lu_panel_buffer_ld(int64_t n) {
 
 int lu_step(double* A, int64_t lda, int64_t n, int64_t kp, int64_t wp, const int* pairs_prev,
             int64_t k, int64_t w, int mode, int* piv, int* info, int* pairs, hipStream_t s,
-            const double* buf, double* lout, const double* lprev, int64_t ldL) {
+            const double* buf, double* lout, const double* lprev, int64_t ldL, unsigned* nflags = nullptr,
+            double* nbuf = nullptr, int64_t nk = 0, int64_t nw = 0) {
   if (wp > kStripMaxW || w > 16) return GELIM_FAIL(GELIM_E_ARG, "lu_step: panel wider than 16");
   if (ldL < lu_panel_buffer_ld(n) || (w > 0 && !lout) || (wp > 0 && !lprev))
     return GELIM_FAIL(GELIM_E_ARG, "lu_step: panel buffers missing or too small");
@@ -1216,9 +1289,21 @@ int lu_step(double* A, int64_t lda, int64_t n, int64_t kp, int64_t wp, const int
   const int64_t c0 = (w > 0) ? k + w : k;
   a.wide_c0 = (int)c0;
   const int64_t nwide = (wp > 0) ? (n + 1 - c0 + kStripCols - 1) / kStripCols : 0;
-  const unsigned blocks = (unsigned)(nwide + (w > 0 ? 1 : 0));
-  if (blocks == 0) return GELIM_OK;
   const int64_t m = n - (w > 0 ? k : kp);
+  a.nflags = nullptr;
+  a.nwide = (int)nwide;
+  a.nnar = 0;
+  if (nflags && w > 0 && nw > 0) {
+    // fused narrow update of the next panel's strip [nk, nk + nw) (lu_narrow's
+    // arguments), one 128-row slice per trailing workgroup (NT = 512)
+    if (nw > kStripCols || nk != k + w || !nbuf)
+      return GELIM_FAIL(GELIM_E_ARG, "lu_step: fused narrow strip must follow the panel, width <= 16");
+    a.nflags = nflags;
+    a.nnar = (int)((m + 127) / 128);
+    a.nar = NarrowArgs{A + k * lda + nk, lda, (int)nw, lout, ldL, (int)w, (int)m, pairs, nbuf, ldL};
+  }
+  const unsigned blocks = (unsigned)(nwide + (w > 0 ? 1 : 0) + a.nnar);
+  if (blocks == 0) return GELIM_OK;
   if (m <= 512 && w <= 16) return launch_step<512, 1, 16>(a, mode, blocks, s);
   if (m <= 1024 && w <= 16) return launch_step<512, 2, 16>(a, mode, blocks, s);
   if (m <= 2048 && w <= 16) return launch_step<512, 4, 16>(a, mode, blocks, s);

@@ -21,7 +21,8 @@ int panel_factor(double* P, int64_t ldp, int64_t m, int64_t w, int64_t row0, int
 int64_t lu_panel_buffer_ld(int64_t n);
 int lu_step(double* A, int64_t lda, int64_t n, int64_t kp, int64_t wp, const int* pairs_prev,
             int64_t k, int64_t w, int mode, int* piv, int* info, int* pairs, hipStream_t s,
-            const double* buf, double* lout, const double* lprev, int64_t ldL);
+            const double* buf, double* lout, const double* lprev, int64_t ldL, unsigned* nflags = nullptr,
+            double* nbuf = nullptr, int64_t nk = 0, int64_t nw = 0);
 int lu_narrow(double* A, int64_t lda, int64_t n, int64_t kp, int64_t wp, const int* pairs,
               int64_t k, int64_t w, double* buf, hipStream_t s, const double* L, int64_t ldL);
 int pairs_trsm(double* C, int64_t ldc, int64_t ncols, const double* L, int64_t ldl, int64_t w,
@@ -106,7 +107,9 @@ struct gelim_gauss_plan {
   int64_t split = 0;                     // hybrid: fused steps for columns < split, then the
                                          // resident LU on the trailing (n - split) system
   void* rws = nullptr;                   // its hand-off workspace
-  double* sbuf = nullptr;                // narrow-kernel strip buffer (16 x ldL, column-major)
+  double* sbuf = nullptr;                // narrow-update strip buffers (2 x 16 x ldL, column-major, ping-pong)
+  bool narrow_fused = false;             // GELIM_NARROW_FUSED=1: the narrow update inside the step launch
+  unsigned* nflags = nullptr;            // fused narrow: 2 hand-off flags per step (zeroed per solve)
   double* lbuf = nullptr;                // fused steps: factored panels, column-major, ping-pong
   int64_t ldL = 0;                       //   (2 x 16 x ldL doubles)
   // wide-panel engine (n > big_tail): columns [0, big_k) are eliminated by
@@ -425,16 +428,23 @@ int enqueue(gelim_gauss_plan* p, const void* src, int64_t src_ld, void* dx, void
     // step i writes its factored panel to lbuf[i % 2]; step i + 1's trailing
     // updates and narrow(i) read it there
     auto lb = [&](size_t i) { return p->lbuf + (i & 1) * 16 * p->ldL; };
+    // narrow(i)'s output: read by step i + 1's panel workgroup while the fused
+    // narrow(i + 1) of that same launch writes the other buffer
+    auto sb = [&](size_t i) { return p->sbuf + (i & 1) * 16 * p->ldL; };
+    const bool fuse = nar && p->narrow_fused;
+    if (fuse) GELIM_TRY(zero_async(p->nflags, sizeof(unsigned) * 2 * (S + 1), s));
     for (size_t i = 0; i <= S; ++i) {
       const int64_t kp = i ? p->step_k[i - 1] : 0, wp = i ? p->step_w[i - 1] : 0;
       const int64_t k = i < S ? p->step_k[i] : kend, w = i < S ? p->step_w[i] : 0;
       const int* prev = i ? p->pairs + (i - 1) * kPairSlot : nullptr;
       int* cur = i < S ? p->pairs + i * kPairSlot : nullptr;
+      const bool nx = nar && i + 1 < S;  // a narrow update of panel i + 1's strip follows step i
       GELIM_TRY(lu_step(A, lda, n, kp, wp, prev, k, w, p->pivot, p->piv, p->info, cur, s,
-                        nar ? p->sbuf : nullptr, i < S ? lb(i) : nullptr, i ? lb(i - 1) : nullptr,
-                        p->ldL));
-      if (nar && i + 1 < S)
-        GELIM_TRY(lu_narrow(A, lda, n, k, w, cur, p->step_k[i + 1], p->step_w[i + 1], p->sbuf, s,
+                        nar && i ? sb(i - 1) : nullptr, i < S ? lb(i) : nullptr, i ? lb(i - 1) : nullptr,
+                        p->ldL, fuse && nx ? p->nflags + 2 * i : nullptr, sb(i), nx ? p->step_k[i + 1] : 0,
+                        nx ? p->step_w[i + 1] : 0));
+      if (nx && !fuse)
+        GELIM_TRY(lu_narrow(A, lda, n, k, w, cur, p->step_k[i + 1], p->step_w[i + 1], sb(i), s,
                             lb(i), p->ldL));
     }
     if (hyb) {
@@ -639,6 +649,7 @@ extern "C" gelim_gauss_plan* gelim_gauss_plan_create(int64_t n, int algo, int pi
   if (const char* e = std::getenv("GELIM_SCHEDULE")) p->fused = std::string(e) != "classic";
   if (p->lookahead) p->fused = false;
   if (const char* e = std::getenv("GELIM_NARROW")) p->narrow = std::atoi(e) != 0;
+  if (const char* e = std::getenv("GELIM_NARROW_FUSED")) p->narrow_fused = std::atoi(e) != 0;
   {
     // GELIM_SCHEDULE: auto (default) | resident | fused | classic.  auto =
     // the resident LU up to n = 1024 (R <= 2 register slots: measured 0.73
@@ -685,7 +696,9 @@ extern "C" gelim_gauss_plan* gelim_gauss_plan_create(int64_t n, int algo, int pi
         if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return fail("event");
     if (hipMalloc((void**)&p->pairs, sizeof(int) * kPairSlot * S) != hipSuccess) return fail("pairs");
     p->ldL = gelim::lu_panel_buffer_ld(n);
-    if (hipMalloc((void**)&p->sbuf, sizeof(double) * 16 * p->ldL) != hipSuccess) return fail("sbuf");
+    if (hipMalloc((void**)&p->sbuf, sizeof(double) * 2 * 16 * p->ldL) != hipSuccess) return fail("sbuf");
+    if (hipMalloc((void**)&p->nflags, sizeof(unsigned) * 2 * (p->step_k.size() + 1)) != hipSuccess)
+      return fail("nflags");
     if (hipMalloc((void**)&p->lbuf, sizeof(double) * 2 * 16 * p->ldL) != hipSuccess) return fail("lbuf");
     if (p->resident && hipMalloc(&p->rws, gelim::rlu_workspace_bytes(n)) != hipSuccess)
       return fail("resident LU workspace");
@@ -717,6 +730,7 @@ extern "C" void gelim_gauss_plan_destroy(gelim_gauss_plan* p) {
       if (e) (void)hipEventDestroy(e);
   (void)hipFree(p->pairs);
   (void)hipFree(p->sbuf);
+  (void)hipFree(p->nflags);
   (void)hipFree(p->lbuf);
   (void)hipFree(p->rws);
   (void)hipFree(p->work);

@@ -306,6 +306,159 @@ __global__ __launch_bounds__(16 * NB / TR) void diag_inv_kernel(const T* __restr
   if (!fin) atomicMin(info, k0 + 1);
 }
 
+// ---- two Gauss-Jordan steps per barrier ----------------------------------------
+// The same uniform rank-1 steps, paired: rows k, k+1 and columns k, k+1 of
+// the block are published raw (before step k) behind ONE barrier, and every
+// thread derives step k+1's operands itself -- column k+1 and row k+1 after
+// step k are one FMA each from the published values (c1_i = a_i,k+1 - g_i
+// u_k+1, r1_j = a_k+1,j - g_k+1 u_j, pivot a_k+1,k+1 - g_k+1 u_k+1), exactly
+// the FMAs their owners perform in the one-step form -- then applies
+// a -= g u^T + g' u'^T.  Every element sees the same operation sequence as
+// in diag_inv_kernel (bit-identical results) with half the barriers.
+template <typename TI>
+struct alignas(16) GjPairLds {
+  TI row[2][2][NB / kTl * kGjStride];  // [parity][row k / k+1]
+  TI col[2][2][NB / kTl * kGjStride];  // [parity][column k / k+1]
+};
+
+template <int TR, int KK>  // KK even: pair (k, k+1), k = 8 kg + KK
+__device__ __forceinline__ void gj_pair(double (&a)[TR][kTl], GjPairLds<double>& sh, int kg, int rg, int cg) {
+  static_assert(KK % 2 == 0 && TR % 2 == 0, "pairs of rows share a tile");
+  const int k = kTl * kg + KK;
+  constexpr int par = (KK / 2) & 1;  // kTl / 2 pairs per tile: even, so the parity is static
+  constexpr int RPG = kTl / TR;
+  const double akk = sh.row[par][0][gj_at(k)];
+  const double ak1 = sh.row[par][0][gj_at(k + 1)];  // a[k][k+1]
+  const double a1k = sh.row[par][1][gj_at(k)];      // a[k+1][k]
+  const double a11 = sh.row[par][1][gj_at(k + 1)];
+  const double pk = gj_recip(akk);
+  double u[kTl], g[TR], u1[kTl], g1[TR];
+#pragma unroll
+  for (int j = 0; j < kTl; j += 2) {
+    const double2 v = *reinterpret_cast<const double2*>(&sh.row[par][0][kGjStride * cg + j]);
+    const double2 w = *reinterpret_cast<const double2*>(&sh.row[par][1][kGjStride * cg + j]);
+    u[j] = v.x * pk;
+    u[j + 1] = v.y * pk;
+    u1[j] = w.x;
+    u1[j + 1] = w.y;
+  }
+#pragma unroll
+  for (int i = 0; i < TR; i += 2) {
+    const double2 v = *reinterpret_cast<const double2*>(&sh.col[par][0][gj_at(TR * rg) + i]);
+    const double2 w = *reinterpret_cast<const double2*>(&sh.col[par][1][gj_at(TR * rg) + i]);
+    g[i] = v.x;
+    g[i + 1] = v.y;
+    g1[i] = w.x;
+    g1[i + 1] = w.y;
+  }
+  const bool kcol = cg == kg;                   // columns k, k+1 are in this thread's tile
+  const bool krow = rg == RPG * kg + KK / TR;  // rows k, k+1 are
+  u[KK] = kcol ? 1.0 + pk : u[KK];
+  g[KK % TR] -= krow ? 1.0 : 0.0;
+  // step k applied to column k+1 (rows of this tile), row k+1 (columns of
+  // this tile) and the next pivot
+  const double uk1 = ak1 * pk;  // u[k+1]
+  const double gk1 = a1k;       // g[k+1]
+#pragma unroll
+  for (int i = 0; i < TR; ++i) g1[i] = fma(-g[i], uk1, g1[i]);
+#pragma unroll
+  for (int j = 0; j < kTl; ++j) u1[j] = fma(-gk1, u[j], u1[j]);
+  const double pk1 = gj_recip(fma(-gk1, uk1, a11));
+#pragma unroll
+  for (int j = 0; j < kTl; ++j) u1[j] *= pk1;
+  u1[KK + 1] = kcol ? 1.0 + pk1 : u1[KK + 1];
+  g1[(KK + 1) % TR] -= krow ? 1.0 : 0.0;
+  // the next pair's rows / columns first, published raw
+  constexpr int KN = (KK + 2) % kTl;
+  constexpr int rn = KN % TR;
+  const int kgn = KK + 2 == kTl ? kg + 1 : kg;
+  const int rgn = (k + 2) / TR;
+  const bool more = k + 2 < NB;
+#pragma unroll
+  for (int j = 0; j < kTl; ++j) {
+    a[rn][j] = fma(-g1[rn], u1[j], fma(-g[rn], u[j], a[rn][j]));
+    a[rn + 1][j] = fma(-g1[rn + 1], u1[j], fma(-g[rn + 1], u[j], a[rn + 1][j]));
+  }
+#pragma unroll
+  for (int i = 0; i < TR; ++i)
+    if (i != rn && i != rn + 1) {
+      a[i][KN] = fma(-g1[i], u1[KN], fma(-g[i], u[KN], a[i][KN]));
+      a[i][KN + 1] = fma(-g1[i], u1[KN + 1], fma(-g[i], u[KN + 1], a[i][KN + 1]));
+    }
+  if (more && rg == rgn) {
+#pragma unroll
+    for (int j = 0; j < kTl; j += 2) {
+      *reinterpret_cast<double2*>(&sh.row[par ^ 1][0][kGjStride * cg + j]) = make_double2(a[rn][j], a[rn][j + 1]);
+      *reinterpret_cast<double2*>(&sh.row[par ^ 1][1][kGjStride * cg + j]) =
+          make_double2(a[rn + 1][j], a[rn + 1][j + 1]);
+    }
+  }
+  if (more && cg == kgn) {
+#pragma unroll
+    for (int i = 0; i < TR; i += 2) {
+      *reinterpret_cast<double2*>(&sh.col[par ^ 1][0][gj_at(TR * rg) + i]) = make_double2(a[i][KN], a[i + 1][KN]);
+      *reinterpret_cast<double2*>(&sh.col[par ^ 1][1][gj_at(TR * rg) + i]) =
+          make_double2(a[i][KN + 1], a[i + 1][KN + 1]);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < TR; ++i)
+#pragma unroll
+    for (int j = 0; j < kTl; ++j)
+      if (i != rn && i != rn + 1 && j != KN && j != KN + 1)
+        a[i][j] = fma(-g1[i], u1[j], fma(-g[i], u[j], a[i][j]));
+  __syncthreads();
+}
+
+template <int TR, int... KK>
+__device__ __forceinline__ void gj_pairs(double (&a)[TR][kTl], GjPairLds<double>& sh, int kg, int rg, int cg,
+                                         std::integer_sequence<int, KK...>) {
+  (gj_pair<TR, 2 * KK>(a, sh, kg, rg, cg), ...);
+}
+
+template <int TR>
+__global__ __launch_bounds__(16 * NB / TR) void diag_inv_pair_kernel(const double* __restrict__ Ablk, int64_t lda,
+                                                                    int k0, double* __restrict__ Dinv,
+                                                                    int* __restrict__ info) {
+  __shared__ GjPairLds<double> sh;
+  const int t = threadIdx.x, rg = t >> 4, cg = t & 15;
+  double a[TR][kTl];
+#pragma unroll
+  for (int i = 0; i < TR; ++i) {
+    const double* src = Ablk + (int64_t)(TR * rg + i) * lda + kTl * cg;
+#pragma unroll
+    for (int j = 0; j < kTl; ++j) a[i][j] = src[j];
+  }
+  if (rg == 0) {
+#pragma unroll
+    for (int j = 0; j < kTl; ++j) {
+      sh.row[0][0][kGjStride * cg + j] = a[0][j];
+      sh.row[0][1][kGjStride * cg + j] = a[1][j];
+    }
+  }
+  if (cg == 0) {
+#pragma unroll
+    for (int i = 0; i < TR; ++i) {
+      sh.col[0][0][gj_at(TR * rg) + i] = a[i][0];
+      sh.col[0][1][gj_at(TR * rg) + i] = a[i][1];
+    }
+  }
+  __syncthreads();
+  for (int kg = 0; kg < NB / kTl; ++kg)
+    gj_pairs<TR>(a, sh, kg, rg, cg, std::make_integer_sequence<int, kTl / 2>{});
+  bool fin = true;
+#pragma unroll
+  for (int i = 0; i < TR; ++i) {
+    double* dst = Dinv + (int64_t)(TR * rg + i) * NB + kTl * cg;
+#pragma unroll
+    for (int j = 0; j < kTl; ++j) {
+      fin = fin && isfinite(a[i][j]);
+      dst[j] = a[i][j];
+    }
+  }
+  if (!fin) atomicMin(info, k0 + 1);
+}
+
 // ---- blocked Gauss-Jordan inverse on the matrix cores ------------------------
 // The same inverse, blocked: block steps of KB = 32 (or 16) pivots.  The 128 x 128
 // block lives in LDS (133 KB of the CU's 160 KB); per block step b (rows /
@@ -516,6 +669,14 @@ int block_inv(const double* Ablk, int64_t lda, int64_t col, double* Di, int* inf
   }
   const char* e = std::getenv("GELIM_GJ_TR");  // read per launch (tests switch it)
   const int tr = e && (std::atoi(e) == 8 || std::atoi(e) == 2) ? std::atoi(e) : 4;
+  // two Gauss-Jordan steps per barrier (bit-identical): 57.0 vs 58.6 us per
+  // block alone (profiles/gj_pair_r4.txt); GELIM_GJ_PAIR=0 for one per barrier
+  const char* ep = std::getenv("GELIM_GJ_PAIR");
+  if (tr == 4 && !(ep && std::atoi(ep) == 0)) {
+    hipLaunchKernelGGL((diag_inv_pair_kernel<4>), dim3(1), dim3(16 * NB / 4), 0, s, Ablk, lda, (int)col, Di, info);
+    HIP_TRY(hipGetLastError());
+    return GELIM_OK;
+  }
   if (tr == 2)
     hipLaunchKernelGGL((diag_inv_kernel<double, 2>), dim3(1), dim3(16 * NB / 2), 0, s, Ablk, lda, (int)col, Di,
                        (double*)nullptr, info);

@@ -299,3 +299,43 @@ def test_rbt_with_blocked_inverse(gelim, cuda, monkeypatch, n, form):
     assert s.last_steps <= 4
     assert gelim.ops.gauss.error_metric(x) < 1e-8
     s.close()
+
+
+@pytest.mark.parametrize("kind", ["dominant", "rbt_like"])
+def test_block_inverse_pairs_bitwise(gelim, cuda, monkeypatch, kind):
+    """Two Gauss-Jordan steps per barrier (GELIM_GJ_PAIR=1) perform every
+    element's FMAs in the one-step order: the inverse is bit-identical; a
+    zero pivot block is reported through info."""
+    from gelim.utils.tensors import ptr, stream_handle
+
+    lib = gelim._native.lib()
+    g = torch.Generator(device="cpu").manual_seed(11 + len(kind))
+    A = torch.randn(128, 128, generator=g, dtype=torch.float64)
+    if kind == "dominant":
+        A += 64 * torch.eye(128, dtype=torch.float64)
+    else:
+        Q, _ = torch.linalg.qr(torch.randn(128, 128, generator=g, dtype=torch.float64))
+        A = Q @ torch.diag(torch.logspace(0, 4, 128, dtype=torch.float64)) @ Q.T + 0.1 * A
+    big = torch.zeros(160, 140, dtype=torch.float64)
+    big[7:135, 9:137] = A
+    bg = big.to(cuda)
+    blk = bg[7:135, 9:137]
+    out = {}
+    for pair in ("0", "1"):
+        monkeypatch.setenv("GELIM_GJ_PAIR", pair)
+        D = torch.full((128, 128), float("nan"), dtype=torch.float64, device=cuda)
+        info = torch.full((1,), 0x7F7F7F7F, dtype=torch.int32, device=cuda)
+        gelim._native.check(lib.gelim_rbt_block_inverse(ptr(blk), bg.stride(0), 0, ptr(D), ptr(info),
+                                                        stream_handle(cuda)), "block_inverse")
+        torch.cuda.synchronize()
+        assert info.item() == 0x7F7F7F7F
+        out[pair] = D.cpu()
+    assert torch.equal(out["0"], out["1"])
+    assert (out["1"] @ A - torch.eye(128, dtype=torch.float64)).abs().max().item() < 1e-12 * torch.linalg.cond(A).item()
+    Z = torch.zeros(128, 128, dtype=torch.float64, device=cuda)
+    D = torch.empty(128, 128, dtype=torch.float64, device=cuda)
+    info = torch.full((1,), 0x7F7F7F7F, dtype=torch.int32, device=cuda)
+    gelim._native.check(lib.gelim_rbt_block_inverse(ptr(Z), 128, 384, ptr(D), ptr(info), stream_handle(cuda)),
+                        "block_inverse")
+    torch.cuda.synchronize()
+    assert info.item() == 385

@@ -672,8 +672,11 @@ int block_inv(const double* Ablk, int64_t lda, int64_t col, double* Di, int* inf
   // two Gauss-Jordan steps per barrier (bit-identical): 57.0 vs 58.6 us per
   // block alone (profiles/gj_pair_r4.txt); GELIM_GJ_PAIR=0 for one per barrier
   const char* ep = std::getenv("GELIM_GJ_PAIR");
-  if (tr == 4 && !(ep && std::atoi(ep) == 0)) {
-    hipLaunchKernelGGL((diag_inv_pair_kernel<4>), dim3(1), dim3(16 * NB / 4), 0, s, Ablk, lda, (int)col, Di, info);
+  if ((tr == 4 || tr == 2) && !(ep && std::atoi(ep) == 0)) {
+    if (tr == 4)
+      hipLaunchKernelGGL((diag_inv_pair_kernel<4>), dim3(1), dim3(16 * NB / 4), 0, s, Ablk, lda, (int)col, Di, info);
+    else
+      hipLaunchKernelGGL((diag_inv_pair_kernel<2>), dim3(1), dim3(16 * NB / 2), 0, s, Ablk, lda, (int)col, Di, info);
     HIP_TRY(hipGetLastError());
     return GELIM_OK;
   }

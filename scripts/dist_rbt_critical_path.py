@@ -23,7 +23,7 @@ Setup: the butterfly transform (local) and the all_gather of the super-blocks
 import sys
 
 # measured on one MI355X (us); profiles/dist_rbt_8rank_critical_path.md
-T_INV = 58.3                       # 128 x 128 Gauss-Jordan inverse (one workgroup)
+T_INV = 57.0                       # 128 x 128 Gauss-Jordan inverse (one workgroup, two steps per barrier)
 T_SS = {1: 8.3, 2: 12.1, 4: 19.2, 8: 34.4}   # persistent block solve of P blocks
 T_GEMV = 4.6                       # 8192 x 128 local GEMV
 T_PACK_8192 = 8.1                  # column pack, 8192 x 128 (8.4 MB)

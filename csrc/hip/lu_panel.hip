@@ -1029,10 +1029,9 @@ __device__ __forceinline__ void narrow_body(const NarrowArgs& g, int r0, NarrowL
   double la[4];
   if (t < 256) {
     const int rr = t >> 4, cc = t & 15;
-    if (t < 1 + 4 * kStripMaxW) {
-      const int np = ldc<COH>(g.pairs);
-      sh.pr[t] = ldc_sel<COH>(g.pairs + t, t == 0 || t <= 2 * np);
-    }
+    // the whole pair slot in one round trip (entries past 2 * pairs[0] are
+    // never used), not pairs[0] first and the pairs behind it
+    if (t < 1 + 4 * kStripMaxW) sh.pr[t] = ldc<COH>(g.pairs + t);
     sh.l11[rr][cc] = ldc_sel<COH>(g.L + (int64_t)min(cc, wp - 1) * g.ldl + min(rr, wp - 1), cc < rr && rr < wp);
     sh.x[rr][cc] = ldc_sel<COH>(g.C + (int64_t)min(rr, wp - 1) * g.ldc + min(cc, ncols - 1), rr < wp && cc < ncols);
   }

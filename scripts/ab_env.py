@@ -1,4 +1,4 @@
-"""A/B timing of per-launch environment knobs (GELIM_PANEL_NT, GELIM_PANEL_IO,
+"""A/B timing of per-launch environment knobs (GELIM_PANEL_IO, GELIM_NARROW,
 ...) on the fused blocked-LU solve, interleaved in ONE process, eager launches.
 
   python scripts/ab_env.py N 'NAME:VAR=V,VAR=V' 'NAME:VAR=V' ...

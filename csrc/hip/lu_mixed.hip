@@ -1312,9 +1312,25 @@ extern "C" gelim_mixed_plan* gelim_mixed_plan_create2(int64_t n, const double* u
     int reserve = 0;
     if (const char* e = std::getenv("GELIM_RBT_RESERVE")) reserve = std::max(0, std::atoi(e));
     p->cap = reserve == 0 ? 0 : ncu > reserve + 8 ? ncu - reserve : std::max(8, ncu / 2);
-    if (gelim::side_stream_create(&p->side) != GELIM_OK) return fail("side stream");
-    if (std::getenv("GELIM_CRIT_PRIO")) {
-      if (gelim::side_stream_create(&p->crit, 1) != GELIM_OK) return fail("critical stream");
+    // GELIM_RBT_MASK=<k>: the side stream's GEMMs stay off k CUs (CU-masked
+    // queue; GELIM_RBT_MASK_SPREAD=0 takes the lowest-numbered CUs) and the
+    // chain runs on a stream of its own, so its thin GEMMs and inverses
+    // always find free CUs
+    int mask = 0, spread = 1;
+    if (const char* e = std::getenv("GELIM_RBT_MASK")) mask = std::max(0, std::atoi(e));
+    if (const char* e = std::getenv("GELIM_RBT_MASK_SPREAD")) spread = std::atoi(e) != 0;
+    if (mask > 0) {
+      if (gelim::masked_stream_create(&p->side, mask, spread) != GELIM_OK) return fail("masked side stream");
+    } else if (gelim::side_stream_create(&p->side) != GELIM_OK) {
+      return fail("side stream");
+    }
+    if (mask > 0 || std::getenv("GELIM_CRIT_PRIO")) {
+      const char* ec = std::getenv("GELIM_RBT_MASK_CRIT");  // 1: the chain on the reserved CUs alone
+      if (mask > 0 && ec && std::atoi(ec) != 0) {
+        if (gelim::masked_stream_create(&p->crit, mask, spread, true) != GELIM_OK) return fail("critical stream");
+      } else if (gelim::side_stream_create(&p->crit, 1) != GELIM_OK) {
+        return fail("critical stream");
+      }
       if (hipEventCreateWithFlags(&p->ef, hipEventDisableTiming) != hipSuccess) return fail("event");
       if (hipEventCreateWithFlags(&p->ej, hipEventDisableTiming) != hipSuccess) return fail("event");
     }

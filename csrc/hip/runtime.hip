@@ -287,6 +287,32 @@ int side_stream_create(hipStream_t* out, int kind) {
 
 }  // namespace gelim
 
+namespace gelim {
+// A stream whose kernels may run on every CU but `reserve` of them, which
+// stay free for the other streams' work (a CU mask is a property of the
+// hardware queue behind the stream).  spread = 1 reserves every
+// (ncu / reserve)-th CU -- the same count in every XCD whichever way the
+// mask bits map onto them -- 0 the lowest-numbered ones.  only = true: the
+// stream runs on the reserved CUs alone.
+int masked_stream_create(hipStream_t* out, int reserve, int spread, bool only) {
+  *out = nullptr;
+  int dev = 0, ncu = 0;
+  HIP_TRY(hipGetDevice(&dev));
+  HIP_TRY(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+  if (reserve <= 0 || reserve >= ncu) return GELIM_FAIL(GELIM_E_ARG, "masked stream: reserve out of range");
+  std::vector<uint32_t> mask((size_t)(ncu + 31) / 32, 0u);
+  const int step = std::max(1, ncu / reserve);
+  int held = 0;
+  for (int c = 0; c < ncu; ++c) {
+    const bool res = spread ? (c % step == 0 && held < reserve) : c < reserve;
+    held += res ? 1 : 0;
+    if (res == only) mask[(size_t)c / 32] |= 1u << (c % 32);
+  }
+  HIP_TRY(hipExtStreamCreateWithCUMask(out, (uint32_t)mask.size(), mask.data()));
+  return GELIM_OK;
+}
+}  // namespace gelim
+
 // A non-blocking stream that runs concurrently with the default stream
 // (probed; see side_stream_create).  Destroy with gelim_gpu_stream_destroy.
 extern "C" int gelim_gpu_side_stream_create(void** out) {

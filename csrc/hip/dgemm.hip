@@ -77,6 +77,7 @@ struct Args {
   double alpha;
   int acc;  // 1: C += alpha A B, 0: C = alpha A B (C is not read)
   int group;  // tile order: runs of `group` tile rows, column-major inside a run (<= 1: row-major)
+  int wt;     // 1: C stored write-through (agent-scope sc1 stores: no dirty L2 left for the next launch boundary)
 };
 
 // Tile index -> (tile row, tile column).  Grouped order: the 64 workgroups an
@@ -226,7 +227,15 @@ __device__ __forceinline__ void tile_body(const Args& g, int m0, int n0, double*
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int row = m0 + wm + 16 * i + q + 4 * r;
-        if (store && (FULL || (row < g.M && col < g.N))) g.C[(int64_t)row * g.ldc + col] = acc[i][j][r];
+        if (store && (FULL || (row < g.M && col < g.N))) {
+          double* cp = g.C + (int64_t)row * g.ldc + col;
+          if (g.wt)
+            __hip_atomic_store(reinterpret_cast<unsigned long long*>(cp),
+                               (unsigned long long)__double_as_longlong(acc[i][j][r]), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+          else
+            *cp = acc[i][j][r];
+        }
       }
     }
 }
@@ -307,7 +316,11 @@ int dgemm_launch(double* C, int64_t ldc, const double* A, int64_t lda, const dou
     return e ? std::atoi(e) : 1;  // grouped orders 4 / 8 / 16 measured within noise of row-major
   }();
   const int group = group_arg >= 0 ? group_arg : group_env;
-  Args g{C, ldc, A, lda, B, ldb, (int)M, (int)N, (int)K, tn, tm * tn, alpha, accumulate ? 1 : 0, group};
+  static const int wt = [] {
+    const char* e = std::getenv("GELIM_DGEMM_WT");
+    return e ? std::atoi(e) != 0 : 0;
+  }();
+  Args g{C, ldc, A, lda, B, ldb, (int)M, (int)N, (int)K, tn, tm * tn, alpha, accumulate ? 1 : 0, group, wt};
   // max_wg > 0: at most max_wg CUs (rounded down to a multiple of 8)
   const int cap = max_wg > 0 ? std::max(8, max_wg / 8 * 8) : 0;
   // few tiles: one 256-thread workgroup per tile already stays within the

@@ -14,11 +14,27 @@
 namespace gelim {
 namespace {
 
+// wt = 1: write-through (agent-scope sc1) stores, so the launch boundary
+// after the copy has no dirty L2 to write back (GELIM_COPY_WT)
 __global__ __launch_bounds__(256) void copy2d_words_kernel(unsigned* __restrict__ d, int64_t dp,
-                                                          const unsigned* __restrict__ sp, int64_t spp, int64_t w) {
+                                                          const unsigned* __restrict__ sp, int64_t spp, int64_t w,
+                                                          int wt) {
   const unsigned* srow = sp + (int64_t)blockIdx.y * spp;
   unsigned* drow = d + (int64_t)blockIdx.y * dp;
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < w; i += (int64_t)gridDim.x * 256) drow[i] = srow[i];
+  if (wt) {
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < w; i += (int64_t)gridDim.x * 256)
+      __hip_atomic_store(drow + i, srow[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  } else {
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < w; i += (int64_t)gridDim.x * 256) drow[i] = srow[i];
+  }
+}
+
+int copy_wt() {
+  static const int v = [] {
+    const char* e = std::getenv("GELIM_COPY_WT");
+    return e ? std::atoi(e) != 0 : 0;
+  }();
+  return v;
 }
 
 // r[i] = aug[i][n] - sum_j aug[i][j] x[j] (fp64; one wave per row); with
@@ -123,7 +139,7 @@ int copy2d_async(void* dst, size_t dpitch, const void* src, size_t spitch, size_
     const size_t nr = std::min<size_t>(65535, rows - r);
     hipLaunchKernelGGL(copy2d_words_kernel, dim3(bx, (unsigned)nr), dim3(256), 0, s,
                        static_cast<unsigned*>(dst) + r * (dpitch / 4), (int64_t)(dpitch / 4),
-                       static_cast<const unsigned*>(src) + r * (spitch / 4), (int64_t)(spitch / 4), w);
+                       static_cast<const unsigned*>(src) + r * (spitch / 4), (int64_t)(spitch / 4), w, copy_wt());
     HIP_TRY(hipGetLastError());
   }
   return GELIM_OK;

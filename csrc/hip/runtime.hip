@@ -225,21 +225,44 @@ __global__ void probe_set_kernel(int* w) {
 }
 
 std::mutex g_park_mu;
-std::vector<hipStream_t> g_parked;  // streams that shared the default stream's queue
-int g_side_stats[2] = {0, 0};       // {probed streams, parked streams} (diagnostics)
+// Streams that shared a queue with the stream they were probed against.  They
+// stay alive while parked (so the runtime does not hand their queue out
+// again during the same search) and are offered first to the next search;
+// the pool is capped, past the cap a failed stream is destroyed.
+constexpr size_t kParkCap = 12;
+std::vector<hipStream_t> g_parked;
+int g_side_stats[2] = {0, 0};  // {probed streams, streams found sharing a queue} (diagnostics)
 
-// 1: side runs concurrently with the default stream, 0: it does not, < 0: error
-int probe_concurrent(hipStream_t side, int* w) {
+// 1: `setter` runs concurrently with `waiter`, 0: it does not (they share a
+// hardware queue), < 0: error
+int probe_pair(hipStream_t waiter, hipStream_t setter, int* w) {
   int h[2] = {0, 0};
-  HIP_TRY(hipMemsetAsync(w, 0, 2 * sizeof(int), nullptr));
-  HIP_TRY(hipStreamSynchronize(nullptr));
-  hipLaunchKernelGGL(probe_wait_kernel, dim3(1), dim3(64), 0, nullptr, w, kProbeTicks);
-  hipLaunchKernelGGL(probe_set_kernel, dim3(1), dim3(64), 0, side, w);
+  HIP_TRY(hipMemsetAsync(w, 0, 2 * sizeof(int), waiter));
+  HIP_TRY(hipStreamSynchronize(waiter));
+  hipLaunchKernelGGL(probe_wait_kernel, dim3(1), dim3(64), 0, waiter, w, kProbeTicks);
+  hipLaunchKernelGGL(probe_set_kernel, dim3(1), dim3(64), 0, setter, w);
   HIP_TRY(hipGetLastError());
-  HIP_TRY(hipStreamSynchronize(side));
-  HIP_TRY(hipStreamSynchronize(nullptr));
+  HIP_TRY(hipStreamSynchronize(setter));
+  HIP_TRY(hipStreamSynchronize(waiter));
   HIP_TRY(hipMemcpy(h, w, sizeof(h), hipMemcpyDeviceToHost));
   return h[1] == 1 ? 1 : 0;
+}
+
+// 1 when s runs beside the default stream AND beside every stream of
+// others[0..nothers), 0 when it shares a queue with one of them
+int probe_all(hipStream_t s, hipStream_t const* others, int nothers, int* w) {
+  int ok = probe_pair(nullptr, s, w);
+  for (int i = 0; ok == 1 && i < nothers; ++i)
+    if (others[i]) ok = probe_pair(others[i], s, w);
+  return ok;
+}
+
+void park(hipStream_t s) {
+  if (g_parked.size() < kParkCap) {
+    g_parked.push_back(s);
+  } else {
+    (void)hipStreamDestroy(s);
+  }
 }
 }  // namespace
 
@@ -272,7 +295,10 @@ int stream_priority(int kind) {
   return std::max(greatest, std::min(least, v));
 }
 
-int side_stream_create(hipStream_t* out, int kind) {
+// A stream concurrent with the default stream and with others[0..nothers):
+// parked streams of earlier searches are tried first (priority 0 only: a
+// parked stream has the default priority), then up to 8 new ones.
+int probed_stream_create(hipStream_t* out, int kind, hipStream_t const* others, int nothers) {
   *out = nullptr;
   const int prio = stream_priority(kind);
   if (!probe_enabled()) {
@@ -282,6 +308,19 @@ int side_stream_create(hipStream_t* out, int kind) {
   std::lock_guard<std::mutex> lk(g_park_mu);  // one probe at a time (shared words)
   int* w = nullptr;
   GELIM_TRY(probe_words(&w));
+  if (prio == 0) {
+    for (size_t i = 0; i < g_parked.size(); ++i) {
+      const int ok = probe_all(g_parked[i], others, nothers, w);
+      ++g_side_stats[0];
+      if (ok < 0) return ok;
+      if (ok == 1) {
+        *out = g_parked[i];
+        g_parked.erase(g_parked.begin() + (ptrdiff_t)i);
+        return GELIM_OK;
+      }
+      ++g_side_stats[1];
+    }
+  }
   hipStream_t s = nullptr;
   int rc = GELIM_OK;
   for (int attempt = 0; attempt < 8; ++attempt) {
@@ -290,16 +329,18 @@ int side_stream_create(hipStream_t* out, int kind) {
       s = nullptr;
       break;
     }
-    const int ok = probe_concurrent(s, w);
+    const int ok = probe_all(s, others, nothers, w);
     ++g_side_stats[0];
     if (ok != 0 || attempt == 7) break;  // concurrent, an error (keep the stream), or out of tries
     ++g_side_stats[1];
-    g_parked.push_back(s);
+    park(s);
     s = nullptr;
   }
   *out = s;
   return s ? GELIM_OK : rc;
 }
+
+int side_stream_create(hipStream_t* out, int kind) { return probed_stream_create(out, kind, nullptr, 0); }
 
 }  // namespace gelim
 
@@ -360,12 +401,40 @@ extern "C" int gelim_gpu_stream_probe(void* stream) {
   std::lock_guard<std::mutex> lk(gelim::g_park_mu);
   int* w = nullptr;
   GELIM_TRY(gelim::probe_words(&w));
-  const int ok = gelim::probe_concurrent((hipStream_t)stream, w);
+  const int ok = gelim::probe_pair(nullptr, (hipStream_t)stream, w);
   if (ok >= 0) {
     ++gelim::g_side_stats[0];
     if (ok == 0) ++gelim::g_side_stats[1];
   }
   return ok;
+}
+
+// A new non-blocking stream that runs concurrently with the default stream
+// and with each of others[0..nothers) (null entries skipped): the streams a
+// rank keeps busy at once -- main, the lookahead side stream and the stream
+// its collectives run on -- each on a hardware queue of its own.
+extern "C" int gelim_gpu_stream_create_probed(void** out, void* const* others, int32_t nothers) {
+  if (nothers < 0 || nothers > 16) return GELIM_FAIL(GELIM_E_ARG, "stream_create_probed: nothers");
+  hipStream_t s = nullptr;
+  GELIM_TRY(gelim::probed_stream_create(&s, 0, (hipStream_t const*)others, nothers));
+  *out = (void*)s;
+  return GELIM_OK;
+}
+
+// One half of a concurrency probe on caller-chosen streams and words (two
+// ints, zeroed by the caller): role 0 launches the bounded waiter (words[1]
+// becomes 1 if it saw words[0] set within `ticks` 100 MHz ticks, else 2),
+// role 1 the setter.  Used to check that a collective queued on one stream
+// does not serialise behind a kernel on another (parallel/comm.py).
+extern "C" int gelim_gpu_probe_kernel(void* stream, int32_t* words, int32_t role, int64_t ticks) {
+  if (role == 0) {
+    hipLaunchKernelGGL(gelim::probe_wait_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, words,
+                       (unsigned long long)std::max<int64_t>(1, ticks));
+  } else {
+    hipLaunchKernelGGL(gelim::probe_set_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, words);
+  }
+  HIP_TRY(hipGetLastError());
+  return GELIM_OK;
 }
 
 // {streams probed, streams that shared the default stream's queue}

@@ -61,6 +61,8 @@ _PROTOS = {
     "gelim_gpu_side_stream_create": (_int, [C.POINTER(C.c_void_p)]),
     "gelim_gpu_stream_destroy": (_int, [_vp]),
     "gelim_gpu_stream_probe": (_int, [_vp]),
+    "gelim_gpu_stream_create_probed": (_int, [C.POINTER(C.c_void_p), _vp, _i32]),
+    "gelim_gpu_probe_kernel": (_int, [_vp, _vp, _i32, _i64]),
     "gelim_gpu_stream_priority_range": (_int, [_vp]),
     "gelim_gpu_side_stream_stats": (None, [_vp]),
     "gelim_gpu_init_synthetic": (_int, [_vp, _i64, _i64, _vp]),

@@ -19,7 +19,7 @@ from __future__ import annotations
 
 import datetime
 import os
-from dataclasses import dataclass
+from dataclasses import dataclass, field
 
 import torch
 import torch.distributed as dist
@@ -53,6 +53,21 @@ class _Staged:
         return self.work.is_completed()
 
 
+class _Event:
+    """Handle of a collective issued on the communicator's own stream:
+    wait() makes the CURRENT stream wait for it (no host block)."""
+
+    def __init__(self, ev: torch.cuda.Event):
+        self.ev = ev
+
+    def wait(self) -> bool:
+        torch.cuda.current_stream().wait_event(self.ev)
+        return True
+
+    def is_completed(self) -> bool:
+        return self.ev.query()
+
+
 @dataclass
 class Communicator:
     rank: int = 0
@@ -60,11 +75,51 @@ class Communicator:
     device: torch.device = torch.device("cpu")
     backend: str = "none"
     group: object = None
+    # a torch.distributed group is live even at ONE rank (init_from_env
+    # force_pg / GELIM_FORCE_PG=1): every collective then really goes through
+    # the backend (RCCL on a GPU), which is how the RCCL path of every
+    # distributed schedule is exercised on a one-GPU box
+    pg: bool = False
+    _cstream: object = field(default=None, repr=False, compare=False)
 
     # -- collectives ------------------------------------------------------
     @property
     def distributed(self) -> bool:
-        return self.world_size > 1
+        return self.world_size > 1 or self.pg
+
+    @property
+    def own_stream(self) -> bool:
+        """RCCL ranks issue their asynchronous collectives on a dedicated,
+        probed stream (comm_stream) rather than on torch's internal RCCL
+        stream, a pool stream whose hardware queue nobody checks: HIP maps
+        streams onto GPU_MAX_HW_QUEUES (4) queues, and a collective whose
+        queue is the lookahead side stream's would wait behind the whole
+        trailing update (profiles/hw_queues_r4.txt).  GELIM_COMM_STREAM=torch
+        restores torch's own stream (A/B)."""
+        return (self.backend == "nccl" and self.device.type == "cuda"
+                and os.environ.get("GELIM_COMM_STREAM", "own") != "torch")
+
+    def comm_stream(self) -> torch.cuda.Stream:
+        """The stream this rank's asynchronous collectives run on: a
+        process-lifetime stream on a hardware queue of its own, probed to run
+        beside the default stream and the lookahead side stream
+        (utils/tensors.dedicated_stream).  A synchronous collective
+        (async_op=False) runs on the CURRENT stream in torch >= 2.7, so it is
+        issued under this stream."""
+        if self._cstream is None:
+            from ..utils.tensors import dedicated_stream
+
+            self._cstream = dedicated_stream(self.device, "comm")
+        return self._cstream
+
+    def _on_comm_stream(self, issue) -> _Event:
+        cs = self.comm_stream()
+        cs.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(cs):
+            issue()
+            ev = torch.cuda.Event()
+            ev.record(cs)
+        return _Event(ev)
 
     @property
     def staged(self) -> bool:
@@ -83,6 +138,8 @@ class Communicator:
         """Non-blocking broadcast: returns a handle whose wait() makes the
         current stream wait for the data (RCCL runs on its own stream, after
         the work already queued on the current one)."""
+        if self.distributed and self.own_stream:
+            return self._on_comm_stream(lambda: dist.broadcast(t, src=self.global_rank(src), group=self.group))
         if self.distributed:
             return dist.broadcast(t, src=self.global_rank(src), group=self.group, async_op=True)
         return _Done()
@@ -111,6 +168,9 @@ class Communicator:
         if self.distributed and self.staged:
             self.all_gather(out, t)
             return _Done()
+        if self.distributed and self.own_stream:
+            src = t.contiguous().view(-1)
+            return self._on_comm_stream(lambda: dist.all_gather_into_tensor(out.view(-1), src, group=self.group))
         if self.distributed:
             return dist.all_gather_into_tensor(out.view(-1), t.contiguous().view(-1), group=self.group,
                                                async_op=True)
@@ -164,7 +224,31 @@ class Communicator:
         g = dist.new_group(ranks=ranks, backend=self.backend if self.backend != "none" else None)
         if self.rank not in ranks:
             return Communicator(0, 1, self.device, self.backend, None)
-        return Communicator(ranks.index(self.rank), len(ranks), self.device, self.backend, g)
+        return Communicator(ranks.index(self.rank), len(ranks), self.device, self.backend, g,
+                            pg=self.pg, _cstream=self._cstream)
+
+    def overlap_probe(self, other: torch.cuda.Stream, ticks: int = 500000) -> bool:
+        """True when an asynchronous collective (broadcast_async) plus the
+        current stream's wait on it do NOT queue behind a kernel running on
+        `other` (the lookahead side stream): a bounded waiter kernel (5 ms)
+        runs on `other` until a setter kernel, queued on the current stream
+        after the broadcast, releases it.  False means the collective or the
+        current stream shares `other`'s hardware queue -- the lookahead would
+        silently serialise."""
+        from .. import _native
+        from ..utils.tensors import ptr
+
+        lib = _native.lib()
+        dev = self.device
+        words = torch.zeros(2, dtype=torch.int32, device=dev)
+        t = torch.zeros(4096, dtype=torch.float64, device=dev)
+        torch.cuda.synchronize(dev)
+        _native.check(lib.gelim_gpu_probe_kernel(other.cuda_stream, ptr(words), 0, ticks), "probe_kernel")
+        self.broadcast_async(t, 0).wait()
+        _native.check(lib.gelim_gpu_probe_kernel(torch.cuda.current_stream(dev).cuda_stream, ptr(words), 1, 0),
+                      "probe_kernel")
+        torch.cuda.synchronize(dev)
+        return int(words[1].item()) == 1
 
 
 def env_world() -> tuple[int, int, int]:
@@ -174,12 +258,16 @@ def env_world() -> tuple[int, int, int]:
 
 
 def init_from_env(backend: str | None = None, device: str | None = None,
-                  timeout_s: float = 600.0) -> Communicator:
+                  timeout_s: float = 600.0, force_pg: bool | None = None) -> Communicator:
     """Join the job described by RANK/WORLD_SIZE/LOCAL_RANK/MASTER_* (torchrun).
     backend None -> GELIM_DIST_BACKEND if set, else "nccl" (RCCL) when a GPU
     is visible, else "gloo".  gloo with a GPU device is the transport of
     several ranks sharing ONE GPU (tests): device tensors, host-staged where
-    gloo has no device path (Communicator.staged)."""
+    gloo has no device path (Communicator.staged).
+
+    force_pg (default: GELIM_FORCE_PG=1): a one-rank job still creates the
+    process group (an in-memory store, no rendezvous), so the distributed
+    schedules run their collectives through RCCL on a single GPU."""
     rank, world, local = env_world()
     use_gpu = device != "cpu" and (device is not None or torch.cuda.is_available())
     want = backend or os.environ.get("GELIM_DIST_BACKEND")
@@ -191,8 +279,19 @@ def init_from_env(backend: str | None = None, device: str | None = None,
         torch.cuda.set_device(dev)
     else:
         dev = torch.device("cpu")
-    if world <= 1:
+    if force_pg is None:
+        force_pg = os.environ.get("GELIM_FORCE_PG", "0") == "1"
+    if world <= 1 and not force_pg:
         return Communicator(0, 1, dev, "none")
+    if world <= 1:
+        backend = backend or os.environ.get("GELIM_DIST_BACKEND") or ("nccl" if use_gpu else "gloo")
+        if not dist.is_initialized():
+            kw = dict(backend=backend, store=dist.HashStore(), rank=0, world_size=1,
+                      timeout=datetime.timedelta(seconds=timeout_s))
+            if backend == "nccl":
+                kw["device_id"] = dev
+            dist.init_process_group(**kw)
+        return Communicator(0, 1, dev, backend, pg=True)
     backend = backend or os.environ.get("GELIM_DIST_BACKEND") or ("nccl" if use_gpu else "gloo")
     # failure detection: a rank that dies or hangs must not leave the others
     # blocked forever.  RCCL's async error handling turns a collective that

@@ -64,6 +64,7 @@ without GPUs.
 from __future__ import annotations
 
 import math
+import time
 from dataclasses import dataclass
 
 import torch
@@ -379,6 +380,7 @@ class DistributedGauss:
         if G == 0:
             return
         fuse = comm.world_size == 1
+        t_issue = time.perf_counter()
         end = self.nloc + 1  # local columns + b
         main = torch.cuda.current_stream(self.device)
         side = self._side
@@ -436,6 +438,7 @@ class DistributedGauss:
                     main.wait_event(ev_rest[g + 1 - nb])
                 handles[g + 1] = comm.broadcast_async(B[(g + 1) % nb][:self._bsize(g + 1)], src=o1)
         main.wait_event(ev_rest[G - 1])
+        self.last_issue_s = time.perf_counter() - t_issue  # host time to issue the schedule
 
     def _tail_solve(self, loc: torch.Tensor, G: int) -> None:
         """The trailing system (rows and columns from K = G*D, every panel

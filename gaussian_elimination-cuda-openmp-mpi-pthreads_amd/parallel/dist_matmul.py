@@ -103,7 +103,7 @@ def allgather_matmul(comm: Communicator, A_loc: torch.Tensor, B_loc: torch.Tenso
     if A_loc.shape[1] != kb * P:
         raise ValueError("allgather_matmul needs K divisible by the world size")
     C = torch.empty((A_loc.shape[0], N), dtype=torch.float32, device=A_loc.device)
-    if P == 1:
+    if P == 1 and not comm.distributed:  # (a one-rank process group still runs the gathers)
         matmul_acc_(C, A_loc, B_loc, accumulate=False, kernel=kernel)
         return C
     chunks = max(1, min(chunks or default_chunks(P), N))

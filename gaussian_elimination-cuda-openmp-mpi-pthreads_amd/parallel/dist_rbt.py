@@ -58,6 +58,7 @@ matmul) -- the orchestration, layouts and collectives are identical.
 from __future__ import annotations
 
 import math
+import time
 
 import numpy as np
 import torch
@@ -115,6 +116,13 @@ class DistributedRBT:
         self.lookahead = lookahead
         self.max_steps = max_steps
         self.np = padded_order(n, self.P)
+        self.pad_ratio = self.np / max(1, n)
+        if self.P > 1 and self.pad_ratio > 1.25:
+            import warnings
+
+            warnings.warn(f"DistributedRBT: n = {n} on {self.P} ranks is padded to {self.np} (a multiple of "
+                          f"{4 * NB * self.P}): {self.pad_ratio ** 3:.1f}x the factorisation flops of n; "
+                          "DistributedGauss or fewer ranks may be faster", RuntimeWarning, stacklevel=2)
         self.nb = self.np // NB
         self.nloc = self.np // self.P
         self.nbl = self.nb // self.P  # local blocks = super-blocks
@@ -150,8 +158,8 @@ class DistributedRBT:
         self._Wm = torch.zeros((NB, NB), **f64)
         self._Ws = torch.zeros((NB, self.nloc), **f64)
         self._info = torch.full((1,), 0x7F7F7F7F, dtype=torch.int32, device=dev)
+        self._serr = torch.zeros(1, dtype=torch.int32, device=dev)  # block solves: hand-off timeout word
         if self.gpu:
-            self._serr = torch.zeros(1, dtype=torch.int32, device=dev)  # block solves: hand-off timeout word
             self._side = side_stream(dev)  # probed: never on the default stream's queue
         else:
             self._Wu = butterfly_dense(self._ud, self.np)
@@ -322,6 +330,7 @@ class DistributedRBT:
           side (every rank):   [wait panel k] [panel k -> the next block this
                                rank owns after k+1] (ev_first) [the rest] (ev_rest)"""
         comm, r, P, nb = self.comm, self.rank, self.P, self.nb
+        t_issue = time.perf_counter()
         main = torch.cuda.current_stream(self.device)
         side = self._side
         side.wait_stream(main)  # M as the transform left it
@@ -367,6 +376,7 @@ class DistributedRBT:
                     main.wait_event(ev_rest[k + 1 - nbuf])  # the buffer slots of k+1 are free again
                 ship(k + 1)
         main.wait_event(ev_rest[nb - 1])
+        self.last_issue_s = time.perf_counter() - t_issue  # host time to issue the schedule
 
     # -- solves ----------------------------------------------------------------
     def _gather_solve_blocks(self) -> None:
@@ -454,10 +464,21 @@ class DistributedRBT:
                 self._gemv(self.M[:s * S, s * NB:(s + 1) * NB], xb, acc[:s * S])
         out = torch.empty_like(c)
         self._rbt_vec(xs, self.vd if self.gpu else None, False, out)
-        if self.gpu and int(self._serr.item()) != 0:
-            self._serr.zero_()
-            raise _native.GelimError("distributed RBT: block-solve hand-off timed out")
         return out
+
+    def _apply_timed_out(self) -> bool:
+        """True on EVERY rank when any rank's block solves of the last apply
+        timed out in a hand-off (its error word set; the result is then
+        incomplete): one all_reduce max of the words, which are cleared.  All
+        ranks then take the same fallback (the single-GPU engine's rule:
+        gelim_mixed_solve hands such a system to partial pivoting) instead of
+        one rank raising while the others block in the next collective."""
+        v = self._serr.to(torch.int64)
+        self.comm.all_reduce(v, "max")
+        if int(v.item()) == 0:
+            return False
+        self._serr.zero_()
+        return True
 
     def _residual(self, loc: torch.Tensor, x: torch.Tensor) -> tuple[torch.Tensor, float]:
         """r = b - A x of the ORIGINAL n-system (x[n:] is zero: the identity
@@ -497,6 +518,8 @@ class DistributedRBT:
             return self._fallback(loc, f"no-pivot LU: non-finite diagonal-block inverse at column {info - 1}")
         self._gather_solve_blocks()
         x = self.apply(loc[:, self.nloc].contiguous())
+        if self._apply_timed_out():
+            return self._fallback(loc, "block-solve hand-off timed out")
         x[self.n:] = 0.0
         eps = torch.finfo(torch.float64).eps
         strict, loose = 4.0 * eps, max(math.sqrt(self.n), 8.0) * eps
@@ -518,6 +541,8 @@ class DistributedRBT:
                 best, xb = om, x.clone()
             prev = om
             x = x + self.apply(r)
+            if self._apply_timed_out():
+                return self._fallback(loc, "block-solve hand-off timed out")
             x[self.n:] = 0.0
         raise AssertionError("unreachable")
 

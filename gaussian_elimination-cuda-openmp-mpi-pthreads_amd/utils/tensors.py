@@ -24,29 +24,58 @@ def stream_handle(device: torch.device | None = None) -> int | None:
     return torch.cuda.current_stream(device).cuda_stream
 
 
-def side_stream(device: torch.device) -> torch.cuda.Stream:
-    """A torch stream that runs BESIDE the default stream.  HIP shares
-    hardware queues between streams once a process has created
-    GPU_MAX_HW_QUEUES of them, and a lookahead stream on the default
+_DEDICATED: dict[tuple[int, str], torch.cuda.ExternalStream] = {}
+_DEDICATED_LOCK = __import__("threading").Lock()
+
+
+def dedicated_stream(device: torch.device, role: str) -> torch.cuda.ExternalStream:
+    """The process-lifetime stream of `role` on `device` ("side": the
+    lookahead trailing-update stream of the distributed solvers, "comm": the
+    stream RCCL collectives are issued on, parallel/comm.py).
+
+    HIP maps streams onto GPU_MAX_HW_QUEUES (4) hardware queues per process
+    and shares queues once they run out; a lookahead stream on the default
     stream's queue silently serialises behind it (the distributed 2048 solve
-    took 16 instead of 8 ms, profiles/hw_queues_r4.txt).  So torch's pool
-    streams are probed (runtime.hip gelim_gpu_stream_probe: a bounded wait on
-    the default stream for a flag the candidate sets) and the first one that
-    runs concurrently is returned -- a pool stream, so its lifetime is
-    torch's."""
+    took 16 instead of 8 ms, profiles/hw_queues_r4.txt), and a collective on
+    the side stream's queue would wait behind the whole trailing update.  So
+    each role's stream is created natively (gelim_gpu_stream_create_probed)
+    and probed to run beside the default stream AND every other role's stream
+    already made on the device; the roles together take 3 of the 4 queues.
+    Not one of torch's pool streams: torch hands those out round-robin to
+    any later torch.cuda.Stream() caller, which could put unrelated work in
+    the lookahead stream.  Created once per (device, role) and never
+    destroyed, so solvers made and dropped in a loop do not create streams."""
+    import ctypes
+    import warnings
+
     from .. import _native
 
-    lib = _native.lib()
-    s = None
-    with torch.cuda.device(device):
-        for _ in range(33):  # torch's pool holds 32 streams per priority
-            s = torch.cuda.Stream(device)
-            rc = int(lib.gelim_gpu_stream_probe(s.cuda_stream))
-            if rc < 0:
-                _native.check(rc, "stream_probe")
-            if rc == 1:
-                break
-    return s
+    key = (device.index if device.index is not None else torch.cuda.current_device(), role)
+    with _DEDICATED_LOCK:
+        s = _DEDICATED.get(key)
+        if s is not None:
+            return s
+        lib = _native.lib()
+        others = [v.cuda_stream for (d, _), v in _DEDICATED.items() if d == key[0]]
+        arr = (ctypes.c_void_p * max(1, len(others)))(*others)
+        out = ctypes.c_void_p()
+        before = side_stream_stats()
+        with torch.cuda.device(key[0]):
+            _native.check(lib.gelim_gpu_stream_create_probed(ctypes.byref(out), arr, len(others)),
+                          "stream_create_probed")
+        after = side_stream_stats()
+        if after[1] - before[1] >= 8:  # every try shared a queue: the last one is kept
+            warnings.warn(f"no {role} stream found running beside the default stream and {len(others)} other "
+                          f"dedicated stream(s) on cuda:{key[0]}; the lookahead may serialise", RuntimeWarning)
+        s = torch.cuda.ExternalStream(out.value, device=torch.device("cuda", key[0]))
+        _DEDICATED[key] = s
+        return s
+
+
+def side_stream(device: torch.device) -> torch.cuda.ExternalStream:
+    """The lookahead side stream of the distributed solvers (shared by every
+    solver -- and every emulated rank -- of the process on `device`)."""
+    return dedicated_stream(device, "side")
 
 
 def side_stream_stats() -> tuple[int, int]:

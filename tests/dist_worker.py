@@ -12,13 +12,19 @@ sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
 def _init(rank, world, port, device, timeout_s=120):
     """device "cpu": gloo CPU ranks; "cuda": every rank on cuda:0 over gloo
     (RCCL refuses two ranks on one GPU) -- device tensors, gloo's
-    asynchronous device broadcast / all_reduce, host-staged all_gather."""
+    asynchronous device broadcast / all_reduce, host-staged all_gather;
+    "nccl": RCCL, rank r on cuda:r (the process group is created even for
+    one rank)."""
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK="0" if device == "cuda" else str(rank),
                       MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     from gelim.parallel import comm as C
 
     if device == "cpu":
         return C.init_from_env(device="cpu", timeout_s=timeout_s)
+    if device == "cpu-pg":  # gloo group even for one rank (force_pg)
+        return C.init_from_env(device="cpu", timeout_s=timeout_s, force_pg=True)
+    if device == "nccl":  # RCCL: one rank per GPU (a one-rank group on the one-GPU box)
+        return C.init_from_env(backend="nccl", device=f"cuda:{rank}", timeout_s=timeout_s, force_pg=True)
     return C.init_from_env(backend="gloo", device="cuda:0", timeout_s=timeout_s)
 
 
@@ -124,3 +130,107 @@ def rbt(rank, world, port, outdir, n, seed, device, mode, lookahead=True, fast=T
     except Exception:
         (Path(outdir) / f"err{rank}.txt").write_text(traceback.format_exc())
         raise
+
+
+def rccl_one_rank(outdir, n_gauss=2048, n_rbt=2048):
+    """Every distributed schedule through a ONE-rank RCCL process group on
+    cuda:0, each result next to the same schedule on the plain one-rank
+    communicator (backend "none": no collective runs).  One rank's
+    collectives leave the data as it is, so the two must agree bit for bit;
+    what differs is that every broadcast / all_gather / all_reduce is a real
+    RCCL call on the communicator's stream, ordered by events against the
+    main and side streams.  Writes res.json and the solutions."""
+    import json
+    import time
+
+    import torch
+    import torch.distributed as dist
+
+    import gelim
+    from gelim.parallel import DistributedGauss, DistributedRBT
+    from gelim.parallel import comm as C
+    from gelim.parallel.dist_matmul import allgather_matmul, make_summa_groups, summa_matmul
+    from gelim.utils.tensors import side_stream, side_stream_stats
+
+    out = Path(outdir)
+    res = {}
+    try:
+        comm = _init(0, 1, 0, "nccl")
+        dev = comm.device
+        none = C.Communicator(0, 1, dev, "none")
+        res.update(backend=comm.backend, pg=comm.pg, initialized=dist.is_initialized(),
+                   pg_backend=str(dist.get_backend()), world=dist.get_world_size())
+        side = side_stream(dev)
+        res["overlap_own_stream"] = comm.overlap_probe(side)
+        os.environ["GELIM_COMM_STREAM"] = "torch"
+        res["overlap_torch_stream"] = comm.overlap_probe(side)
+        os.environ.pop("GELIM_COMM_STREAM")
+        res["streams"] = {"side": side.cuda_stream, "comm": comm.comm_stream().cuda_stream,
+                          "default": torch.cuda.current_stream(dev).cuda_stream}
+        res["side_stream_stats"] = list(side_stream_stats())
+
+        def run_gauss(c, n, **kw):
+            dg = DistributedGauss(c, n, **kw)
+            x = dg.solve_(dg.generate_random(seed=41))
+            torch.cuda.synchronize(dev)
+            t0 = time.perf_counter()
+            x = dg.solve_(dg.generate_random(seed=41))
+            torch.cuda.synchronize(dev)
+            return x.cpu(), time.perf_counter() - t0, dg._panel_blocks(use_tail=bool(dg.lookahead))
+
+        for tag, kw in (("gauss_la_tail0", dict(tail=0)), ("gauss_la", {}), ("gauss_serial", dict(lookahead=False))):
+            xp, tp, G = run_gauss(comm, n_gauss, **kw)
+            xn, tn, _ = run_gauss(none, n_gauss, **kw)
+            torch.save(xp, out / f"{tag}.pt")
+            res[tag] = {"bitwise": bool(torch.equal(xp, xn)), "panels": G, "rccl_s": tp, "none_s": tn}
+
+        def run_rbt(c, n):
+            d = DistributedRBT(c, n, single_fast_path=False)
+            x = d.solve_(d.generate_random(seed=43))
+            torch.cuda.synchronize(dev)
+            t0 = time.perf_counter()
+            x = d.solve_(d.generate_random(seed=43))
+            torch.cuda.synchronize(dev)
+            dt = time.perf_counter() - t0
+            meta = (d.last_steps, d.last_berr, d.last_fallback)
+            d.close()
+            return x.cpu(), dt, meta
+
+        xp, tp, mp_ = run_rbt(comm, n_rbt)
+        xn, tn, _ = run_rbt(none, n_rbt)
+        torch.save(xp, out / "rbt.pt")
+        res["rbt"] = {"bitwise": bool(torch.equal(xp, xn)), "rccl_s": tp, "none_s": tn, "steps": mp_[0],
+                      "berr": mp_[1], "fallback": mp_[2]}
+
+        g = torch.Generator(device=dev).manual_seed(3)
+        A = torch.randn(512, 768, generator=g, device=dev)
+        B = torch.randn(768, 640, generator=g, device=dev)
+        ref = A @ B
+        cp = allgather_matmul(comm, A, B)
+        cn = allgather_matmul(none, A, B)
+        res["matmul_allgather"] = {"bitwise": bool(torch.equal(cp, cn)),
+                                   "rel": float(((cp.double() - ref.double()).abs().max() / ref.abs().max()).item())}
+        groups = make_summa_groups(comm, 1, 1)
+        sp = summa_matmul(comm, A, B, (1, 1), groups=groups, panels=3)
+        sn = summa_matmul(none, A, B, (1, 1), panels=3)
+        res["matmul_summa"] = {"bitwise": bool(torch.equal(sp, sn)),
+                               "subgroup_backend": groups[0].backend, "subgroup_pg": groups[0].pg}
+        # point-to-point through RCCL: a batched send to / receive from the rank itself
+        t = torch.arange(1000, dtype=torch.float64, device=dev)
+        r = torch.zeros_like(t)
+        try:
+            for q in comm.sendrecv(t, 0, r, 0):
+                q.wait()
+            torch.cuda.synchronize(dev)
+            res["p2p_self"] = {"ok": bool(torch.equal(t, r))}
+        except Exception as e:  # noqa: BLE001
+            res["p2p_self"] = {"ok": False, "error": repr(e)[:300]}
+        comm.barrier()
+        C.destroy()
+        res["ok"] = True
+    except Exception:
+        res["ok"] = False
+        res["traceback"] = traceback.format_exc()
+    (out / "res.json").write_text(json.dumps(res, indent=1, default=str))
+    if not res["ok"]:
+        raise SystemExit(1)

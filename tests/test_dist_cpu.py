@@ -113,3 +113,20 @@ def test_dist_handoff_abort_raises(gelim, monkeypatch):
     monkeypatch.setattr(dg, "factor_", aborted)
     with pytest.raises(gelim.GelimError, match="code 5"):
         dg.solve_(dg.generate_random(seed=3))
+
+
+def test_one_rank_process_group_cpu(tmp_path, gelim):
+    """force_pg: a one-rank job still creates a (gloo) process group, so every
+    collective of the schedule really runs; the solution must equal the plain
+    one-rank communicator's bit for bit."""
+    from gelim.parallel import DistributedGauss
+    from gelim.parallel.comm import Communicator
+
+    codes = _spawn(dist_worker.gauss, 1, _port(), str(tmp_path), 200, 32, 13, "cpu-pg", "random")
+    errs = list(tmp_path.glob("err*.txt"))
+    assert not errs, errs[0].read_text()
+    assert codes == [0]
+    assert (tmp_path / "meta0.txt").read_text().split()[:2] == ["gloo", "1"]
+    x = torch.load(tmp_path / "x0.pt")
+    dg = DistributedGauss(Communicator(), 200, block=32)
+    assert torch.equal(x, dg.solve_(dg.generate_random(seed=13)))

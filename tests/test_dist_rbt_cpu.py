@@ -118,3 +118,43 @@ def test_dist_rbt_reference_matrix_cpu(tmp_path, gelim):
     assert codes == [0, 0]
     x = torch.load(tmp_path / "x0.pt")
     assert gelim.ops.gauss.error_metric(x) < 1e-12
+
+
+def test_emulated_dist_rbt_solve_timeout_falls_back_on_every_rank(gelim):
+    """One rank's block solves report a timed-out hand-off (its error word
+    set): every rank must see it (all_reduce max of the words) and take the
+    same partial-pivoting fallback -- not one rank raising while the others
+    block in the next collective."""
+    n, P = 600, 3
+
+    class Faulty(DistributedRBT):
+        def apply(self, rhs):
+            out = super().apply(rhs)
+            if self.rank == 1 and not getattr(self, "_fired", False):
+                self._fired = True
+                self._serr.fill_(5)
+            return out
+
+    def body(c):
+        d = Faulty(c, n, single_fast_path=False)
+        x = d.solve_(d.generate_random(seed=9))
+        return x, d.last_fallback, int(d._serr.item())
+
+    res = run_emulated(P, body, device="cpu", timeout_s=300)
+    aug = gelim.random_system(n, seed=9)
+    ref = torch.linalg.solve(aug[:, :n], aug[:, n])
+    for x, fb, word in res:
+        assert fb == "block-solve hand-off timed out"
+        assert word == 0
+        assert torch.equal(x, res[0][0])
+        assert ((x - ref).abs().max() / ref.abs().max()).item() < 1e-10
+
+
+def test_dist_rbt_pad_warning():
+    """n far below the 512 P padding multiple: the flop blow-up is reported."""
+    from gelim.parallel.emulated import make_world
+
+    c = make_world(8)[0]
+    with pytest.warns(RuntimeWarning, match="padded to 4096"):
+        d = DistributedRBT(c, 2048, single_fast_path=False)
+    assert d.pad_ratio == 2.0

@@ -1,0 +1,92 @@
+"""The RCCL transport on the one MI355X: a ONE-rank `nccl` process group
+(init_from_env(force_pg=True)) drives every distributed schedule, so each
+broadcast / all_gather / all_reduce / batched p2p is a real RCCL call issued
+on the communicator's dedicated stream and ordered against the main and
+lookahead side streams by events -- the path an 8-GPU node runs, minus the
+links.  Each result must equal, bit for bit, the same schedule on the plain
+one-rank communicator (no collective at all): a one-rank collective leaves
+the data unchanged, so any difference is an ordering bug (a stream reading a
+buffer before its collective landed).
+
+The stream check: a bounded waiter kernel occupies the side stream while a
+broadcast is issued and the main stream waits on it; the setter queued after
+the broadcast must release the waiter, i.e. the collective does not share the
+side stream's hardware queue (the lookahead would otherwise serialise).
+
+Reference: the MPI collectives these replace,
+OpenMP_and_MPI/gauss_mpi/gauss_internal_input.c:130-206."""
+import json
+import os
+import subprocess
+import sys
+from pathlib import Path
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+HERE = Path(__file__).resolve().parent
+
+
+@pytest.fixture(scope="module")
+def rccl_run(tmp_path_factory, cuda):
+    out = tmp_path_factory.mktemp("rccl")
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", MASTER_ADDR="127.0.0.1")
+    code = f"import dist_worker; dist_worker.rccl_one_rank({str(out)!r})"
+    proc = subprocess.run([sys.executable, "-u", "-c", code], cwd=HERE, env=env, capture_output=True, text=True,
+                          timeout=300)
+    resf = out / "res.json"
+    assert resf.exists(), f"rc={proc.returncode}\n{proc.stdout[-3000:]}\n{proc.stderr[-3000:]}"
+    res = json.loads(resf.read_text())
+    assert res.get("ok"), res.get("traceback", res)
+    return out, res
+
+
+def test_rccl_group_is_real(rccl_run):
+    _, res = rccl_run
+    assert res["backend"] == "nccl" and res["pg"] and res["initialized"]
+    assert res["pg_backend"] == "nccl" and res["world"] == 1
+
+
+def test_rccl_collectives_beside_side_stream(rccl_run):
+    _, res = rccl_run
+    assert res["overlap_own_stream"], res
+    s = res["streams"]
+    assert len({s["side"], s["comm"], s["default"]}) == 3
+
+
+@pytest.mark.parametrize("tag", ["gauss_la_tail0", "gauss_la", "gauss_serial"])
+def test_rccl_dist_gauss_bitwise(rccl_run, gelim, tag):
+    out, res = rccl_run
+    r = res[tag]
+    assert r["bitwise"], r
+    if tag == "gauss_la_tail0":
+        assert r["panels"] >= 4
+    x = torch.load(out / f"{tag}.pt")
+    aug = gelim.random_system(2048, seed=41, device="cuda:0").double().cpu()
+    ref = torch.linalg.solve(aug[:, :2048], aug[:, 2048])
+    assert torch.allclose(x, ref, rtol=1e-7, atol=1e-7)
+
+
+def test_rccl_dist_rbt_bitwise(rccl_run, gelim):
+    out, res = rccl_run
+    r = res["rbt"]
+    assert r["bitwise"], r
+    assert r["fallback"] is None
+    x = torch.load(out / "rbt.pt")
+    aug = gelim.random_system(2048, seed=43, device="cuda:0").double().cpu()
+    ref = torch.linalg.solve(aug[:, :2048], aug[:, 2048])
+    assert torch.allclose(x, ref, rtol=1e-8, atol=1e-8)
+
+
+def test_rccl_dist_matmul_bitwise(rccl_run):
+    _, res = rccl_run
+    assert res["matmul_allgather"]["bitwise"] and res["matmul_allgather"]["rel"] < 1e-5
+    assert res["matmul_summa"]["bitwise"]
+    assert res["matmul_summa"]["subgroup_backend"] == "nccl" and res["matmul_summa"]["subgroup_pg"]
+
+
+def test_rccl_p2p_self(rccl_run):
+    _, res = rccl_run
+    assert res["p2p_self"]["ok"], res["p2p_self"]

@@ -82,6 +82,16 @@ inline std::string device_name() {
   std::exit(-1);
 }
 
+// A GPU backend on a host without a HIP device: say so (and what to use
+// instead) before any HIP call fails with a runtime message.
+inline void require_gpu(const char* what, const char* instead) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n == 0) {
+    std::fprintf(stderr, "no HIP device found: %s needs an AMD GPU; %s\n", what, instead);
+    std::exit(-1);
+  }
+}
+
 #define CLI_CHECK(expr)                 \
   do {                                  \
     if ((expr) != 0) cli::die(#expr);   \

@@ -94,6 +94,7 @@ int main(int argc, char* argv[]) {
 
   // initMatrix + initRHS on the host, in the reference's order (P1e:296-297)
   const bool gpu = cli::is_gpu(backend);
+  if (gpu) cli::require_gpu((std::string("--backend=") + cli::backend_name(backend)).c_str(), "use --backend=omp (or seq, pthreads-v1, pthreads-v2, pthreads-v3) for the CPU engines");
   const int64_t lda = gpu ? n + 1 : n;  // GPU: augmented [A | R]
   std::vector<double> A((size_t)n * lda), R(n), X(n);
   if (gelim_dat_read(fname, A.data(), n, lda) != 0) cli::die("dat_read");

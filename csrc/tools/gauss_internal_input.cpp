@@ -115,6 +115,8 @@ int main(int argc, char* argv[]) {
     printf("Setting CPU Affinity : %s\n", (affinity && num_threads <= nprocs) ? "Yes" : "No");
   }
 
+  if (cli::is_gpu(backend))
+    cli::require_gpu((std::string("--backend=") + cli::backend_name(backend)).c_str(), "use --backend=omp (or seq, pthreads-v1, pthreads-v2, pthreads-v3) for the CPU engines");
   std::vector<double> B(n), C(n);
   double elapsed = 0.0;
   if (!cli::is_gpu(backend)) {

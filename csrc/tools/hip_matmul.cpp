@@ -70,6 +70,7 @@ int main(int argc, char* argv[]) {
     std::cout << "Invalid array size" << std::endl;
     exit(0);
   }
+  cli::require_gpu("hip_matmul (GPU Time)", "the sequential / OpenMP loops alone are not a mode of this program");
   const size_t elems = (size_t)nsize * nsize;
   const size_t bytes = elems * sizeof(float);
   float *A, *B, *C;

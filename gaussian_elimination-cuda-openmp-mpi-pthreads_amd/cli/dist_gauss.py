@@ -21,6 +21,10 @@ column block-cyclic: one panel broadcast per block (parallel/dist_gauss.py).
 random butterfly transform, no pivot chain, fp64 refinement, partial-
 pivoting fallback), the distributed form of `--backend=hip-rbt`.
 
+stdout is the MPI programs' own lines and nothing else: internal mode
+`Application time: %f Secs` (plus `Max error vs exact solution` with
+--verify), external mode `Time:  %f seconds` and `Error: %e`.
+
 --emulate P runs P ranks as threads of this one process on one device (the
 emulated communicator, parallel/emulated.py) — the distributed algorithm on a
 single GPU.  --checkpoint-dir / --checkpoint-every / --resume save and resume
@@ -187,7 +191,7 @@ def run(args, comm) -> int:
             dt = time.perf_counter() - t0
             if comm.rank == 0:
                 err = error_metric(x)
-                print(f"\nMatrix File: {args.file}; Matrix Size: {n} ; Ranks: {comm.world_size}", flush=True)
+                # exactly the MPI program's two lines, no header (gauss_mpi/gauss_external_input.c:369,378)
                 print(f"Time:  {dt:f} seconds")
                 print(f"Error: {err:e}", flush=True)
                 if args.json:

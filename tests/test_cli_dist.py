@@ -43,6 +43,10 @@ def test_dist_gauss_external_cli():
     assert re.search(r"^Time:  \d+\.\d{6} seconds$", out, re.M), out
     err = float(re.search(r"^Error: (\S+)$", out, re.M).group(1))
     assert err < 1e-12
+    # the MPI program prints these two lines and no header (gauss_mpi/gauss_external_input.c:369-378)
+    # (gloo's own connection messages also reach stdout: ignored)
+    lines = [ln for ln in out.strip().splitlines() if "Gloo" not in ln and "peer ranks" not in ln]
+    assert len(lines) == 2 and lines[0].startswith("Time:  ") and lines[1].startswith("Error: "), out
 
 
 @pytest.mark.parametrize("algo,nproc", [("ring", 2), ("summa", 4)])

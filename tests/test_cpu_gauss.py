@@ -163,3 +163,15 @@ def test_refinement_cpu_seq(gelim):
     assert e1 <= max(e0, 1e-14)
     ref = torch.linalg.solve(aug[:, :n], aug[:, n])
     assert torch.allclose(x, ref, rtol=1e-12, atol=1e-12)
+
+
+def test_cli_gpu_backend_without_gpu_says_so():
+    """A GPU backend on a GPU-less host names the problem and the CPU
+    alternative instead of a runtime error from inside a plan."""
+    import torch
+
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is visible")
+    r = run_cli(BIN / "gauss_internal_input", "-s", "32")
+    assert r.returncode != 0
+    assert "no HIP device found" in r.stderr and "--backend=omp" in r.stderr

@@ -242,6 +242,9 @@ class Communicator:
         dev = self.device
         words = torch.zeros(2, dtype=torch.int32, device=dev)
         t = torch.zeros(4096, dtype=torch.float64, device=dev)
+        # warm-up first: the stream set-up (probes that synchronise streams)
+        # and the collective's first-call work must not run under the waiter
+        self.broadcast_async(t, 0).wait()
         torch.cuda.synchronize(dev)
         _native.check(lib.gelim_gpu_probe_kernel(other.cuda_stream, ptr(words), 0, ticks), "probe_kernel")
         self.broadcast_async(t, 0).wait()

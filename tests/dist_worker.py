@@ -201,6 +201,10 @@ def rccl_one_rank(outdir, n_gauss=2048, n_rbt=2048):
         torch.save(xp, out / "rbt.pt")
         res["rbt"] = {"bitwise": bool(torch.equal(xp, xn)), "rccl_s": tp, "none_s": tn, "steps": mp_[0],
                       "berr": mp_[1], "fallback": mp_[2]}
+        d1 = DistributedRBT(none, n_rbt)  # the single-GPU native engine on the same system
+        d1.solve_(d1.generate_random(seed=43))
+        res["rbt"]["native_steps"], res["rbt"]["native_berr"] = d1.last_steps, d1.last_berr
+        d1.close()
 
         g = torch.Generator(device=dev).manual_seed(3)
         A = torch.randn(512, 768, generator=g, device=dev)

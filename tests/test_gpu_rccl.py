@@ -39,6 +39,9 @@ def rccl_run(tmp_path_factory, cuda):
     resf = out / "res.json"
     assert resf.exists(), f"rc={proc.returncode}\n{proc.stdout[-3000:]}\n{proc.stderr[-3000:]}"
     res = json.loads(resf.read_text())
+    keep = HERE.parent / "gpurun_out"
+    if keep.is_dir():  # on the GPU box: the record travels back with the call
+        (keep / "rccl_one_rank_res.json").write_text(resf.read_text())
     assert res.get("ok"), res.get("traceback", res)
     return out, res
 
@@ -74,10 +77,11 @@ def test_rccl_dist_rbt_bitwise(rccl_run, gelim):
     r = res["rbt"]
     assert r["bitwise"], r
     assert r["fallback"] is None
+    assert r["berr"] <= 64 * torch.finfo(torch.float64).eps
     x = torch.load(out / "rbt.pt")
     aug = gelim.random_system(2048, seed=43, device="cuda:0").double().cpu()
     ref = torch.linalg.solve(aug[:, :2048], aug[:, 2048])
-    assert torch.allclose(x, ref, rtol=1e-8, atol=1e-8)
+    assert ((x - ref).abs().max() / ref.abs().max()).item() < 1e-9
 
 
 def test_rccl_dist_matmul_bitwise(rccl_run):

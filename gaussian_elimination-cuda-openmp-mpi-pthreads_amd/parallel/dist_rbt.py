@@ -108,7 +108,7 @@ class DistributedRBT:
     """Randomised block-LDU solve of one n x n system over all ranks of comm."""
 
     def __init__(self, comm: Communicator, n: int, seed: int = SEED, lookahead: bool = True,
-                 single_fast_path: bool = True, max_steps: int = 6):
+                 single_fast_path: bool = True, max_steps: int = 6, graph: bool = True):
         self.comm, self.n = comm, n
         self.P, self.rank = comm.world_size, comm.rank
         self.device = comm.device
@@ -128,6 +128,16 @@ class DistributedRBT:
         self.nbl = self.nb // self.P  # local blocks = super-blocks
         self.ld = self.nloc + 2       # b in column nloc; even, 16-byte rows
         self.fast = single_fast_path and self.P == 1 and self.gpu
+        # hipGraph replay of the fixed schedules (factorisation loop, apply):
+        # the host issue of one block -- ~15 launches, two collectives, their
+        # events -- costs 120 us eagerly and 255 us with RCCL's host side,
+        # more than the GPU chain of a block at 8 ranks
+        # (profiles/dist_issue_r5.md).  Only where every op is a stream op:
+        # RCCL or no collective at all (gloo and the emulated ranks meet on
+        # the host).
+        self.graph = graph and self.gpu and lookahead and comm.backend in ("none", "nccl")
+        self._graphs: dict[str, torch.cuda.CUDAGraph | None] = {}
+        self.last_issue_s = None
         self._ud, self._vd = butterfly_diagonals(self.np, seed)
         lb = torch.arange(self.nloc) // NB
         self.gcol = ((lb * self.P + self.rank) * NB + torch.arange(self.nloc) % NB).to(self.device)
@@ -151,6 +161,8 @@ class DistributedRBT:
         self.ud = torch.from_numpy(self._ud).to(dev)
         self.vd = torch.from_numpy(self._vd).to(dev)
         self.M = torch.zeros((self.np, self.ld), **f64)
+        self._Fs = self._Ds = None
+        self._ain = torch.zeros(self.np, **f64)  # apply's input, captured by address
         self.Dinv = torch.zeros((self.nbl, NB, NB), **f64)
         nbuf = NBUF if lookahead else 2
         self._xbufs = [torch.zeros(self.np * NB, **f64) for _ in range(nbuf)]  # column k from the diagonal down
@@ -293,7 +305,9 @@ class DistributedRBT:
         self._info.fill_(0x7F7F7F7F)
         self._transform(loc)
         if self.lookahead and self.gpu:
-            self._factor_lookahead()
+            t0 = time.perf_counter()
+            self._replay("factor", self._factor_lookahead)
+            self.last_issue_s = time.perf_counter() - t0  # host time to issue (or replay) the schedule
         else:
             self._factor_serial()
         v = self._info.to(torch.int64)
@@ -330,7 +344,6 @@ class DistributedRBT:
           side (every rank):   [wait panel k] [panel k -> the next block this
                                rank owns after k+1] (ev_first) [the rest] (ev_rest)"""
         comm, r, P, nb = self.comm, self.rank, self.P, self.nb
-        t_issue = time.perf_counter()
         main = torch.cuda.current_stream(self.device)
         side = self._side
         side.wait_stream(main)  # M as the transform left it
@@ -376,7 +389,6 @@ class DistributedRBT:
                     main.wait_event(ev_rest[k + 1 - nbuf])  # the buffer slots of k+1 are free again
                 ship(k + 1)
         main.wait_event(ev_rest[nb - 1])
-        self.last_issue_s = time.perf_counter() - t_issue  # host time to issue the schedule
 
     # -- solves ----------------------------------------------------------------
     def _gather_solve_blocks(self) -> None:
@@ -388,10 +400,13 @@ class DistributedRBT:
             mine[s] = self.M[s * S:(s + 1) * S, s * NB:(s + 1) * NB]
         g = torch.empty((P, ns, S, NB), dtype=torch.float64, device=self.device)
         self.comm.all_gather(g.view(-1), mine.view(-1))
-        self._Fs = g.permute(1, 2, 0, 3).reshape(ns, S, S).contiguous()
+        if getattr(self, "_Fs", None) is None:  # persistent: a captured apply reads them by address
+            self._Fs = torch.empty((ns, S, S), dtype=torch.float64, device=self.device)
+            self._Ds = torch.empty((ns, P, NB, NB), dtype=torch.float64, device=self.device)
+        self._Fs.copy_(g.permute(1, 2, 0, 3).reshape(ns, S, S))
         gd = torch.empty((P, ns, NB, NB), dtype=torch.float64, device=self.device)
         self.comm.all_gather(gd.view(-1), self.Dinv.contiguous().view(-1))
-        self._Ds = gd.permute(1, 0, 2, 3).contiguous()  # (ns, P, 128, 128)
+        self._Ds.copy_(gd.permute(1, 0, 2, 3))  # (ns, P, 128, 128)
         del mine, g, gd
 
     def _super_solve(self, s: int, rhs: torch.Tensor, x: torch.Tensor, ysave: torch.Tensor | None,
@@ -434,8 +449,45 @@ class DistributedRBT:
             W = self._Wu if transpose else self._Wv
             out.copy_(W.T @ v if transpose else W @ v)
 
+    def _replay(self, name: str, fn):
+        """fn() -- a fixed schedule over persistent buffers -- eagerly on its
+        first call, then captured ONCE into a hipGraph (torch.cuda.graph: the
+        side and communicator streams join the capture through their events,
+        so the graph holds both streams' work and the RCCL collectives) and
+        replayed on the current stream.  Returns fn's result (a static
+        tensor of the graph when captured)."""
+        if not self.graph:
+            return fn()
+        if name not in self._graphs:  # warm-up: RCCL / allocator first-call work stays out of the capture
+            self._graphs[name] = None
+            return fn()
+        ent = self._graphs[name]
+        if ent is None:
+            g = torch.cuda.CUDAGraph()
+            try:
+                with torch.cuda.graph(g, capture_error_mode="thread_local"):
+                    out = fn()
+            except Exception as e:  # noqa: BLE001 - a transport that cannot be captured: stay eager
+                import warnings
+
+                warnings.warn(f"DistributedRBT: hipGraph capture of {name} failed ({e!r}); issuing eagerly",
+                              RuntimeWarning)
+                self.graph = False
+                torch.cuda.synchronize(self.device)
+                return fn()
+            ent = self._graphs[name] = (g, out)
+        ent[0].replay()
+        return ent[1]
+
     def apply(self, rhs: torch.Tensor) -> torch.Tensor:
-        """(U^T)^-1-free correction: V (LU)^-1 U^T rhs for a replicated np-vector."""
+        """(U^T)^-1-free correction: V (LU)^-1 U^T rhs for a replicated
+        np-vector (graph-replayed on GPU ranks, see _replay)."""
+        if not self.graph:
+            return self._apply(rhs)
+        self._ain.copy_(rhs)
+        return self._replay("apply", lambda: self._apply(self._ain)).clone()
+
+    def _apply(self, rhs: torch.Tensor) -> torch.Tensor:
         P, S, ns = self.P, NB * self.P, self.nbl
         r = self.rank
         dev = self.device

@@ -66,26 +66,28 @@ def main():
         torch.cuda.synchronize(dev)
         return time.perf_counter() - t0
 
-    # DistributedRBT: the distributed schedule on one rank
-    d = DistributedRBT(comm, a.n, single_fast_path=False)
-    loc = d.generate_random(seed=99)
-    d.solve_(loc.clone())
-    rows = []
-    for _ in range(a.reps):
-        wall = as_runs(lambda: d.factor_(loc))
-        issue_wall = d.last_issue_s
-        g, issue_q = gpu_only(lambda: d.factor_(loc))
-        torch.cuda.synchronize(dev)
-        t0 = time.perf_counter()
+    # DistributedRBT: the distributed schedule on one rank, eager and graph-replayed
+    for tag, graph in (("rbt_eager", False), ("rbt", True)):
+        d = DistributedRBT(comm, a.n, single_fast_path=False, graph=graph)
+        loc = d.generate_random(seed=99)
         d.solve_(loc)
-        torch.cuda.synchronize(dev)
-        rows.append({"factor_wall_s": wall, "factor_issue_s": issue_wall, "factor_gpu_only_s": g,
-                     "issue_queued_s": issue_q, "solve_s": time.perf_counter() - t0})
-    out["rbt"] = {"blocks": d.nb, "runs": rows,
-                  "issue_us_per_block": min(r["factor_issue_s"] for r in rows) / d.nb * 1e6,
-                  "gpu_us_per_block": min(r["factor_gpu_only_s"] for r in rows) / d.nb * 1e6}
-    d.close()
-    del d, loc
+        d.solve_(loc)  # (graph: the second solve captures)
+        rows = []
+        for _ in range(a.reps):
+            wall = as_runs(lambda: d.factor_(loc))
+            issue_wall = d.last_issue_s
+            g, issue_q = gpu_only(lambda: d.factor_(loc))
+            torch.cuda.synchronize(dev)
+            t0 = time.perf_counter()
+            d.solve_(loc)
+            torch.cuda.synchronize(dev)
+            rows.append({"factor_wall_s": wall, "factor_issue_s": issue_wall, "factor_gpu_only_s": g,
+                         "solve_s": time.perf_counter() - t0, "steps": d.last_steps})
+        out[tag] = {"blocks": d.nb, "graph": d.graph, "runs": rows,
+                    "issue_us_per_block": min(r["factor_issue_s"] for r in rows) / d.nb * 1e6,
+                    "gpu_us_per_block": min(r["factor_gpu_only_s"] for r in rows) / d.nb * 1e6}
+        d.close()
+        del d, loc
 
     # DistributedGauss: lookahead schedule, every block a broadcast panel (tail = 0) and the default
     for tag, tail in (("gauss_tail0", 0), ("gauss", None)):

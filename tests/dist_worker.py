@@ -184,23 +184,28 @@ def rccl_one_rank(outdir, n_gauss=2048, n_rbt=2048):
             torch.save(xp, out / f"{tag}.pt")
             res[tag] = {"bitwise": bool(torch.equal(xp, xn)), "panels": G, "rccl_s": tp, "none_s": tn}
 
-        def run_rbt(c, n):
-            d = DistributedRBT(c, n, single_fast_path=False)
-            x = d.solve_(d.generate_random(seed=43))
-            torch.cuda.synchronize(dev)
-            t0 = time.perf_counter()
-            x = d.solve_(d.generate_random(seed=43))
-            torch.cuda.synchronize(dev)
+        def run_rbt(c, n, graph=True):
+            """Three solves: eager, captured + replayed, replayed (graph=True)."""
+            d = DistributedRBT(c, n, single_fast_path=False, graph=graph)
+            xs = []
+            for _ in range(3):
+                torch.cuda.synchronize(dev)
+                t0 = time.perf_counter()
+                xs.append(d.solve_(d.generate_random(seed=43)).cpu())
+                torch.cuda.synchronize(dev)
             dt = time.perf_counter() - t0
-            meta = (d.last_steps, d.last_berr, d.last_fallback)
+            meta = (d.last_steps, d.last_berr, d.last_fallback, d.graph)
             d.close()
-            return x.cpu(), dt, meta
+            return xs, dt, meta
 
         xp, tp, mp_ = run_rbt(comm, n_rbt)
-        xn, tn, _ = run_rbt(none, n_rbt)
-        torch.save(xp, out / "rbt.pt")
-        res["rbt"] = {"bitwise": bool(torch.equal(xp, xn)), "rccl_s": tp, "none_s": tn, "steps": mp_[0],
-                      "berr": mp_[1], "fallback": mp_[2]}
+        xn, tn, mn_ = run_rbt(none, n_rbt)
+        xe, te, _ = run_rbt(comm, n_rbt, graph=False)
+        torch.save(xp[-1], out / "rbt.pt")
+        res["rbt"] = {"bitwise": bool(torch.equal(xp[-1], xn[-1])), "rccl_s": tp, "none_s": tn, "rccl_eager_s": te,
+                      "graph_rccl": mp_[3], "graph_none": mn_[3],
+                      "replay_equals_eager": all(torch.equal(x, xe[0]) for x in xp + xn + xe),
+                      "steps": mp_[0], "berr": mp_[1], "fallback": mp_[2]}
         d1 = DistributedRBT(none, n_rbt)  # the single-GPU native engine on the same system
         d1.solve_(d1.generate_random(seed=43))
         res["rbt"]["native_steps"], res["rbt"]["native_berr"] = d1.last_steps, d1.last_berr

@@ -76,6 +76,10 @@ def test_rccl_dist_rbt_bitwise(rccl_run, gelim):
     out, res = rccl_run
     r = res["rbt"]
     assert r["bitwise"], r
+    # the graph-replayed schedule (factorisation + applies captured once, RCCL
+    # collectives inside the graph) gives the eager schedule's bits
+    assert r["graph_rccl"] and r["graph_none"], r
+    assert r["replay_equals_eager"], r
     assert r["fallback"] is None
     assert r["berr"] <= 64 * torch.finfo(torch.float64).eps
     x = torch.load(out / "rbt.pt")

@@ -63,6 +63,16 @@ _PROTOS = {
     "gelim_gpu_stream_probe": (_int, [_vp]),
     "gelim_gpu_stream_create_probed": (_int, [C.POINTER(C.c_void_p), _vp, _i32]),
     "gelim_gpu_probe_kernel": (_int, [_vp, _vp, _i32, _i64]),
+    "gelim_rccl_load": (_int, [C.c_char_p]),
+    "gelim_rccl_version": (_int, []),
+    "gelim_rccl_unique_id": (_int, [_vp]),
+    "gelim_rccl_comm_create": (_int, [C.POINTER(C.c_void_p), _vp, _i32, _i32]),
+    "gelim_rccl_comm_destroy": (_int, [_vp, _i32]),
+    "gelim_rccl_async_error": (_int, [_vp]),
+    "gelim_rccl_bcast": (_int, [_vp, _vp, _i64, _i32, _i32, _vp]),
+    "gelim_rccl_allreduce": (_int, [_vp, _vp, _vp, _i64, _i32, _i32, _vp]),
+    "gelim_rccl_allgather": (_int, [_vp, _vp, _vp, _i64, _i32, _vp]),
+    "gelim_rccl_sendrecv": (_int, [_vp, _vp, _i64, _i32, _vp, _i64, _i32, _i32, _vp]),
     "gelim_gpu_stream_priority_range": (_int, [_vp]),
     "gelim_gpu_side_stream_stats": (None, [_vp]),
     "gelim_gpu_init_synthetic": (_int, [_vp, _i64, _i64, _vp]),

@@ -68,6 +68,83 @@ class _Event:
         return self.ev.query()
 
 
+_DTYPE = {torch.float64: 0, torch.float32: 1, torch.int32: 2, torch.int64: 3, torch.uint8: 4}
+_OP = {"sum": 0, "max": 1, "min": 2}
+_NATIVE: list = []  # every live NativeRccl of the process (destroy() releases them)
+
+
+class NativeRccl:
+    """One RCCL communicator owned by libgelim (csrc/comm/rccl_comm.hip):
+    each collective is one RCCL call on a caller-chosen stream, ~3 us of host
+    time against ~65 us through ProcessGroupNCCL, capturable into hipGraphs
+    (torch's watchdog queries the events of collectives recorded during a
+    capture and aborts the process).  The RCCL is torch's own librccl.so (one
+    instance in the process); the 128-byte unique id of the communicator goes
+    from its rank 0 to the others through the process group's store, under
+    `key`.  Creation is collective over the nranks members."""
+
+    def __init__(self, key: str, nranks: int, rank: int, device: torch.device):
+        import ctypes
+
+        from .. import _native
+
+        self.lib = lib = _native.lib()
+        path = os.path.join(os.path.dirname(torch.__file__), "lib", "librccl.so")
+        _native.check(lib.gelim_rccl_load(path.encode()), "rccl_load")
+        store = dist.distributed_c10d._get_default_store()
+        idb = (ctypes.c_uint8 * 128)()
+        if rank == 0:
+            _native.check(lib.gelim_rccl_unique_id(idb), "rccl_unique_id")
+            store.set(key, bytes(idb))
+        else:
+            ctypes.memmove(idb, store.get(key), 128)
+        h = ctypes.c_void_p()
+        with torch.cuda.device(device):
+            _native.check(lib.gelim_rccl_comm_create(ctypes.byref(h), idb, nranks, rank), "rccl_comm_create")
+        self.handle, self.nranks, self.rank, self.device = h.value, nranks, rank, device
+        _NATIVE.append(self)
+
+    def check(self, rc: int, what: str) -> None:
+        from .. import _native
+
+        _native.check(rc, what)
+
+    @staticmethod
+    def dtype(t: torch.Tensor) -> int:
+        try:
+            return _DTYPE[t.dtype]
+        except KeyError:
+            raise TypeError(f"RCCL collective on {t.dtype}") from None
+
+    def bcast(self, t: torch.Tensor, root: int, stream: int) -> None:
+        self.check(self.lib.gelim_rccl_bcast(self.handle, t.data_ptr(), t.numel(), self.dtype(t), root, stream),
+                   "rccl_bcast")
+
+    def allreduce(self, t: torch.Tensor, op: str, stream: int) -> None:
+        self.check(self.lib.gelim_rccl_allreduce(self.handle, t.data_ptr(), t.data_ptr(), t.numel(), self.dtype(t),
+                                                 _OP[op], stream), "rccl_allreduce")
+
+    def allgather(self, out: torch.Tensor, t: torch.Tensor, stream: int) -> None:
+        self.check(self.lib.gelim_rccl_allgather(self.handle, t.data_ptr(), out.data_ptr(), t.numel(),
+                                                 self.dtype(t), stream), "rccl_allgather")
+
+    def sendrecv(self, send_t: torch.Tensor | None, dst: int, recv_t: torch.Tensor | None, src: int,
+                 stream: int) -> None:
+        ref = send_t if send_t is not None else recv_t
+        self.check(self.lib.gelim_rccl_sendrecv(
+            self.handle, send_t.data_ptr() if send_t is not None else None,
+            send_t.numel() if send_t is not None else 0, dst,
+            recv_t.data_ptr() if recv_t is not None else None, recv_t.numel() if recv_t is not None else 0, src,
+            self.dtype(ref), stream), "rccl_sendrecv")
+
+    def destroy(self, abort: bool = False) -> None:
+        if self.handle:
+            self.lib.gelim_rccl_comm_destroy(self.handle, int(abort))
+            self.handle = None
+        if self in _NATIVE:
+            _NATIVE.remove(self)
+
+
 @dataclass
 class Communicator:
     rank: int = 0
@@ -81,6 +158,8 @@ class Communicator:
     # distributed schedule is exercised on a one-GPU box
     pg: bool = False
     _cstream: object = field(default=None, repr=False, compare=False)
+    key: str = "world"  # store key prefix of this communicator's native RCCL id
+    _rccl: object = field(default=None, repr=False, compare=False)
 
     # -- collectives ------------------------------------------------------
     @property
@@ -88,38 +167,49 @@ class Communicator:
         return self.world_size > 1 or self.pg
 
     @property
-    def own_stream(self) -> bool:
-        """RCCL ranks issue their asynchronous collectives on a dedicated,
-        probed stream (comm_stream) rather than on torch's internal RCCL
-        stream, a pool stream whose hardware queue nobody checks: HIP maps
-        streams onto GPU_MAX_HW_QUEUES (4) queues, and a collective whose
-        queue is the lookahead side stream's would wait behind the whole
-        trailing update (profiles/hw_queues_r4.txt).  GELIM_COMM_STREAM=torch
-        restores torch's own stream (A/B)."""
-        return (self.backend == "nccl" and self.device.type == "cuda"
-                and os.environ.get("GELIM_COMM_STREAM", "own") != "torch")
+    def native(self) -> bool:
+        """RCCL ranks run their device collectives through libgelim's own
+        RCCL communicator (NativeRccl) on chosen streams; GELIM_COMM=torch
+        routes them through torch.distributed instead (A/B, and the
+        fallback if a native communicator cannot be created)."""
+        return (self.backend == "nccl" and self.device.type == "cuda" and self.distributed
+                and os.environ.get("GELIM_COMM", "native") != "torch")
+
+    def rccl(self) -> NativeRccl:
+        if self._rccl is None:
+            self._rccl = NativeRccl(f"gelim_rccl/{self.key}", self.world_size, self.rank, self.device)
+        return self._rccl
 
     def comm_stream(self) -> torch.cuda.Stream:
         """The stream this rank's asynchronous collectives run on: a
         process-lifetime stream on a hardware queue of its own, probed to run
         beside the default stream and the lookahead side stream
-        (utils/tensors.dedicated_stream).  A synchronous collective
-        (async_op=False) runs on the CURRENT stream in torch >= 2.7, so it is
-        issued under this stream."""
+        (utils/tensors.dedicated_stream) -- not torch's internal RCCL
+        stream, a pool stream whose hardware queue nobody checks: HIP maps
+        streams onto GPU_MAX_HW_QUEUES (4) queues, and a collective on the
+        side stream's queue would wait behind the whole trailing update
+        (profiles/hw_queues_r4.txt).  (Through torch, a synchronous
+        collective runs on the CURRENT stream in torch >= 2.7, so it is
+        issued under this stream.)"""
         if self._cstream is None:
             from ..utils.tensors import dedicated_stream
 
             self._cstream = dedicated_stream(self.device, "comm")
         return self._cstream
 
-    def _on_comm_stream(self, issue) -> _Event:
+    def _on_comm_stream(self, issue, *tensors: torch.Tensor) -> _Event:
         cs = self.comm_stream()
         cs.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(cs):
-            issue()
+            issue(cs.cuda_stream)
             ev = torch.cuda.Event()
             ev.record(cs)
+        for t in tensors:  # the caching allocator must not hand these out before cs is done
+            t.record_stream(cs)
         return _Event(ev)
+
+    def _cur(self) -> int:
+        return torch.cuda.current_stream(self.device).cuda_stream
 
     @property
     def staged(self) -> bool:
@@ -130,29 +220,39 @@ class Communicator:
         return self.backend == "gloo" and self.device.type == "cuda"
 
     def broadcast(self, t: torch.Tensor, src: int) -> torch.Tensor:
-        if self.distributed:
+        if self.native:
+            self.rccl().bcast(t, src, self._cur())
+        elif self.distributed:
             dist.broadcast(t, src=self.global_rank(src), group=self.group)
         return t
 
     def broadcast_async(self, t: torch.Tensor, src: int):
         """Non-blocking broadcast: returns a handle whose wait() makes the
-        current stream wait for the data (RCCL runs on its own stream, after
-        the work already queued on the current one)."""
-        if self.distributed and self.own_stream:
-            return self._on_comm_stream(lambda: dist.broadcast(t, src=self.global_rank(src), group=self.group))
+        current stream wait for the data (the collective runs on the
+        communicator's stream, after the work already queued on the current
+        one)."""
+        if self.native:
+            nc = self.rccl()
+            return self._on_comm_stream(lambda s: nc.bcast(t, src, s), t)
+        if self.distributed and self.backend == "nccl" and self.device.type == "cuda":
+            return self._on_comm_stream(lambda s: dist.broadcast(t, src=self.global_rank(src), group=self.group))
         if self.distributed:
             return dist.broadcast(t, src=self.global_rank(src), group=self.group, async_op=True)
         return _Done()
 
     def all_reduce(self, t: torch.Tensor, op: str = "sum") -> torch.Tensor:
-        if self.distributed:
+        if self.native:
+            self.rccl().allreduce(t, op, self._cur())
+        elif self.distributed:
             rop = {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN}[op]
             dist.all_reduce(t, op=rop, group=self.group)
         return t
 
     def all_gather(self, out: torch.Tensor, t: torch.Tensor) -> torch.Tensor:
         """out: (world_size * t.numel()) contiguous tensor."""
-        if self.distributed and self.staged:
+        if self.native:
+            self.rccl().allgather(out, t.contiguous(), self._cur())
+        elif self.distributed and self.staged:
             ho = torch.empty(out.numel(), dtype=out.dtype)
             dist.all_gather_into_tensor(ho, t.detach().reshape(-1).cpu(), group=self.group)
             out.view(-1).copy_(ho)
@@ -168,12 +268,14 @@ class Communicator:
         if self.distributed and self.staged:
             self.all_gather(out, t)
             return _Done()
-        if self.distributed and self.own_stream:
-            src = t.contiguous().view(-1)
-            return self._on_comm_stream(lambda: dist.all_gather_into_tensor(out.view(-1), src, group=self.group))
+        src = t.contiguous().view(-1)
+        if self.native:
+            nc = self.rccl()
+            return self._on_comm_stream(lambda s: nc.allgather(out, src, s), out, src)
+        if self.distributed and self.backend == "nccl" and self.device.type == "cuda":
+            return self._on_comm_stream(lambda s: dist.all_gather_into_tensor(out.view(-1), src, group=self.group))
         if self.distributed:
-            return dist.all_gather_into_tensor(out.view(-1), t.contiguous().view(-1), group=self.group,
-                                               async_op=True)
+            return dist.all_gather_into_tensor(out.view(-1), src, group=self.group, async_op=True)
         out.view(-1).copy_(t.reshape(-1))
         return _Done()
 
@@ -185,12 +287,18 @@ class Communicator:
                 dist.barrier(group=self.group)
 
     def send(self, t: torch.Tensor, dst: int):
+        if self.native:  # stream-ordered on the current stream
+            self.rccl().sendrecv(t, dst, None, 0, self._cur())
+            return _Done()
         if self.staged:
             h = t.detach().cpu()
             return _Staged(dist.isend(h, dst=self.global_rank(dst), group=self.group), h)
         return dist.isend(t, dst=self.global_rank(dst), group=self.group)
 
     def recv(self, t: torch.Tensor, src: int):
+        if self.native:
+            self.rccl().sendrecv(None, 0, t, src, self._cur())
+            return _Done()
         if self.staged:
             h = torch.empty(t.shape, dtype=t.dtype)
             return _Staged(dist.irecv(h, src=self.global_rank(src), group=self.group), h, t)
@@ -200,6 +308,9 @@ class Communicator:
         """Send to dst and receive from src as ONE batched p2p operation
         (batch_isend_irecv: RCCL group semantics, so a ring of such calls
         cannot deadlock on serialised send kernels).  Returns the requests."""
+        if self.native:  # one grouped RCCL send/recv on the current stream
+            self.rccl().sendrecv(send_t, dst, recv_t, src, self._cur())
+            return [_Done(), _Done()]
         if self.staged:
             hs = send_t.detach().cpu()
             hr = torch.empty(recv_t.shape, dtype=recv_t.dtype)
@@ -222,10 +333,12 @@ class Communicator:
         if not self.distributed:  # one rank: the only subgroup is itself
             return Communicator(0, 1, self.device, self.backend, None)
         g = dist.new_group(ranks=ranks, backend=self.backend if self.backend != "none" else None)
+        self._nsub = getattr(self, "_nsub", 0) + 1  # every rank makes the same calls: same keys
         if self.rank not in ranks:
             return Communicator(0, 1, self.device, self.backend, None)
+        key = f"{self.key}/sub{self._nsub}:" + "-".join(map(str, ranks))
         return Communicator(ranks.index(self.rank), len(ranks), self.device, self.backend, g,
-                            pg=self.pg, _cstream=self._cstream)
+                            pg=self.pg, _cstream=self._cstream, key=key)
 
     def overlap_probe(self, other: torch.cuda.Stream, ticks: int = 500000) -> bool:
         """True when an asynchronous collective (broadcast_async) plus the
@@ -311,6 +424,10 @@ def init_from_env(backend: str | None = None, device: str | None = None,
     return Communicator(rank, world, dev, backend)
 
 
-def destroy() -> None:
+def destroy(abort: bool = False) -> None:
+    """Release the native RCCL communicators (abort=True: ncclCommAbort,
+    after a failed peer) and the process group."""
+    for nc in list(_NATIVE):
+        nc.destroy(abort)
     if dist.is_initialized():
         dist.destroy_process_group()

@@ -175,6 +175,7 @@ class DistributedGauss:
             self._buf = torch.empty((n + 1) * D, dtype=torch.float64, device=self.device)
             self._piv = torch.zeros(D + 64, dtype=torch.int32, device=self.device)
         self._xt = None  # solution of the tail system (GPU lookahead path), set by factor_
+        self.last_issue_s = 0.0  # host time to issue the last lookahead schedule
 
     # -- data placement -----------------------------------------------------
     def empty_local(self) -> torch.Tensor:

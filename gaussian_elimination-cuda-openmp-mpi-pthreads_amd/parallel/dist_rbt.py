@@ -133,9 +133,10 @@ class DistributedRBT:
         # events -- costs 120 us eagerly and 255 us with RCCL's host side,
         # more than the GPU chain of a block at 8 ranks
         # (profiles/dist_issue_r5.md).  Only where every op is a stream op:
-        # RCCL or no collective at all (gloo and the emulated ranks meet on
-        # the host).
-        self.graph = graph and self.gpu and lookahead and comm.backend in ("none", "nccl")
+        # libgelim's native RCCL or no collective at all (gloo and the
+        # emulated ranks meet on the host; torch's ProcessGroupNCCL watchdog
+        # aborts on collectives recorded during a capture).
+        self.graph = graph and self.gpu and lookahead and (comm.backend == "none" or comm.native)
         self._graphs: dict[str, torch.cuda.CUDAGraph | None] = {}
         self.last_issue_s = None
         self._ud, self._vd = butterfly_diagonals(self.np, seed)

@@ -114,7 +114,7 @@ def main():
                     "issue_us_per_panel": min(r["factor_issue_s"] for r in rows) / max(1, G) * 1e6,
                     "gpu_us_per_panel": min(r["panels_gpu_only_s"] for r in rows) / max(1, G) * 1e6}
         del dg
-    print(json.dumps(out, indent=1))
+    print(json.dumps(out, indent=1), flush=True)
     C.destroy()
 
 

@@ -161,10 +161,11 @@ def rccl_one_rank(outdir, n_gauss=2048, n_rbt=2048):
         res.update(backend=comm.backend, pg=comm.pg, initialized=dist.is_initialized(),
                    pg_backend=str(dist.get_backend()), world=dist.get_world_size())
         side = side_stream(dev)
+        res["native"] = comm.native
         res["overlap_own_stream"] = comm.overlap_probe(side)
-        os.environ["GELIM_COMM_STREAM"] = "torch"
+        os.environ["GELIM_COMM"] = "torch"  # torch.distributed's RCCL path (same dedicated stream)
         res["overlap_torch_stream"] = comm.overlap_probe(side)
-        os.environ.pop("GELIM_COMM_STREAM")
+        os.environ.pop("GELIM_COMM")
         res["streams"] = {"side": side.cuda_stream, "comm": comm.comm_stream().cuda_stream,
                           "default": torch.cuda.current_stream(dev).cuda_stream}
         res["side_stream_stats"] = list(side_stream_stats())
@@ -181,8 +182,12 @@ def rccl_one_rank(outdir, n_gauss=2048, n_rbt=2048):
         for tag, kw in (("gauss_la_tail0", dict(tail=0)), ("gauss_la", {}), ("gauss_serial", dict(lookahead=False))):
             xp, tp, G = run_gauss(comm, n_gauss, **kw)
             xn, tn, _ = run_gauss(none, n_gauss, **kw)
+            os.environ["GELIM_COMM"] = "torch"
+            xt, tt, _ = run_gauss(comm, n_gauss, **kw)
+            os.environ.pop("GELIM_COMM")
             torch.save(xp, out / f"{tag}.pt")
-            res[tag] = {"bitwise": bool(torch.equal(xp, xn)), "panels": G, "rccl_s": tp, "none_s": tn}
+            res[tag] = {"bitwise": bool(torch.equal(xp, xn)), "torch_path_bitwise": bool(torch.equal(xt, xn)),
+                        "panels": G, "rccl_s": tp, "none_s": tn, "rccl_torch_path_s": tt}
 
         def run_rbt(c, n, graph=True):
             """Three solves: eager, captured + replayed, replayed (graph=True)."""
@@ -201,8 +206,13 @@ def rccl_one_rank(outdir, n_gauss=2048, n_rbt=2048):
         xp, tp, mp_ = run_rbt(comm, n_rbt)
         xn, tn, mn_ = run_rbt(none, n_rbt)
         xe, te, _ = run_rbt(comm, n_rbt, graph=False)
+        os.environ["GELIM_COMM"] = "torch"
+        xt, tt, mt_ = run_rbt(comm, n_rbt)  # torch.distributed's RCCL: eager (no capture)
+        os.environ.pop("GELIM_COMM")
+        xe = xe + xt
         torch.save(xp[-1], out / "rbt.pt")
         res["rbt"] = {"bitwise": bool(torch.equal(xp[-1], xn[-1])), "rccl_s": tp, "none_s": tn, "rccl_eager_s": te,
+                      "rccl_torch_path_s": tt, "graph_torch_path": mt_[3],
                       "graph_rccl": mp_[3], "graph_none": mn_[3],
                       "replay_equals_eager": all(torch.equal(x, xe[0]) for x in xp + xn + xe),
                       "steps": mp_[0], "berr": mp_[1], "fallback": mp_[2]}

@@ -48,13 +48,13 @@ def rccl_run(tmp_path_factory, cuda):
 
 def test_rccl_group_is_real(rccl_run):
     _, res = rccl_run
-    assert res["backend"] == "nccl" and res["pg"] and res["initialized"]
+    assert res["backend"] == "nccl" and res["pg"] and res["initialized"] and res["native"]
     assert res["pg_backend"] == "nccl" and res["world"] == 1
 
 
 def test_rccl_collectives_beside_side_stream(rccl_run):
     _, res = rccl_run
-    assert res["overlap_own_stream"], res
+    assert res["overlap_own_stream"] and res["overlap_torch_stream"], res
     s = res["streams"]
     assert len({s["side"], s["comm"], s["default"]}) == 3
 
@@ -63,7 +63,7 @@ def test_rccl_collectives_beside_side_stream(rccl_run):
 def test_rccl_dist_gauss_bitwise(rccl_run, gelim, tag):
     out, res = rccl_run
     r = res[tag]
-    assert r["bitwise"], r
+    assert r["bitwise"] and r["torch_path_bitwise"], r
     if tag == "gauss_la_tail0":
         assert r["panels"] >= 4
     x = torch.load(out / f"{tag}.pt")
@@ -78,7 +78,7 @@ def test_rccl_dist_rbt_bitwise(rccl_run, gelim):
     assert r["bitwise"], r
     # the graph-replayed schedule (factorisation + applies captured once, RCCL
     # collectives inside the graph) gives the eager schedule's bits
-    assert r["graph_rccl"] and r["graph_none"], r
+    assert r["graph_rccl"] and r["graph_none"] and not r["graph_torch_path"], r
     assert r["replay_equals_eager"], r
     assert r["fallback"] is None
     assert r["berr"] <= 64 * torch.finfo(torch.float64).eps

@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--n", type=int, default=8192)
     ap.add_argument("--pg", action="store_true")
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--out", default=None, help="also write the JSON here")
     a = ap.parse_args()
     import torch
 
@@ -115,6 +116,8 @@ def main():
                     "gpu_us_per_panel": min(r["panels_gpu_only_s"] for r in rows) / max(1, G) * 1e6}
         del dg
     print(json.dumps(out, indent=1), flush=True)
+    if a.out:
+        Path(a.out).write_text(json.dumps(out, indent=1))
     C.destroy()
 
 

@@ -25,10 +25,9 @@ between device syncs + barriers, max over ranks):
   dist_matmul_16384(_s) 16384^2 fp32 over ALL N ranks (strong scaling)
   gauss_8192_1gpu(_s)   one 8192^2 system per GPU on the single-GPU solver
   hip_pivot_2048        the per-pivot algorithm (fp64, fp32)
-  gauss_rbt             the randomised no-pivoting engines at 2048 / 8192: hip-rbt
+  gauss_rbt             the randomised no-pivoting engine at 2048 / 8192 / 16384: hip-rbt
                         (butterfly transform + fp64 block-LDU on the matrix cores +
-                        fp64 refinement to a componentwise backward error <= 4 eps)
-                        and hip-mixed (same with fp32 trailing products + GMRES-IR);
+                        fp64 refinement to a componentwise backward error <= 4 eps);
                         fp64-class answers by a different algorithm than the
                         headline's partial pivoting, so reported beside it
   external_matrices     the reference's .dat matrices vs its best OpenMP times
@@ -288,7 +287,7 @@ def main() -> None:
             result[short] = v["time_s"]
     rb = result.get("gauss_rbt")
     if isinstance(rb, dict):
-        for nn in ("2048", "8192"):
+        for nn in ("2048", "8192", "16384"):
             v = rb.get(nn, {}).get("hip-rbt")
             if isinstance(v, dict) and "time_s" in v:
                 result[f"gauss_{nn}_rbt_s"] = v["time_s"]
@@ -385,7 +384,9 @@ def bench_dist_rbt(comm, gelim, torch, n: int) -> dict:
     """The n^2 system over ALL ranks with the randomised block-LDU engine
     (parallel/dist_rbt.py: butterfly transform local to each rank, one
     [Dinv_k | L_k] broadcast per 128-column block with lookahead, super-block
-    solves, fp64 refinement on the original system); second solve timed.  One
+    solves, fp64 refinement on the original system; the factorisation loop
+    and the applies replayed from hipGraphs with libgelim's RCCL
+    communicators inside); third solve timed.  One
     rank: the single-GPU native solve of the same padded system, and the
     distributed schedule on that one rank beside it."""
     from gelim.parallel import DistributedRBT
@@ -398,7 +399,7 @@ def bench_dist_rbt(comm, gelim, torch, n: int) -> dict:
         def run():
             holder["x"] = d.solve_(holder.pop("loc"))
 
-        for _ in range(2):
+        for _ in range(3):  # eager, captured into a hipGraph, replayed: the last is timed
             holder["loc"] = d.generate_random(seed=99)
             dt = _timed(comm, torch, dev, run)
         return dt, holder["x"]
@@ -408,7 +409,8 @@ def bench_dist_rbt(comm, gelim, torch, n: int) -> dict:
     out = {"time_s": dt, "error": gelim.ops.gauss.error_metric(x), "ranks": comm.world_size,
            "padded_order": d.np, "corrections": d.last_steps, "backward_error": d.last_berr,
            "fallback": d.last_fallback, "tflops_total": (2.0 / 3.0) * n ** 3 / dt * 1e-12,
-           "path": "single-GPU native solve" if d.fast else "distributed schedule"}
+           "path": "single-GPU native solve" if d.fast else "distributed schedule",
+           "graph": bool(getattr(d, "graph", False)), "native_rccl": comm.native}
     d.close()
     if comm.world_size == 1:
         d1 = DistributedRBT(comm, n, single_fast_path=False)
@@ -474,25 +476,23 @@ def bench_single(comm, gelim, torch, n: int, seed: int, reps: int = 3) -> dict:
 
 
 def bench_rbt(comm, gelim, torch) -> dict:
-    """Randomised no-pivoting engines (each rank its own system): the whole
-    solve (transform, factorisation, refinement) per call, with the
+    """The randomised no-pivoting engine hip-rbt (each rank its own system):
+    the whole solve (transform, factorisation, refinement) per call, with the
     refinement's correction count, its final componentwise backward error and
     whether it fell back to partial pivoting."""
     dev = comm.device
     out = {}
-    for n in (2048, 8192):
+    for n in (2048, 8192, 16384):
         aug = gelim.random_system(n, seed=31 + n, device=dev)
-        res = {}
-        for backend in ("hip-rbt", "hip-mixed"):
-            s = gelim.GaussSolver(n, backend=backend, device=dev)
-            holder = {}
-            s.solve(aug)
-            dt = _timed(comm, torch, dev, lambda: holder.__setitem__("x", s.solve(aug)), reps=3)
-            res[backend] = {"time_s": dt, "error": gelim.ops.gauss.error_metric(holder["x"]),
-                            "corrections": s.last_steps, "gmres_iterations": s.last_inner,
-                            "backward_error": s.last_berr, "fallback": s.last_fallback}
-            s.close()
-        out[str(n)] = res
+        s = gelim.GaussSolver(n, backend="hip-rbt", device=dev)
+        holder = {}
+        s.solve(aug)
+        dt = _timed(comm, torch, dev, lambda: holder.__setitem__("x", s.solve(aug)), reps=3)
+        out[str(n)] = {"hip-rbt": {"time_s": dt, "error": gelim.ops.gauss.error_metric(holder["x"]),
+                                   "corrections": s.last_steps, "backward_error": s.last_berr,
+                                   "fallback": s.last_fallback}}
+        s.close()
+        del aug
     return out
 
 

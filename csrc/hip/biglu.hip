@@ -435,40 +435,13 @@ int factor(double* A, int64_t lda, int64_t m, int64_t c0, int mode, int* ipiv, i
 size_t workspace_bytes() { return leafk::kKeyBytes + leafk::kRowBytes + sleaf::scratch_bytes(); }
 int leaf_width() { return LW; }
 
-// Leaf participant shape (waves x rows per lane), GELIM_LEAF_SHAPE = 1x1 |
-// 1x2 | 1x4 | 2x2 | 4x1 | 4x4 (read once; default 1x2: one wave of 128
-// rows, 2 per lane, the 32-column panel in 128 architectural VGPRs); a shape
-// that would need more than kMaxP participants falls back to 1x2 (m <= 32768),
-// 2x2 (m <= 65536), then 4x4.  Measured (profiles/leaf_shape_r4.txt), whole
-// solves 3072 / 4096 / 8192 / 16384: 1x2 7.7 / 11.5 / 31.3 / 125.4 ms, 2x2
-// 7.9 / 12.0 / 31.8 / 127.0, 1x4 (round 3: half of its 256-VGPR panel in
-// AGPRs, every update of it accvgpr read + FMA + accvgpr write) 8.2 / 12.5 /
-// 33.8 / 129.1, 1x1 7.8 / 11.8 / 31.8 / 131.1, 4x1 8.6 / 13.6 / 34.6 / 132.7.
-// GELIM_LEAF_WAVES = 1 | 2 | 4 (older knob) maps to 1x4 | 2x2 | 4x4.
+// Leaf participant shape for m rows: one wave of 2 rows per lane (1x2, the
+// measured best, profiles/leaf_shape_r4.txt), then 2x2 and 4x4 waves x rows
+// per lane as m outgrows kMaxP participants of the smaller shape.  (1x4, 1x1
+// and 4x1 were measured and dropped in round 5 with their knobs.)
 LeafShape leaf_shape(int64_t m) {
-  static const LeafShape env = [] {
-    if (const char* e = std::getenv("GELIM_LEAF_SHAPE")) {
-      const std::string v(e);
-      if (v == "1x4") return LeafShape{1, 4};
-      if (v == "1x2") return LeafShape{1, 2};
-      if (v == "1x1") return LeafShape{1, 1};
-      if (v == "2x2") return LeafShape{2, 2};
-      if (v == "4x1") return LeafShape{4, 1};
-      if (v == "4x4") return LeafShape{4, 4};
-      return LeafShape{1, 2};
-    }
-    if (const char* e = std::getenv("GELIM_LEAF_WAVES")) {
-      const int v = std::atoi(e);
-      if (v == 1) return LeafShape{1, 4};
-      if (v == 2) return LeafShape{2, 2};
-      if (v == 4) return LeafShape{4, 4};
-    }
-    return LeafShape{1, 2};
-  }();
-  auto fits = [&](LeafShape sh) { return m <= (int64_t)leafk::kMaxP * 64 * sh.nwv * sh.rw; };  // <= kMaxP participants
-  if (fits(env)) return env;
   for (LeafShape sh : {LeafShape{1, 2}, LeafShape{2, 2}})
-    if (sh.nwv * sh.rw > env.nwv * env.rw && fits(sh)) return sh;
+    if (m <= (int64_t)leafk::kMaxP * 64 * sh.nwv * sh.rw) return sh;
   return LeafShape{4, 4};
 }
 int leaf_waves(int64_t m) { return leaf_shape(m).nwv; }
@@ -526,26 +499,17 @@ int leaf_factor(double* A, int64_t lda, int64_t m, int64_t c0, int mode, int* ip
   a.x.key = static_cast<leafk::u32x4*>(ws);
   a.x.row = reinterpret_cast<leafk::u32x4*>(static_cast<char*>(ws) + leafk::kKeyBytes);
   a.stamps = stamps;
-  // fused sweep (the key sweep carries every candidate row, P <= 32) vs key
-  // sweep then row load (GELIM_LEAF_2HOP=1); within noise of each other for
-  // single-wave participants (profiles/leaf_fused_vs_2hop.txt)
-  static const bool fused = std::getenv("GELIM_LEAF_2HOP") == nullptr;
+  // fused sweep: the key sweep carries every candidate row (P <= 32); the
+  // two-hop form (key sweep, then a row load) is what larger P takes inside
+  // the leaf (profiles/leaf_fused_vs_2hop.txt)
+  constexpr bool fused = true;
   const bool zero = mode != GELIM_PIVOT_PARTIAL;
-  if (shp.nwv == 1 && shp.rw == 4) {
-    if (zero) leafk::launch_leaf_shape<1, 4, 0>(a, fused, s);
-    else leafk::launch_leaf_shape<1, 4, 1>(a, fused, s);
-  } else if (shp.nwv == 1 && shp.rw == 1) {
-    if (zero) leafk::launch_leaf_shape<1, 1, 0>(a, fused, s);
-    else leafk::launch_leaf_shape<1, 1, 1>(a, fused, s);
-  } else if (shp.nwv == 1 && shp.rw == 2) {
+  if (shp.nwv == 1) {
     if (zero) leafk::launch_leaf_shape<1, 2, 0>(a, fused, s);
     else leafk::launch_leaf_shape<1, 2, 1>(a, fused, s);
   } else if (shp.nwv == 2) {
     if (zero) leafk::launch_leaf_shape<2, 2, 0>(a, fused, s);
     else leafk::launch_leaf_shape<2, 2, 1>(a, fused, s);
-  } else if (shp.rw == 1) {
-    if (zero) leafk::launch_leaf_shape<4, 1, 0>(a, fused, s);
-    else leafk::launch_leaf_shape<4, 1, 1>(a, fused, s);
   } else {
     if (zero) leafk::launch_leaf_shape<4, 4, 0>(a, fused, s);
     else leafk::launch_leaf_shape<4, 4, 1>(a, fused, s);
@@ -632,14 +596,9 @@ int laswp_net(double* A, int64_t lda, const int* net, int64_t lbeg, int64_t lend
 
 // U12 = L11^-1 C for the nb rows of C (ldc) over ncols columns, L11 the unit
 // lower nb x nb block at L (ldl); nb <= 256, a multiple of 32.
-// GELIM_TRSM_FUSED=0: the per-32-row-block TRSM + GEMM sequence instead
-bool trsm_fused() {
-  static const bool v = [] {
-    const char* e = std::getenv("GELIM_TRSM_FUSED");
-    return !(e && std::atoi(e) == 0);
-  }();
-  return v;
-}
+// the fused TRSM kernel (the per-32-row-block TRSM + GEMM sequence it
+// replaced is kept for the distributed apply's long panels)
+bool trsm_fused() { return true; }
 
 int panel_trsm(double* C, int64_t ldc, int64_t ncols, int64_t nb, const double* L, int64_t ldl, hipStream_t s,
                int max_wg) {

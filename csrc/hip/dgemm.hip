@@ -77,7 +77,6 @@ struct Args {
   double alpha;
   int acc;  // 1: C += alpha A B, 0: C = alpha A B (C is not read)
   int group;  // tile order: runs of `group` tile rows, column-major inside a run (<= 1: row-major)
-  int wt;     // 1: C stored write-through (agent-scope sc1 stores: no dirty L2 left for the next launch boundary)
 };
 
 // Tile index -> (tile row, tile column).  Grouped order: the 64 workgroups an
@@ -228,13 +227,7 @@ __device__ __forceinline__ void tile_body(const Args& g, int m0, int n0, double*
       for (int r = 0; r < 4; ++r) {
         const int row = m0 + wm + 16 * i + q + 4 * r;
         if (store && (FULL || (row < g.M && col < g.N))) {
-          double* cp = g.C + (int64_t)row * g.ldc + col;
-          if (g.wt)
-            __hip_atomic_store(reinterpret_cast<unsigned long long*>(cp),
-                               (unsigned long long)__double_as_longlong(acc[i][j][r]), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-          else
-            *cp = acc[i][j][r];
+          g.C[(int64_t)row * g.ldc + col] = acc[i][j][r];
         }
       }
     }
@@ -299,7 +292,9 @@ __global__ __launch_bounds__(kPThreads, 1) void dgemm_persist_kernel(Args g) {
 
 // C (M x N, ldc) += alpha * A (M x K, lda) * B (K x N, ldb); alpha in {+1, -1}
 // in practice (any value works: A is scaled once on its way into LDS).
-// group < 0: the GELIM_DGEMM_GROUP tile order (read once), else that order.
+// group < 0: row-major tile order (grouped orders 4 / 8 / 16 measured within
+// noise of it, profiles/dgemm_r3_lds.txt), else that order.  C is stored
+// plainly (write-through stores were within noise, profiles/dgemm_wt_r4.txt).
 int dgemm_launch(double* C, int64_t ldc, const double* A, int64_t lda, const double* B, int64_t ldb, int64_t M,
                  int64_t N, int64_t K, double alpha, int max_wg, hipStream_t s, int accumulate, int group_arg) {
   if (M <= 0 || N <= 0 || K <= 0) return GELIM_OK;
@@ -311,16 +306,8 @@ int dgemm_launch(double* C, int64_t ldc, const double* A, int64_t lda, const dou
     return GELIM_FAIL(GELIM_E_ARG, "dgemm: unsupported alignment / leading dimensions (K=" + std::to_string(K) +
                                        " lda=" + std::to_string(lda) + " ldb=" + std::to_string(ldb) + ")");
   const int tm = (int)((M + BM - 1) / BM), tn = (int)((N + BN - 1) / BN);
-  static const int group_env = [] {
-    const char* e = std::getenv("GELIM_DGEMM_GROUP");
-    return e ? std::atoi(e) : 1;  // grouped orders 4 / 8 / 16 measured within noise of row-major
-  }();
-  const int group = group_arg >= 0 ? group_arg : group_env;
-  static const int wt = [] {
-    const char* e = std::getenv("GELIM_DGEMM_WT");
-    return e ? std::atoi(e) != 0 : 0;
-  }();
-  Args g{C, ldc, A, lda, B, ldb, (int)M, (int)N, (int)K, tn, tm * tn, alpha, accumulate ? 1 : 0, group, wt};
+  const int group = group_arg >= 0 ? group_arg : 1;
+  Args g{C, ldc, A, lda, B, ldb, (int)M, (int)N, (int)K, tn, tm * tn, alpha, accumulate ? 1 : 0, group};
   // max_wg > 0: at most max_wg CUs (rounded down to a multiple of 8)
   const int cap = max_wg > 0 ? std::max(8, max_wg / 8 * 8) : 0;
   // few tiles: one 256-thread workgroup per tile already stays within the
@@ -343,21 +330,10 @@ int dgemm_launch(double* C, int64_t ldc, const double* A, int64_t lda, const dou
       (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
       return cus;
     }();
-    static const int force = [] {
-      const char* e = std::getenv("GELIM_DGEMM_TILE");
-      return e ? std::atoi(e) : 0;
-    }();
-    const bool small = force ? force == 64 : (int64_t)tm * tn < (int64_t)ncu;
-    // thin problems with a short K (the block-LDU engine's column / row block
-    // updates and W products, K = 128 / 256): the register-direct kernel of
-    // dgemm_thin.hip (no LDS, no per-K-step barrier), GELIM_DGEMM_THIN=0 off
-    static const int thin = [] {
-      const char* e = std::getenv("GELIM_DGEMM_THIN");
-      return e ? std::atoi(e) : 0;
-    }();
-    if (thin && small && cap == 0 && force == 0 && K <= 256 &&
-        dgemm_thin(C, ldc, A, lda, B, ldb, M, N, K, alpha, accumulate, 0, s) == GELIM_OK)
-      return GELIM_OK;
+    // (the register-direct thin kernel of dgemm_thin.hip measured no faster
+    // at the block-LDU engine's K = 128 / 256 shapes, profiles/dgemm_thin_r4.txt;
+    // it stays callable as gelim_gpu_dgemm_thin)
+    const bool small = (int64_t)tm * tn < (int64_t)ncu;
     if (small && cap == 0) {
       const int tm6 = (int)((M + 63) / 64), tn6 = (int)((N + 63) / 64);
       Args g6 = g;

@@ -270,8 +270,7 @@ int matmul_f32(const float* A, int64_t lda, const float* B, int64_t ldb, float* 
       (void)hipGetDevice(&dev);
       (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
       const int64_t big_tiles = ((M + 127) / 128) * ((N + 127) / 128);
-      const char* ev = std::getenv("GELIM_SGEMM_TILE");
-      const bool big = ev ? std::atoi(ev) == 128 : big_tiles >= 2 * (int64_t)cus;
+      const bool big = big_tiles >= 2 * (int64_t)cus;
       auto launch = [&](auto tag) {
         constexpr int BM = decltype(tag)::BM, BN = decltype(tag)::BN, BK = decltype(tag)::BK;
         const int tiles_m = (int)((M + BM - 1) / BM), tiles_n = (int)((N + BN - 1) / BN);
@@ -285,20 +284,11 @@ int matmul_f32(const float* A, int64_t lda, const float* B, int64_t ldb, float* 
           hipLaunchKernelGGL((mfma_gemm_kernel<true, BM, BN, BK>), dim3(ntiles), dim3(kMmThreads), 0, s, p,
                              tiles_n, ntiles);
       };
-      // GELIM_SGEMM_SHAPE=BMxBNxBK: A/B runs of other tile shapes
-      const char* sv = std::getenv("GELIM_SGEMM_SHAPE");
-      const int shape = sv ? std::atoi(sv) * 1000000 + std::atoi(std::strchr(sv, 'x') ? std::strchr(sv, 'x') + 1 : sv) * 1000 +
-                                 std::atoi(std::strrchr(sv, 'x') ? std::strrchr(sv, 'x') + 1 : sv)
-                           : 0;
       // measured (profiles/gemm_microbench.txt, round 2): 128x64x16 is the
       // fastest shape once there are >= 2 128x128 tiles per CU (8192^2: 125
-      // vs 120 TF for 128x128x32), 64x64x16 below (2048^2)
-      if (shape == 64064032) launch(Shape<64, 64, 32>{});
-      else if (shape == 128128032) launch(Shape<128, 128, 32>{});
-      else if (shape == 128064032) launch(Shape<128, 64, 32>{});
-      else if (shape == 64128016) launch(Shape<64, 128, 16>{});
-      else if (shape == 64064016) launch(Shape<64, 64, 16>{});
-      else if (big || shape == 128064016) launch(Shape<128, 64, 16>{});
+      // vs 120 TF for 128x128x32), 64x64x16 below (2048^2); 64x64x32,
+      // 128x128x32, 128x64x32 and 64x128x16 were slower at both
+      if (big) launch(Shape<128, 64, 16>{});
       else launch(Shape<64, 64, 16>{});
       break;
     }

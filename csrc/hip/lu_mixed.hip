@@ -1,33 +1,19 @@
-// Randomised no-pivoting engines (GaussSolver backends "hip-mixed" and
-// "hip-rbt"): a random butterfly transform (RBT) of the system, a NO-pivoting
-// blocked LU of the transformed matrix on the matrix cores -- fp32 factors
-// ("hip-mixed") or fp64 factors ("hip-rbt") -- and fp64 iterative refinement
-// against the original system (the loop is in models/gauss_solver.py; when it
-// does not reach the fp64 error class the solver falls back to the fp64
-// partial-pivoting engine by itself).
+// Randomised no-pivoting engine (GaussSolver backend "hip-rbt"): a random
+// butterfly transform (RBT) of the system, a NO-pivoting blocked LU of the
+// transformed matrix on the fp64 matrix cores, and fp64 iterative refinement
+// against the original system (gelim_mixed_solve; when it does not reach the
+// fp64 error class the solver falls back to the partial-pivoting engine).
+// (Round 3-4 also had fp32 trailing products + GMRES-IR, "hip-mixed": slower
+// than this fp64 engine at every n and not convergent at 16384 -- removed in
+// round 5, profiles/trsv_split_r5.txt.)
 //
-// Why: every exact partial-pivoting engine here is bound by its pivot chain
-// (one global arg-max per column: ~3 us per column on the wide-panel leaves
-// at n = 8192, profiles/leaf_fused_vs_2hop.txt).  A two-sided recursive
-// butterfly transform U^T A V (Parker 1995; Baboulin, Dongarra et al. 2013)
-// makes pivoting unnecessary with probability close to one, and without
-// pivoting the factorisation has no per-column global reduction at all.  The
-// reference's loop (OpenMP_and_MPI/gauss_openmp/gauss_external_input.c:153-182,
-// fp64, partial pivoting) is what the refinement answers to: the residual is
-// always taken in fp64 on the ORIGINAL system.
-//
-// Factorisation (T = float or double): block LDU without pivoting, 128-column
-// blocks.  Per block k:
-//  * diag_inv_kernel: ONE workgroup inverts the (Schur) diagonal block A_kk
-//    by Gauss-Jordan in fp64 registers (8 x 8 tiles per thread, one uniform
-//    rank-1 update and one barrier per column) -> Dinv_k (kept for the solves);
+// Factorisation: block LDU without pivoting, 128-column blocks.  Per block k:
+//  * diag_inv_pair_kernel: ONE workgroup inverts the (Schur) diagonal block
+//    A_kk by Gauss-Jordan in fp64 registers (4 x 8 tiles per thread, uniform
+//    rank-1 updates, one barrier per two columns) -> Dinv_k (kept for the solves);
 //  * W = A_kk^-1 A_k,rest and A_rest,rest -= A_rest,k W on the matrix cores
-//    (fp64 dgemm.hip v_mfma_f64_16x16x4f64, or fp32 gemm_f32.hip
-//    v_mfma_f32_32x32x2f32 with a rounded copy of the inverse).  A_rest,k and
-//    A_k,rest stay in place as the factor's off-diagonal blocks.
-// The fp32 engine still inverts in fp64: an fp32 Gauss-Jordan of a no-pivoting
-// block with cond ~1e7 would be useless, while a correctly rounded copy of an
-// accurate inverse only costs eps32 relative in W.
+//    (dgemm.hip v_mfma_f64_16x16x4f64).  A_rest,k and A_k,rest stay in place
+//    as the factor's off-diagonal blocks.
 //
 // Solves (blk_trsv_kernel, one persistent launch per direction): workgroup w
 // owns block row b (128 equations); it applies the solved blocks before it in
@@ -62,8 +48,6 @@
 #include "rbt.h"
 
 namespace gelim {
-int matmul_f32(const float* A, int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc, int64_t M, int64_t N,
-               int64_t K, int accumulate, int kernel, hipStream_t s, float alpha, double* C64);
 int dgemm_ex(double* C, int64_t ldc, const double* A, int64_t lda, const double* B, int64_t ldb, int64_t M,
              int64_t N, int64_t K, double alpha, int accumulate, hipStream_t s);
 int dgemm_capped(double* C, int64_t ldc, const double* A, int64_t lda, const double* B, int64_t ldb, int64_t M,
@@ -155,17 +139,17 @@ __global__ __launch_bounds__(256) void rbt_vec_kernel(const double* __restrict__
 // solves) and two GEMMs, W = A11^-1 A12 and A22 -= A21 W; A21 / A12 stay in
 // place as the factor's off-diagonal blocks.
 //
-// One workgroup of 256 threads (one wave per SIMD) inverts the 128 x 128
+// One workgroup of 512 threads (two waves per SIMD) inverts the 128 x 128
 // block in place in registers: thread (rg, cg) = (t >> 4, t & 15) holds the
-// 8 x 8 tile rows 8 rg.., columns 8 cg...  Step k of Gauss-Jordan is ONE
+// 4 x 8 tile rows 4 rg.., columns 8 cg...  Step k of Gauss-Jordan is ONE
 // uniform rank-1 update of the whole block,
 //   a[i][j] -= g_i u_j,  g_i = a[i][k] - [i == k],  u_j = a[k][j] / a[k][k] (j != k),  u_k = 1 + 1 / a[k][k],
 // which gives a'[k][k] = 1/a_kk, a'[k][j] = a_kj/a_kk, a'[i][k] = -a_ik/a_kk
 // and the Schur update elsewhere with no special cases.  Row k and column k
 // are published raw through parity-buffered LDS one step ahead (one barrier
-// per step), and the step loop is unrolled by 8 so every in-tile index (k % 8)
-// is static: publishing is a predicated store, not a register pick.  ~500
-// cycles per step, 128 steps: 72 us per block (the earlier LU + two
+// per PAIR of steps, below), and the step loop is unrolled by 8 so every
+// in-tile index (k % 8) is static: publishing is a predicated store, not a
+// register pick.  57 us per block (the earlier LU + two
 // triangular-inverse loops with one row per lane: 330 us, instruction-bound;
 // a 4-column blocked Gauss-Jordan step -- explicit 4 x 4 pivot-block inverse,
 // rank-4 update -- was slower, 81 us, and lost accuracy: refinement needed
@@ -180,12 +164,6 @@ constexpr int kTl = 8;    // tile columns (and rows, TR = 8)
 constexpr int kGjStride = kTl + 2;
 constexpr int gj_at(int i) { return (i / kTl) * kGjStride + i % kTl; }
 
-template <typename TI>
-struct alignas(16) GjLds {
-  TI row[2][NB / kTl * kGjStride];
-  TI col[2][NB / kTl * kGjStride];
-};
-
 // 1 / pivot: v_rcp_f64 + two Newton steps (within an ulp of the IEEE
 // quotient; the refinement absorbs the rest) -- 3 dependent FMAs instead of
 // the ~8-deep IEEE division sequence on the critical path of every column
@@ -193,117 +171,6 @@ __device__ __forceinline__ double gj_recip(double piv) {
   double pk = __builtin_amdgcn_rcp(piv);
   pk = fma(pk, fma(-piv, pk, 1.0), pk);
   return fma(pk, fma(-piv, pk, 1.0), pk);
-}
-
-// Step k = 8 kg + KK of the Gauss-Jordan inverse on TR x 8 tiles (TR = 8:
-// 256 threads, one wave per SIMD; TR = 4: 512 threads, two waves per SIMD).
-// The raw row / column are published and every thread scales after the
-// barrier (publishing u and g ready to use -- the reciprocal taken from the
-// pivot's lane by v_readlane in the publishing wave -- made the factor 7 %
-// slower: the publisher's longer path before its bulk update is the
-// critical one, profiles/rbt_engine_round3.txt).
-template <int TR, int KK>
-__device__ __forceinline__ void gj_step(double (&a)[TR][kTl], GjLds<double>& sh, int kg, int rg, int cg) {
-  const int k = kTl * kg + KK;
-  constexpr int par = KK & 1;  // kTl is even: k and KK share parity
-  constexpr int RPG = kTl / TR;  // row groups per column group
-  const double pk = gj_recip(sh.row[par][gj_at(k)]);
-  double u[kTl], g[TR];
-#pragma unroll
-  for (int j = 0; j < kTl; j += 2) {
-    const double2 v = *reinterpret_cast<const double2*>(&sh.row[par][kGjStride * cg + j]);
-    u[j] = v.x * pk;
-    u[j + 1] = v.y * pk;
-  }
-#pragma unroll
-  for (int i = 0; i < TR; i += 2) {
-    const double2 v = *reinterpret_cast<const double2*>(&sh.col[par][gj_at(TR * rg) + i]);
-    g[i] = v.x;
-    g[i + 1] = v.y;
-  }
-  u[KK] = (cg == kg) ? 1.0 + pk : u[KK];
-  g[KK % TR] -= (rg == RPG * kg + KK / TR) ? 1.0 : 0.0;
-  // next step's pivot row (in-tile row r1 of row group rg1) and column
-  constexpr int kk1 = (KK + 1) % kTl;
-  constexpr int r1 = (KK + 1) % TR;
-  const int kg1 = KK + 1 == kTl ? kg + 1 : kg;
-  const int rg1 = (k + 1) / TR;
-  const bool more = k + 1 < NB;
-  // the next step's pivot row / column first: their LDS stores then drain
-  // under the bulk of the update instead of after it
-#pragma unroll
-  for (int j = 0; j < kTl; ++j) a[r1][j] = fma(-g[r1], u[j], a[r1][j]);
-#pragma unroll
-  for (int i = 0; i < TR; ++i)
-    if (i != r1) a[i][kk1] = fma(-g[i], u[kk1], a[i][kk1]);
-  if (more && rg == rg1) {
-#pragma unroll
-    for (int j = 0; j < kTl; j += 2)
-      *reinterpret_cast<double2*>(&sh.row[par ^ 1][kGjStride * cg + j]) = make_double2(a[r1][j], a[r1][j + 1]);
-  }
-  if (more && cg == kg1) {
-#pragma unroll
-    for (int i = 0; i < TR; i += 2)
-      *reinterpret_cast<double2*>(&sh.col[par ^ 1][gj_at(TR * rg) + i]) = make_double2(a[i][kk1], a[i + 1][kk1]);
-  }
-#pragma unroll
-  for (int i = 0; i < TR; ++i)
-#pragma unroll
-    for (int j = 0; j < kTl; ++j)
-      if (i != r1 && j != kk1) a[i][j] = fma(-g[i], u[j], a[i][j]);
-  __syncthreads();
-}
-
-template <int TR, int... KK>
-__device__ __forceinline__ void gj_steps(double (&a)[TR][kTl], GjLds<double>& sh, int kg, int rg, int cg,
-                                         std::integer_sequence<int, KK...>) {
-  (gj_step<TR, KK>(a, sh, kg, rg, cg), ...);
-}
-
-// Dinv = Ablk^-1 (fp64, row-major NB x NB) of the NB x NB T block at Ablk
-// (leading dimension lda); with Tinv, also a T copy (the fp32 engine's GEMM
-// operand).  The block is read, not modified.  info: atomicMin of 1 + k0 (the
-// block's first global column) when the inverse is not finite (a zero / tiny
-// pivot).
-template <typename T, int TR>
-__global__ __launch_bounds__(16 * NB / TR) void diag_inv_kernel(const T* __restrict__ Ablk, int64_t lda, int k0,
-                                                               double* __restrict__ Dinv, T* __restrict__ Tinv,
-                                                               int* __restrict__ info) {
-  __shared__ GjLds<double> sh;
-  const int t = threadIdx.x, rg = t >> 4, cg = t & 15;
-  double a[TR][kTl];
-#pragma unroll
-  for (int i = 0; i < TR; ++i) {
-    const T* src = Ablk + (int64_t)(TR * rg + i) * lda + kTl * cg;
-#pragma unroll
-    for (int j = 0; j < kTl; ++j) a[i][j] = (double)src[j];
-  }
-  if (rg == 0) {
-#pragma unroll
-    for (int j = 0; j < kTl; ++j) sh.row[0][kGjStride * cg + j] = a[0][j];
-  }
-  if (cg == 0) {
-#pragma unroll
-    for (int i = 0; i < TR; ++i) sh.col[0][gj_at(TR * rg) + i] = a[i][0];
-  }
-  __syncthreads();
-  for (int kg = 0; kg < NB / kTl; ++kg) gj_steps<TR>(a, sh, kg, rg, cg, std::make_integer_sequence<int, kTl>{});
-  bool fin = true;
-#pragma unroll
-  for (int i = 0; i < TR; ++i) {
-    double* dst = Dinv + (int64_t)(TR * rg + i) * NB + kTl * cg;
-#pragma unroll
-    for (int j = 0; j < kTl; ++j) {
-      fin = fin && isfinite(a[i][j]);
-      dst[j] = a[i][j];
-    }
-    if (Tinv) {
-      T* tdst = Tinv + (int64_t)(TR * rg + i) * NB + kTl * cg;
-#pragma unroll
-      for (int j = 0; j < kTl; ++j) tdst[j] = (T)a[i][j];
-    }
-  }
-  if (!fin) atomicMin(info, k0 + 1);
 }
 
 // ---- two Gauss-Jordan steps per barrier ----------------------------------------
@@ -314,7 +181,8 @@ __global__ __launch_bounds__(16 * NB / TR) void diag_inv_kernel(const T* __restr
 // u_k+1, r1_j = a_k+1,j - g_k+1 u_j, pivot a_k+1,k+1 - g_k+1 u_k+1), exactly
 // the FMAs their owners perform in the one-step form -- then applies
 // a -= g u^T + g' u'^T.  Every element sees the same operation sequence as
-// in diag_inv_kernel (bit-identical results) with half the barriers.
+// one Gauss-Jordan step per barrier would give it (bit-identical results),
+// with half the barriers.
 template <typename TI>
 struct alignas(16) GjPairLds {
   TI row[2][2][NB / kTl * kGjStride];  // [parity][row k / k+1]
@@ -459,236 +327,14 @@ __global__ __launch_bounds__(16 * NB / TR) void diag_inv_pair_kernel(const doubl
   if (!fin) atomicMin(info, k0 + 1);
 }
 
-// ---- blocked Gauss-Jordan inverse on the matrix cores ------------------------
-// The same inverse, blocked: block steps of KB = 32 (or 16) pivots.  The 128 x 128
-// block lives in LDS (133 KB of the CU's 160 KB); per block step b (rows /
-// columns kb = 32 b ..):
-//  1. wave 0 inverts the 32 x 32 pivot block in place by the unblocked
-//     Gauss-Jordan step above (the uniform rank-1 form; lane l holds row
-//     l / 2, half l % 2 of the columns; the pivot row goes through a
-//     wave-private LDS line, the pivot column through one DPP lane swap);
-//  2. the pivot rows: A[kb, j] = P^-1 A[kb, j] for j outside kb;
-//  3. every other row: A[i, j] -= A[i, kb] A[kb, j] (j outside kb) and
-//     A[i, kb] = -A[i, kb] P^-1 -- one GEMM with the pivot block columns of
-//     the right operand = P^-1 and of the start value = 0.
-// Steps 2 and 3 run on v_mfma_f64_16x16x4f64 (16 x 16 tiles, K = 32, every
-// wave one column tile of 6 row tiles in step 3), results held in registers
-// across a barrier, then stored (the GEMMs read what they overwrite).  The
-// 2.1 M FMAs of the inverse move from 128 barrier-separated VALU rank-1
-// steps to 8 MFMA phases + 128 single-wave steps on 32 x 32.
-constexpr int kBjLd = NB + 2;  // LDS row stride (doubles): 16 rows of an operand load hit distinct banks
-constexpr int kBjThreads = 512;
-
-struct BjLds {
-  double a[NB * kBjLd];
-  double rowb[2][32];
-};
-
-template <int CTRL>
-__device__ __forceinline__ double mov_dpp_f64(double x) {
-  const unsigned lo = (unsigned)__builtin_amdgcn_mov_dpp((int)(unsigned)__double_as_longlong(x), CTRL, 0xf, 0xf,
-                                                         false);
-  const unsigned hi = (unsigned)__builtin_amdgcn_mov_dpp(
-      (int)(unsigned)((uint64_t)__double_as_longlong(x) >> 32), CTRL, 0xf, 0xf, false);
-  return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
-}
-
-// step 1: wave 0 inverts the KB x KB pivot block at (kb, kb) in place.  Lane
-// l holds row l / LPR, columns VPL (l % LPR) .. of it (LPR = 64 / KB lanes per
-// row, VPL = KB / LPR values each): the pivot row goes through a
-// wave-private LDS line, the pivot column's entry of a row through one DPP
-// move inside the row's lane group.  Step K (compile time) of it:
-template <int KB, int K>
-__device__ __forceinline__ void bj_leaf_step(BjLds& sh, double (&p)[KB * KB / 64], int r, int cg) {
-  constexpr int LPR = 64 / KB, VPL = KB / LPR;
-  double* rb = sh.rowb[K & 1];
-  if (r == K) {
-#pragma unroll
-    for (int j = 0; j < VPL; j += 2) *reinterpret_cast<double2*>(rb + VPL * cg + j) = make_double2(p[j], p[j + 1]);
-  }
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // wave-private line: in-order LDS
-  double v[VPL];
-#pragma unroll
-  for (int j = 0; j < VPL; j += 2) {
-    const double2 w = *reinterpret_cast<const double2*>(rb + VPL * cg + j);
-    v[j] = w.x;
-    v[j + 1] = w.y;
-  }
-  const double akk = rb[K];
-  // my row's entry in column K: lane-group member K / VPL, register K % VPL
-  double gk;
-  if constexpr (LPR == 2) {
-    const double own = p[K % VPL];
-    const double oth = mov_dpp_f64<0xB1>(own);  // quad_perm [1,0,3,2]: the other lane of the pair
-    gk = (cg == K / VPL) ? own : oth;
-  } else {  // LPR == 4: the quad is the row's lane group
-    constexpr int src = K / VPL;
-    gk = mov_dpp_f64<src | (src << 2) | (src << 4) | (src << 6)>(p[K % VPL]);
-  }
-  const double g = gk - (r == K ? 1.0 : 0.0);
-  const double pk = gj_recip(akk);
-#pragma unroll
-  for (int j = 0; j < VPL; ++j) {
-    const double u = (VPL * cg + j == K) ? 1.0 + pk : v[j] * pk;
-    p[j] = fma(-g, u, p[j]);
-  }
-}
-
-template <int KB, int... K>
-__device__ __forceinline__ void bj_leaf_steps(BjLds& sh, double (&p)[KB * KB / 64], int r, int cg,
-                                              std::integer_sequence<int, K...>) {
-  (bj_leaf_step<KB, K>(sh, p, r, cg), ...);
-}
-
-template <int KB>
-__device__ __forceinline__ void bj_leaf(BjLds& sh, int kb, int lane) {
-  constexpr int LPR = 64 / KB, VPL = KB / LPR;
-  const int r = lane / LPR, cg = lane % LPR;
-  double* prow = &sh.a[(kb + r) * kBjLd + kb + VPL * cg];
-  double p[VPL];
-#pragma unroll
-  for (int j = 0; j < VPL; j += 2) {
-    const double2 v = *reinterpret_cast<const double2*>(prow + j);
-    p[j] = v.x;
-    p[j + 1] = v.y;
-  }
-  bj_leaf_steps<KB>(sh, p, r, cg, std::make_integer_sequence<int, KB>{});
-#pragma unroll
-  for (int j = 0; j < VPL; j += 2) *reinterpret_cast<double2*>(prow + j) = make_double2(p[j], p[j + 1]);
-}
-
-// the c-th 16-row / column tile outside the pivot block [kb, kb + KB)
-template <int KB>
-__device__ __forceinline__ int bj_outside(int c, int kb) { return 16 * c < kb ? 16 * c : 16 * c + KB; }
-
-template <int KB>
-__global__ __launch_bounds__(kBjThreads) void bj_inv_kernel(const double* __restrict__ Ablk, int64_t lda, int k0,
-                                                            double* __restrict__ Dinv, int* __restrict__ info) {
-  constexpr int RT = KB / 16;          // row tiles of the pivot rows
-  constexpr int OT = (NB - KB) / 16;   // tiles outside the pivot block
-  __shared__ BjLds sh;
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  const int m = lane & 15, q = lane >> 4;
-  {  // lanes along a row: coalesced
-    const int c = t & (NB - 1);
-#pragma unroll 8
-    for (int r = t >> 7; r < NB; r += kBjThreads / NB) sh.a[r * kBjLd + c] = Ablk[(int64_t)r * lda + c];
-  }
-  __syncthreads();
-  for (int kb = 0; kb < NB; kb += KB) {
-    if (wave == 0) bj_leaf<KB>(sh, kb, lane);
-    __syncthreads();
-    // step 2: RT x OT tiles of the pivot rows, dealt to the waves
-    constexpr int N2 = (RT * OT + 7) / 8;
-    dev::d4 acc2[N2];
-#pragma unroll
-    for (int u = 0; u < N2; ++u) {
-      const int ti = wave + 8 * u;
-      if (ti < RT * OT) {
-        const int r0 = kb + 16 * (ti / OT), c0 = bj_outside<KB>(ti % OT, kb);
-        dev::d4 acc = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-        for (int kk = 0; kk < KB; kk += 4) {
-          const double av = sh.a[(r0 + m) * kBjLd + kb + kk + q];   // P^-1 (row r0 + m, col kb + k)
-          const double bv = sh.a[(kb + kk + q) * kBjLd + c0 + m];   // A[kb + k, c0 + n]
-          acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
-        }
-        acc2[u] = acc;
-      }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int u = 0; u < N2; ++u) {
-      const int ti = wave + 8 * u;
-      if (ti < RT * OT) {
-        const int r0 = kb + 16 * (ti / OT), c0 = bj_outside<KB>(ti % OT, kb);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) sh.a[(r0 + q + 4 * i) * kBjLd + c0 + m] = acc2[u][i];
-      }
-    }
-    __syncthreads();
-    // step 3: column tile `wave` of the OT row tiles outside the pivot block
-    const int c0 = 16 * wave;
-    const bool pcol = c0 >= kb && c0 < kb + KB;
-    dev::d4 acc3[OT];
-#pragma unroll
-    for (int s = 0; s < OT; ++s) {
-      const int r0 = bj_outside<KB>(s, kb);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) acc3[s][i] = pcol ? 0.0 : sh.a[(r0 + q + 4 * i) * kBjLd + c0 + m];
-    }
-#pragma unroll
-    for (int kk = 0; kk < KB; kk += 4) {
-      const double bv = sh.a[(kb + kk + q) * kBjLd + c0 + m];
-#pragma unroll
-      for (int s = 0; s < OT; ++s) {
-        const double av = sh.a[(bj_outside<KB>(s, kb) + m) * kBjLd + kb + kk + q];
-        acc3[s] = __builtin_amdgcn_mfma_f64_16x16x4f64(-av, bv, acc3[s], 0, 0, 0);
-      }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int s = 0; s < OT; ++s) {
-      const int r0 = bj_outside<KB>(s, kb);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) sh.a[(r0 + q + 4 * i) * kBjLd + c0 + m] = acc3[s][i];
-    }
-    __syncthreads();
-  }
-  bool fin = true;
-  {
-    const int c = t & (NB - 1);
-#pragma unroll 8
-    for (int r = t >> 7; r < NB; r += kBjThreads / NB) {
-      const double v = sh.a[r * kBjLd + c];
-      fin = fin && isfinite(v);
-      Dinv[r * NB + c] = v;
-    }
-  }
-  if (!fin) atomicMin(info, k0 + 1);
-}
-
-// Launch of the diagonal inverse: GELIM_GJ_TR = 4 (default: 512 threads, two
-// waves per SIMD), 8 (256 threads) or 2 (1024 threads: 2048 1.52 ms, slower).  With the padded LDS chunks 4 x 8 tiles
-// are the faster shape (hip-rbt factor 2048 1.43 vs 1.52 ms, 4096 3.85 vs
-// 4.00, 8192 12.94 vs 13.07; before the padding 8 x 8 was, 1.64 vs 1.73).
-// Reserving the inverse's CU (LDS-exclusive launch, no GEMM workgroup beside
-// it) changed nothing measurable (profiles/rbt_engine_round3.txt).
-// The inverse of the NB x NB block at Ablk; `col` (its first global column)
-// only labels a non-finite result in info.
+// The inverse of the NB x NB block at Ablk (two Gauss-Jordan steps per
+// barrier, 4 x 8 tiles on 512 threads: 57.0 us alone, profiles/gj_pair_r4.txt;
+// the round-4 alternatives -- one step per barrier, 8 x 8 / 2 x 8 tiles, the
+// blocked MFMA form with 16- or 32-pivot blocks -- were slower or, blocked,
+// cost the refinement extra corrections, profiles/gj_blocked_r4.txt).  `col`
+// (its first global column) only labels a non-finite result in info.
 int block_inv(const double* Ablk, int64_t lda, int64_t col, double* Di, int* info, hipStream_t s) {
-  // GELIM_GJ_BLOCKED: 1 = the blocked MFMA form with 32-pivot blocks, 2 = with
-  // 16-pivot blocks (read per launch)
-  const char* eb = std::getenv("GELIM_GJ_BLOCKED");
-  const int bj = eb ? std::atoi(eb) : 0;
-  if (bj == 1 || bj == 2) {
-    if (bj == 1) hipLaunchKernelGGL(bj_inv_kernel<32>, dim3(1), dim3(kBjThreads), 0, s, Ablk, lda, (int)col, Di, info);
-    else hipLaunchKernelGGL(bj_inv_kernel<16>, dim3(1), dim3(kBjThreads), 0, s, Ablk, lda, (int)col, Di, info);
-    HIP_TRY(hipGetLastError());
-    return GELIM_OK;
-  }
-  const char* e = std::getenv("GELIM_GJ_TR");  // read per launch (tests switch it)
-  const int tr = e && (std::atoi(e) == 8 || std::atoi(e) == 2) ? std::atoi(e) : 4;
-  // two Gauss-Jordan steps per barrier (bit-identical): 57.0 vs 58.6 us per
-  // block alone (profiles/gj_pair_r4.txt); GELIM_GJ_PAIR=0 for one per barrier
-  const char* ep = std::getenv("GELIM_GJ_PAIR");
-  if ((tr == 4 || tr == 2) && !(ep && std::atoi(ep) == 0)) {
-    if (tr == 4)
-      hipLaunchKernelGGL((diag_inv_pair_kernel<4>), dim3(1), dim3(16 * NB / 4), 0, s, Ablk, lda, (int)col, Di, info);
-    else
-      hipLaunchKernelGGL((diag_inv_pair_kernel<2>), dim3(1), dim3(16 * NB / 2), 0, s, Ablk, lda, (int)col, Di, info);
-    HIP_TRY(hipGetLastError());
-    return GELIM_OK;
-  }
-  if (tr == 2)
-    hipLaunchKernelGGL((diag_inv_kernel<double, 2>), dim3(1), dim3(16 * NB / 2), 0, s, Ablk, lda, (int)col, Di,
-                       (double*)nullptr, info);
-  else if (tr == 4)
-    hipLaunchKernelGGL((diag_inv_kernel<double, 4>), dim3(1), dim3(16 * NB / 4), 0, s, Ablk, lda, (int)col, Di,
-                       (double*)nullptr, info);
-  else
-    hipLaunchKernelGGL((diag_inv_kernel<double, 8>), dim3(1), dim3(16 * NB / 8), 0, s, Ablk, lda, (int)col, Di,
-                       (double*)nullptr, info);
+  hipLaunchKernelGGL((diag_inv_pair_kernel<4>), dim3(1), dim3(16 * NB / 4), 0, s, Ablk, lda, (int)col, Di, info);
   HIP_TRY(hipGetLastError());
   return GELIM_OK;
 }
@@ -901,6 +547,192 @@ __global__ __launch_bounds__(256) void prep_solves_kernel(unsigned long long* __
   }
 }
 
+// ---- split block triangular solve: the chain does only the last blocks ----------
+//
+// The same solve as blk_trsv_kernel, with the off-diagonal work spread over
+// the chip.  In blk_trsv_kernel workgroup w reads ALL w blocks of its block row
+// through one CU (8 MB for the last row at 8192): the chain step is bound by
+// one CU's share of HBM bandwidth, 332 us per 8192 triangle against a ~55 us
+// bandwidth floor (profiles/rbt_trace_8192_r4.txt).  Here every block row b
+// has K helper workgroups: helper h accumulates F_bi x_i for the blocks i < w
+// - kChainOwn with i = h (mod K), as soon as each x_i is published, and
+// publishes its 128 partial sums through a sentinel-filled buffer; the chain
+// workgroup applies only the last kChainOwn blocks (the ones that arrive
+// last), adds the K partials in a fixed order (deterministic), multiplies by
+// the stored inverse and publishes x_b.  The chain step is then a hand-off, a
+// 128 x 128 mat-vec out of registers and the finish, while the F stream runs
+// on up to K + 1 CUs per block row.
+constexpr int kChainOwn = 2;  // blocks the chain workgroup applies itself
+constexpr int kMaxHelpers = 4;
+
+// Lanes poll their OWN published value p[lane] until it is not the
+// sentinel (bounded like settle_x); false when the spin ran out or another
+// workgroup reported an error.
+__device__ __forceinline__ bool settle_own(const double* __restrict__ p, int* err, double& out) {
+  const unsigned long long* pp = reinterpret_cast<const unsigned long long*>(p);
+  unsigned long long v = __hip_atomic_load(pp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  bool ok = true;
+  if (__ballot(v == kSentinel) != 0) {
+    const unsigned long long t0 = rtc();
+    while (__ballot(v == kSentinel) != 0) {
+      __builtin_amdgcn_s_sleep(1);
+      if (v == kSentinel) v = __hip_atomic_load(pp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (rtc() - t0 > kSpinTicks || __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) {
+        if (__lane_id() == 0) __hip_atomic_store(err, 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ok = false;
+        break;
+      }
+    }
+  }
+  out = __builtin_bit_cast(double, v);
+  return ok;
+}
+
+// grid = nblk * (K + 1): ids [0, nblk) are the chain (position w = id), ids
+// nblk + K w + h the helpers of position w.  hpart: nblk * K * 128 doubles,
+// sentinel-filled.  Requires the whole grid co-resident (checked by the host).
+template <typename T, bool UPPER>
+__global__ __launch_bounds__(kDT) void blk_trsv_split_kernel(const T* __restrict__ F, int64_t ldf,
+                                                            const double* __restrict__ Dinv,
+                                                            const double* __restrict__ c, double* __restrict__ x,
+                                                            double* __restrict__ ysave, double* __restrict__ hpart,
+                                                            int nblk, int K, int* __restrict__ err) {
+  __shared__ double part[4][NB];
+  __shared__ double rb[NB];
+  __shared__ int bad;
+  const int t = threadIdx.x, r = t & (NB - 1), lane = t & 63;
+  const int q = __builtin_amdgcn_readfirstlane(t >> 7);
+  const int id = blockIdx.x;
+  const bool chain = id < nblk;
+  const int w = chain ? id : (id - nblk) / K;
+  const int h = chain ? 0 : (id - nblk) % K;
+  if (w >= nblk) return;
+  const int b = UPPER ? nblk - 1 - w : w;
+  const int row = NB * b + r;
+  if (t == 0) bad = 0;
+  const int own0 = w > kChainOwn ? w - kChainOwn : 0;  // the chain applies blocks own0 .. w-1
+  const T* frow = F + (int64_t)row * ldf + kQW * q;
+  auto blk = [&](int i) { return frow + (int64_t)NB * (UPPER ? nblk - 1 - i : i); };
+  auto xidx = [&](int i) { return NB * (UPPER ? nblk - 1 - i : i) + kQW * q; };
+  double acc = 0.0;
+  bool ok = true;
+  T ua[kQW], ub[kQW];
+  auto step = [&](const T(&u)[kQW], unsigned long long v, int i, bool nap) -> bool {
+    double xl;
+    if (!settle_x(x, xidx(i), v, err, xl, nap)) return false;
+#pragma unroll
+    for (int j = 0; j < kQW; ++j) acc = fma(-(double)u[j], bcast_lane(xl, j), acc);
+    return true;
+  };
+
+  if (!chain) {
+    // helper h of position w: blocks i = h, h + K, ... < own0, next block's
+    // factor loads in flight under the current one's wait
+    int i = h;
+    if (i < own0) load_blk(ua, blk(i));
+    for (; i + K < own0; i += 2 * K) {
+      unsigned long long v = issue_x(x, xidx(i));
+      load_blk(ub, blk(i + K));
+      if (!step(ua, v, i, true)) { ok = false; break; }
+      v = issue_x(x, xidx(i + K));
+      if (i + 2 * K < own0) load_blk(ua, blk(i + 2 * K));
+      if (!step(ub, v, i + K, true)) { ok = false; break; }
+    }
+    if (ok && i < own0) ok = step(ua, issue_x(x, xidx(i)), i, true);
+    part[q][r] = acc;
+    if (!ok && lane == 0) bad = 1;
+    __syncthreads();
+    if (bad) return;
+    if (q == 0) {
+      double s = part[0][r] + part[1][r] + part[2][r] + part[3][r];
+      if (__builtin_bit_cast(unsigned long long, s) == kSentinel) s = __builtin_nan("");
+      __hip_atomic_store(reinterpret_cast<unsigned long long*>(hpart + ((int64_t)w * K + h) * NB + r),
+                         __builtin_bit_cast(unsigned long long, s), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    return;
+  }
+
+  // chain: this block's inverse rows and right-hand side first, pinned
+  double dv[kQW];
+  {
+    const double* d = Dinv + ((int64_t)b * NB + r) * NB + kQW * q;
+#pragma unroll
+    for (int j = 0; j < kQW; ++j) dv[j] = d[j];
+  }
+  double cv = c[row];
+#pragma unroll
+  for (int j = 0; j < kQW; ++j) asm volatile("" : "+v"(dv[j]));
+  asm volatile("" : "+v"(cv));
+  // the helpers' partials are read early -- after block w-2, while x_{w-1} is
+  // still on its way -- so a ready partial costs no load on the chain
+  unsigned long long hb[kMaxHelpers];
+  auto prefetch_h = [&]() {
+    if (q == 0) {
+#pragma unroll
+      for (int hh = 0; hh < kMaxHelpers; ++hh)
+        hb[hh] = hh < K ? __hip_atomic_load(reinterpret_cast<const unsigned long long*>(
+                                                hpart + ((int64_t)w * K + hh) * NB + r),
+                                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                        : 0ull;
+    }
+  };
+  // the last kChainOwn (= 2) blocks, in chain order
+  if (own0 + 1 < w) {
+    load_blk(ua, blk(own0));
+    unsigned long long v = issue_x(x, xidx(own0));
+    load_blk(ub, blk(own0 + 1));
+    ok = step(ua, v, own0, true);
+    prefetch_h();
+    if (ok) ok = step(ub, issue_x(x, xidx(own0 + 1)), own0 + 1, false);
+  } else {
+    prefetch_h();
+    if (own0 < w) {
+      load_blk(ua, blk(own0));
+      ok = step(ua, issue_x(x, xidx(own0)), own0, false);
+    }
+  }
+  part[q][r] = acc;
+  if (!ok && lane == 0) bad = 1;
+  __syncthreads();
+  if (bad) return;
+  if (q == 0) {
+    // the helpers' partials, added in helper order after the chain's own
+    // blocks: the same sum in every run
+    double y = cv + part[0][r] + part[1][r] + part[2][r] + part[3][r];
+#pragma unroll
+    for (int hh = 0; hh < kMaxHelpers; ++hh) {
+      if (hh >= K || !ok) break;
+      double hp = __builtin_bit_cast(double, hb[hh]);
+      if (__ballot(hb[hh] == kSentinel) != 0) ok = settle_own(hpart + ((int64_t)w * K + hh) * NB + r, err, hp);
+      y += hp;
+    }
+    if (!ok && lane == 0) bad = 1;
+    rb[r] = y;
+    if (ysave) ysave[row] = y;
+  }
+  __syncthreads();
+  if (bad) return;
+  double xs = 0.0;
+#pragma unroll
+  for (int j = 0; j < kQW; ++j) xs = fma(dv[j], rb[kQW * q + j], xs);
+  __syncthreads();
+  part[q][r] = xs;
+  __syncthreads();
+  if (q == 0) {
+    double xv = part[0][r] + part[1][r] + part[2][r] + part[3][r];
+    if (__builtin_bit_cast(unsigned long long, xv) == kSentinel) xv = __builtin_nan("");
+    __hip_atomic_store(reinterpret_cast<unsigned long long*>(x + row), __builtin_bit_cast(unsigned long long, xv),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+__global__ __launch_bounds__(256) void fill_sentinel2_kernel(unsigned long long* __restrict__ a, int na,
+                                                             unsigned long long* __restrict__ b, int nb) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i < na) a[i] = kSentinel;
+  if (i < nb) b[i] = kSentinel;
+}
+
 // omega = max_i |r_i| / w_i (componentwise backward error; w_i = 0 counts as
 // 0), one workgroup, written to *out.
 __global__ __launch_bounds__(1024) void berr_kernel(const double* __restrict__ r, const double* __restrict__ w, int n,
@@ -927,30 +759,11 @@ __global__ __launch_bounds__(256) void axpy_kernel(double* __restrict__ x, const
   if (i < n) x[i] += d[i];
 }
 
-// Rounded fp32 copy of a rows x cols fp64 block (the fp32 engine's GEMM operands).
-__global__ __launch_bounds__(256) void to_f32_kernel(const double* __restrict__ src, int64_t sld,
-                                                    float* __restrict__ dst, int64_t dld, int cols) {
-  const int64_t r = blockIdx.y;
-  for (int c = blockIdx.x * 256 + threadIdx.x; c < cols; c += gridDim.x * 256)
-    dst[r * dld + c] = (float)src[r * sld + c];
-}
-
-int to_f32(const double* src, int64_t sld, float* dst, int64_t dld, int64_t rows, int64_t cols, hipStream_t s) {
-  const unsigned gx = (unsigned)std::min<int64_t>((cols + 255) / 256, 64);
-  hipLaunchKernelGGL(to_f32_kernel, dim3(gx, (unsigned)rows), dim3(256), 0, s, src, sld, dst, dld, (int)cols);
-  HIP_TRY(hipGetLastError());
-  return GELIM_OK;
-}
-
-// Block LDU factorisation of the transformed (fp64) matrix in place: per
-// block k, Dinv_k = A_kk^-1 (fp64 Gauss-Jordan), W = A_kk^-1 A_k,rest (fp64
-// MFMA), A_rest,rest -= A_rest,k W -- on the fp64 matrix cores, or (A21f /
-// Wf given: the fp32 engine) as an fp32 MFMA product of rounded copies
-// accumulated into the fp64 matrix.  Only that O(n^3) product is fp32: the
-// inverses and W stay fp64, so a badly conditioned diagonal block costs
-// cond * eps64, not cond * eps32.
-int factor_impl(double* M, int64_t ldm, int64_t np, double* Dinv, double* W, float* A21f, float* Wf, int* info,
-                hipStream_t s) {
+// Block LDU factorisation of the transformed (fp64) matrix in place, no
+// lookahead (below 32 blocks): per block k, Dinv_k = A_kk^-1 (Gauss-Jordan),
+// W = A_kk^-1 A_k,rest and A_rest,rest -= A_rest,k W on the fp64 matrix cores
+// (dgemm.hip v_mfma_f64_16x16x4f64).
+int factor_impl(double* M, int64_t ldm, int64_t np, double* Dinv, double* W, int* info, hipStream_t s) {
   for (int64_t k0 = 0; k0 < np; k0 += NB) {
     double* Di = Dinv + (k0 / NB) * NB * NB;
     GELIM_TRY(diag_inv(M, ldm, k0, Di, info, s));
@@ -959,51 +772,9 @@ int factor_impl(double* M, int64_t ldm, int64_t np, double* Dinv, double* W, flo
     double* A12 = M + k0 * ldm + k0 + NB;
     double* A21 = M + (k0 + NB) * ldm + k0;
     double* A22 = M + (k0 + NB) * ldm + k0 + NB;
-    GELIM_TRY(dgemm_ex(W, rest, Di, NB, A12, ldm, NB, rest, NB, 1.0, 0, s));  // W = A11^-1 A12
-    if (!A21f) {
-      GELIM_TRY(dgemm_ex(A22, ldm, A21, ldm, W, rest, rest, rest, NB, -1.0, 1, s));  // A22 -= A21 W
-    } else {
-      GELIM_TRY(to_f32(A21, ldm, A21f, NB, rest, NB, s));
-      GELIM_TRY(to_f32(W, rest, Wf, rest, NB, rest, s));
-      GELIM_TRY(matmul_f32(A21f, NB, Wf, rest, nullptr, ldm, rest, rest, NB, 1, GELIM_MM_MFMA, s, -1.0f, A22));
-    }
+    GELIM_TRY(dgemm_ex(W, rest, Di, NB, A12, ldm, NB, rest, NB, 1.0, 0, s));        // W = A11^-1 A12
+    GELIM_TRY(dgemm_ex(A22, ldm, A21, ldm, W, rest, rest, rest, NB, -1.0, 1, s));  // A22 -= A21 W
   }
-  return GELIM_OK;
-}
-
-// The same factorisation with a one-block lookahead on two streams (fp64):
-// after W_k, the main stream updates only block column k+1 and block row k+1
-// (two thin GEMMs) and inverts the next diagonal block at once, while the
-// side stream runs the big trailing update of step k (rows / columns >= k+2)
-// (optionally on a grid capped below the CU count, GELIM_RBT_RESERVE).  Main waits for side step k-1 before touching block row / column
-// k+1 (the side's step k-1 region); W is double-buffered (side step k reads
-// W_k while main computes W_{k+1}).
-int factor_la(double* M, int64_t ldm, int64_t np, double* Dinv, double* W2, int* info, hipStream_t s,
-              hipStream_t side, hipEvent_t e0, hipEvent_t e1, int cap) {
-  const int64_t nblk = np / NB;
-  GELIM_TRY(diag_inv(M, ldm, 0, Dinv, info, s));
-  bool side_used = false;
-  for (int64_t k = 0; k + 1 < nblk; ++k) {
-    const int64_t k0 = k * NB, rest = np - k0 - NB, rest2 = rest - NB;
-    double* Di = Dinv + k * NB * NB;
-    double* Wk = W2 + (k & 1) * NB * np;
-    double* A21 = M + (k0 + NB) * ldm + k0;
-    GELIM_TRY(dgemm_ex(Wk, rest, Di, NB, M + k0 * ldm + k0 + NB, ldm, NB, rest, NB, 1.0, 0, s));  // W_k
-    if (side_used) HIP_TRY(hipStreamWaitEvent(s, e1, 0));  // side step k-1 done
-    // block column k+1 (all rows below k), then block row k+1 (columns past k+1)
-    GELIM_TRY(dgemm_ex(M + (k0 + NB) * ldm + k0 + NB, ldm, A21, ldm, Wk, rest, rest, NB, NB, -1.0, 1, s));
-    if (rest2 > 0) {
-      GELIM_TRY(dgemm_ex(M + (k0 + NB) * ldm + k0 + 2 * NB, ldm, A21, ldm, Wk + NB, rest, NB, rest2, NB, -1.0, 1, s));
-      HIP_TRY(hipEventRecord(e0, s));
-      HIP_TRY(hipStreamWaitEvent(side, e0, 0));
-      GELIM_TRY(dgemm_capped(M + (k0 + 2 * NB) * ldm + k0 + 2 * NB, ldm, M + (k0 + 2 * NB) * ldm + k0, ldm, Wk + NB,
-                             rest, rest2, rest2, NB, -1.0, cap, side, 1));
-      HIP_TRY(hipEventRecord(e1, side));
-      side_used = true;
-    }
-    GELIM_TRY(diag_inv(M, ldm, k0 + NB, Dinv + (k + 1) * NB * NB, info, s));
-  }
-  if (side_used) HIP_TRY(hipStreamWaitEvent(s, e1, 0));
   return GELIM_OK;
 }
 
@@ -1022,7 +793,7 @@ int factor_la(double* M, int64_t ldm, int64_t np, double* Dinv, double* W2, int*
 //   A[k+4:, k+4:] -= A[k+4:, k:k+2] [W1; W2][:, k+4:]  (K = 256).
 // The pair's W is double-buffered (side reads pair p while main builds p+1).
 int factor_la2(double* M, int64_t ldm, int64_t np, double* Dinv, double* W4, int* info, hipStream_t s,
-               hipStream_t side, hipEvent_t e0, hipEvent_t e1, int cap) {
+               hipStream_t side, hipEvent_t e0, hipEvent_t e1) {
   const int64_t nblk = np / NB;
   GELIM_TRY(diag_inv(M, ldm, 0, Dinv, info, s));
   bool side_used = false;
@@ -1052,98 +823,13 @@ int factor_la2(double* M, int64_t ldm, int64_t np, double* Dinv, double* W4, int
                          -1.0, 1, s));
       HIP_TRY(hipEventRecord(e0, s));
       HIP_TRY(hipStreamWaitEvent(side, e0, 0));
-      GELIM_TRY(dgemm_capped(M + (k0 + 2 * NB + pw) * ldm + k0 + 2 * NB + pw, ldm, M + (k0 + 2 * NB + pw) * ldm + k0,
-                             ldm, Wp + NB + pw, r1, r4, r4, 2 * NB, -1.0, cap, side, 1));
+      GELIM_TRY(dgemm_ex(M + (k0 + 2 * NB + pw) * ldm + k0 + 2 * NB + pw, ldm, M + (k0 + 2 * NB + pw) * ldm + k0, ldm,
+                         Wp + NB + pw, r1, r4, r4, 2 * NB, -1.0, 1, side));
       HIP_TRY(hipEventRecord(e1, side));
       side_used = true;
     }
     GELIM_TRY(diag_inv(M, ldm, k0 + 2 * NB, Dinv + (k + 2) * NB * NB, info, s));
   }
-  if (side_used) HIP_TRY(hipStreamWaitEvent(s, e1, 0));
-  return GELIM_OK;
-}
-
-// factor_la2 with a third stream (aux) that takes every update the next
-// diagonal inverse does not read, so it runs UNDER that inverse (a one-
-// workgroup kernel) instead of before it.  Per pair (k, k+1):
-//   main: W1 = D_k A[k, k+1:];  A[k+1, k+1] -= A[k+1, k] W1[:, :128]   (diagonal block only)
-//   aux:  A[k+2:, k+1] -= A[k+2:, k] W1[:, :128];  A[k+1, k+2:] -= A[k+1, k] W1[:, 128:]
-//   main: D_{k+1}; [join aux]; W2 = D_{k+1} A[k+1, k+2:]; [wait side p-1; side p may start]
-//   main: panel rows k+2 only: A[k+2, panel] -= A[k+2, k:k+2] [W1; W2][:, panel]
-//   aux:  panel rows k+3..:   A[k+3:, panel] -= ...;  panel's block rows right of it (K = 256)
-//   main: D_{k+2}; [join aux before the next pair]
-// Measured slower than factor_la2 (4096: 4.10 vs 3.96 ms, 8192: 13.64 vs
-// 13.07 ms; forced at 2048: 1.73 vs 1.51 ms without lookahead): the inverse
-// does not speed up by having the GEMMs beside it, and each pair adds four
-// cross-stream event waits.  Off by default (GELIM_RBT_AUX=1).
-// Regions: aux writes column k+1 below block k+1, row k+1 right of it, the
-// panel below its first block row and the panel's block rows right of the
-// panel; the side (after the wait on pair p-1) writes rows and columns past
-// the panel; main writes only what the next inverse reads.  Every region a
-// stream reads was written before the event it waited on.
-int factor_la3(double* M, int64_t ldm, int64_t np, double* Dinv, double* W4, int* info, hipStream_t s,
-               hipStream_t side, hipStream_t aux, hipEvent_t e0, hipEvent_t e1, hipEvent_t ea, hipEvent_t eb,
-               int cap) {
-  const int64_t nblk = np / NB;
-  GELIM_TRY(diag_inv(M, ldm, 0, Dinv, info, s));
-  bool side_used = false, aux_used = false;
-  auto fork = [&]() -> int {  // aux continues after everything main issued so far
-    HIP_TRY(hipEventRecord(ea, s));
-    HIP_TRY(hipStreamWaitEvent(aux, ea, 0));
-    return GELIM_OK;
-  };
-  auto join = [&]() -> int {  // main continues after everything aux issued so far
-    if (!aux_used) return GELIM_OK;
-    HIP_TRY(hipEventRecord(eb, aux));
-    HIP_TRY(hipStreamWaitEvent(s, eb, 0));
-    aux_used = false;
-    return GELIM_OK;
-  };
-  for (int64_t k = 0, pair = 0; k + 1 < nblk; k += 2, ++pair) {
-    GELIM_TRY(join());  // the previous pair's panel below its first block row / block rows right of it
-    const int64_t k0 = k * NB, r1 = np - k0 - NB, r2 = r1 - NB;
-    double* Wp = W4 + (pair & 1) * 2 * NB * np;  // 2 NB rows, ld r1
-    double* Ak = M + (k0 + NB) * ldm + k0;       // A[k+1:, k]
-    GELIM_TRY(dgemm_ex(Wp, r1, Dinv + k * NB * NB, NB, M + k0 * ldm + k0 + NB, ldm, NB, r1, NB, 1.0, 0, s));
-    GELIM_TRY(dgemm_ex(M + (k0 + NB) * ldm + k0 + NB, ldm, Ak, ldm, Wp, r1, NB, NB, NB, -1.0, 1, s));
-    if (r2 > 0) {
-      GELIM_TRY(fork());
-      GELIM_TRY(dgemm_ex(M + (k0 + 2 * NB) * ldm + k0 + NB, ldm, Ak + NB * ldm, ldm, Wp, r1, r2, NB, NB, -1.0, 1, aux));
-      GELIM_TRY(dgemm_ex(M + (k0 + NB) * ldm + k0 + 2 * NB, ldm, Ak, ldm, Wp + NB, r1, NB, r2, NB, -1.0, 1, aux));
-      aux_used = true;
-    }
-    GELIM_TRY(diag_inv(M, ldm, k0 + NB, Dinv + (k + 1) * NB * NB, info, s));
-    if (r2 <= 0) break;  // block k+1 was the last
-    GELIM_TRY(join());
-    GELIM_TRY(dgemm_ex(Wp + NB * r1 + NB, r1, Dinv + (k + 1) * NB * NB, NB, M + (k0 + NB) * ldm + k0 + 2 * NB, ldm,
-                       NB, r2, NB, 1.0, 0, s));
-    if (side_used) HIP_TRY(hipStreamWaitEvent(s, e1, 0));  // side's pair p-1 update (rows / columns >= k+2)
-    const int64_t pw = std::min<int64_t>(2 * NB, r2);  // panel width
-    const int64_t r4 = r2 - pw;                       // columns right of the panel
-    double* A2 = M + (k0 + 2 * NB) * ldm + k0;        // A[k+2:, k:k+2]
-    double* P = M + (k0 + 2 * NB) * ldm + k0 + 2 * NB;  // the panel's first element
-    if (r4 > 0) {
-      // the side's region (rows / columns past the panel) reads only the
-      // final L columns k, k+1 and this pair's W
-      HIP_TRY(hipEventRecord(e0, s));
-      HIP_TRY(hipStreamWaitEvent(side, e0, 0));
-      GELIM_TRY(dgemm_capped(M + (k0 + 2 * NB + pw) * ldm + k0 + 2 * NB + pw, ldm, M + (k0 + 2 * NB + pw) * ldm + k0,
-                             ldm, Wp + NB + pw, r1, r4, r4, 2 * NB, -1.0, cap, side, 1));
-      HIP_TRY(hipEventRecord(e1, side));
-      side_used = true;
-    }
-    GELIM_TRY(dgemm_ex(P, ldm, A2, ldm, Wp + NB, r1, NB, pw, 2 * NB, -1.0, 1, s));  // block row k+2 of the panel
-    if (r2 > NB || r4 > 0) {
-      GELIM_TRY(fork());
-      if (r2 > NB)
-        GELIM_TRY(dgemm_ex(P + NB * ldm, ldm, A2 + NB * ldm, ldm, Wp + NB, r1, r2 - NB, pw, 2 * NB, -1.0, 1, aux));
-      if (r4 > 0)
-        GELIM_TRY(dgemm_ex(P + pw, ldm, A2, ldm, Wp + NB + pw, r1, pw, r4, 2 * NB, -1.0, 1, aux));
-      aux_used = true;
-    }
-    GELIM_TRY(diag_inv(M, ldm, k0 + 2 * NB, Dinv + (k + 2) * NB * NB, info, s));
-  }
-  GELIM_TRY(join());
   if (side_used) HIP_TRY(hipStreamWaitEvent(s, e1, 0));
   return GELIM_OK;
 }
@@ -1163,24 +849,58 @@ constexpr int kNotResident = 1;
 
 template <typename T>
 int solve_impl(const T* M, int64_t ldm, int64_t np, const double* Dinv, const double* c, double* z, double* y,
-               double* x, unsigned* flags, hipStream_t s) {
+               double* x, unsigned* flags, hipStream_t s, double* hp = nullptr) {
   const int nblk = (int)(np / NB);
+  // the split form (blk_trsv_split_kernel) when its grid of nblk (K + 1)
+  // workgroups fits at once, with as many helpers per block row as fit
+  static const int split_per_cu = [] {
+    int a = 0, b = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&a, blk_trsv_split_kernel<T, false>, kDT, 0) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, blk_trsv_split_kernel<T, true>, kDT, 0) != hipSuccess)
+      return 0;
+    return std::min(a, b);
+  }();
+  int K = 0;
+  if (hp && split_per_cu > 0 && nblk <= kMaxBlocks)
+    for (int k = kMaxHelpers; k >= 1 && K == 0; --k)
+      if (coresident(split_per_cu, (int64_t)nblk * (k + 1))) K = k;
+  if (K > 0) {
+    int* err = reinterpret_cast<int*>(flags);
+    const int nh = nblk * K * NB;  // helper partials per direction
+    const bool alias = x == c;
+    const unsigned g = (unsigned)((std::max<int64_t>(np, 2 * (int64_t)nh) + 255) / 256);
+    hipLaunchKernelGGL(fill_sentinel2_kernel, dim3(g), dim3(256), 0, s, reinterpret_cast<unsigned long long*>(z),
+                       (int)np, reinterpret_cast<unsigned long long*>(hp), 2 * nh);
+    if (!alias)
+      hipLaunchKernelGGL(fill_sentinel_kernel, dim3((unsigned)((np + 255) / 256)), dim3(256), 0, s,
+                         reinterpret_cast<unsigned long long*>(x), (int)np);
+    HIP_TRY(hipGetLastError());
+    const unsigned grid = (unsigned)(nblk * (K + 1));
+    hipLaunchKernelGGL((blk_trsv_split_kernel<T, false>), dim3(grid), dim3(kDT), 0, s, M, ldm, Dinv, c, z, y, hp,
+                       nblk, K, err);
+    HIP_TRY(hipGetLastError());
+    if (alias) {
+      hipLaunchKernelGGL(fill_sentinel_kernel, dim3((unsigned)((np + 255) / 256)), dim3(256), 0, s,
+                         reinterpret_cast<unsigned long long*>(x), (int)np);
+      HIP_TRY(hipGetLastError());
+    }
+    hipLaunchKernelGGL((blk_trsv_split_kernel<T, true>), dim3(grid), dim3(kDT), 0, s, M, ldm, Dinv, y, x,
+                       (double*)nullptr, hp + nh, nblk, K, err);
+    HIP_TRY(hipGetLastError());
+    return GELIM_OK;
+  }
   static const bool fits = [] {
     int a = 0, b = 0;
     return hipOccupancyMaxActiveBlocksPerMultiprocessor(&a, blk_trsv_kernel<T, false>, kDT, 0) == hipSuccess &&
            hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, blk_trsv_kernel<T, true>, kDT, 0) == hipSuccess &&
            a >= 1 && b >= 1;
   }();
-  static const int pack_env = [] {
-    const char* e = std::getenv("GELIM_TRSV_PACK");
-    return e ? std::atoi(e) : 1;
-  }();
   // the XCD-packed chain maps positions across the whole 8 x 32 grid (position
   // 32 is workgroup 1, waiting on position 31 = workgroup 248), so it needs
   // every one of them resident; one workgroup per block row needs only nblk
   // (workgroups are dispatched in order, each waits on lower ids only)
   if (!fits || nblk > kMaxBlocks) return kNotResident;
-  const int pack = pack_env && coresident(1, 8 * kXcdSlots) ? 1 : 0;
+  const int pack = coresident(1, 8 * kXcdSlots) ? 1 : 0;
   if (!pack && !coresident(1, nblk)) return kNotResident;
   int* err = reinterpret_cast<int*>(flags);  // flags[0]: error word
   const unsigned g = (unsigned)((np + 255) / 256);
@@ -1213,15 +933,13 @@ int solve_impl(const T* M, int64_t ldm, int64_t np, const double* Dinv, const do
 
 struct gelim_mixed_plan {
   int64_t n = 0, np = 0, ldm = 0;
-  int fp64 = 0;             // factor precision: 0 fp32 ("hip-mixed"), 1 fp64 ("hip-rbt")
   double* M = nullptr;      // np x ldm: the transformed matrix, then its block-LDU factor
   double* Dinv = nullptr;   // nblk x NB x NB: inverse of every (Schur) diagonal block
   double* W = nullptr;      // 4 x NB x np: A_kk^-1 A_k,rest (pairs of blocks, double-buffered under lookahead)
-  float* A21f = nullptr;    // np x NB, NB x np: rounded GEMM operands (fp32 engine only)
-  float* Wf = nullptr;
   double* ud = nullptr;     // U's butterfly diagonals (8 x np/4)
   double* vd = nullptr;     // V's
   unsigned* flags = nullptr;  // [0]: the solves' error word
+  double* hp = nullptr;       // split solves' helper partials (2 x kMaxBlocks x kMaxHelpers x NB)
   double* c = nullptr;      // U^T r (np)
   double* y = nullptr;      // L^-1 c (np)
   double* z = nullptr;      // U^-1 y (np)
@@ -1233,35 +951,22 @@ struct gelim_mixed_plan {
   double* dv = nullptr;
   double* xb = nullptr;
   double* om = nullptr;     // device scalar: the backward error
-  int lookahead = 0;        // fp64 engine: lookahead on a side stream
-  int pairs = 1;            // lookahead over pairs of blocks (K = 256 trailing updates)
-  int cap = 0;              // side-stream GEMM grid cap (CUs)
+  int lookahead = 0;        // lookahead over pairs of blocks on a side stream (factor_la2)
   hipStream_t side = nullptr;
   hipEvent_t e0 = nullptr, e1 = nullptr;
-  int aux_on = 0;              // pairs: updates the next inverse does not read on a third stream (factor_la3)
-  hipStream_t aux = nullptr;
-  hipEvent_t ea = nullptr, eb = nullptr;
-  hipStream_t crit = nullptr;  // GELIM_CRIT_PRIO set: the factorisation's chain on a stream of that priority
-  hipEvent_t ef = nullptr, ej = nullptr;
 };
 
 extern "C" int64_t gelim_mixed_max_n(void) { return (int64_t)gelim::kMaxBlocks * gelim::NB; }
 
 extern "C" void gelim_mixed_plan_destroy(gelim_mixed_plan* p) {
   if (!p) return;
-  for (void* q : {(void*)p->M, (void*)p->Dinv, (void*)p->W, (void*)p->A21f, (void*)p->Wf, (void*)p->ud, (void*)p->vd,
+  for (void* q : {(void*)p->M, (void*)p->Dinv, (void*)p->W, (void*)p->ud, (void*)p->vd,
                   (void*)p->rv, (void*)p->wv, (void*)p->dv, (void*)p->xb, (void*)p->om, (void*)p->flags, (void*)p->c,
-                  (void*)p->y, (void*)p->z, (void*)p->xs, (void*)p->info})
+                  (void*)p->y, (void*)p->z, (void*)p->xs, (void*)p->info, (void*)p->hp})
     (void)hipFree(q);
-  if (p->ea) (void)hipEventDestroy(p->ea);
-  if (p->eb) (void)hipEventDestroy(p->eb);
-  if (p->aux) (void)hipStreamDestroy(p->aux);
   if (p->e0) (void)hipEventDestroy(p->e0);
   if (p->e1) (void)hipEventDestroy(p->e1);
   if (p->side) (void)hipStreamDestroy(p->side);
-  if (p->ef) (void)hipEventDestroy(p->ef);
-  if (p->ej) (void)hipEventDestroy(p->ej);
-  if (p->crit) (void)hipStreamDestroy(p->crit);
   delete p;
 }
 
@@ -1269,7 +974,7 @@ extern "C" void gelim_mixed_plan_destroy(gelim_mixed_plan* p) {
 // each (np = gelim_mixed_padded(n)), exp(r/10) with r uniform in [-1/2, 1/2].
 extern "C" int64_t gelim_mixed_padded(int64_t n) { return (n + gelim::kPadTo - 1) / gelim::kPadTo * gelim::kPadTo; }
 
-// fp64 = 0: fp32 factors (GMRES-IR in the caller), 1: fp64 factors.
+// fp64 must be 1 (fp64 factors; the fp32-factor engine was removed).
 extern "C" gelim_mixed_plan* gelim_mixed_plan_create2(int64_t n, const double* ud, const double* vd, int fp64) {
   const int64_t np = gelim_mixed_padded(n);
   if (n <= 0 || np > gelim_mixed_max_n()) {
@@ -1277,10 +982,14 @@ extern "C" gelim_mixed_plan* gelim_mixed_plan_create2(int64_t n, const double* u
                                 "] (persistent triangular solves: every 128-row block resident)");
     return nullptr;
   }
+  if (!fp64) {
+    GELIM_FAIL(GELIM_E_ARG, "mixed plan: fp32 factors (the former hip-mixed engine) were removed in round 5 -- "
+                            "slower than fp64 hip-rbt at every n and not convergent at 16384; use fp64 = 1");
+    return nullptr;
+  }
   auto* p = new gelim_mixed_plan;
   p->n = n;
   p->np = np;
-  p->fp64 = fp64 ? 1 : 0;
   p->ldm = np + 2;  // 16-byte rows, off the power-of-two stride
   auto fail = [&](const char* what) -> gelim_mixed_plan* {
     GELIM_FAIL(GELIM_E_NOMEM, std::string("mixed plan: ") + what);
@@ -1292,58 +1001,19 @@ extern "C" gelim_mixed_plan* gelim_mixed_plan_create2(int64_t n, const double* u
   if (hipMalloc((void**)&p->M, sizeof(double) * (size_t)np * p->ldm) != hipSuccess) return fail("matrix");
   if (hipMalloc((void**)&p->Dinv, sizeof(double) * (size_t)np * gelim::NB) != hipSuccess) return fail("inverses");
   if (hipMalloc((void**)&p->W, 4 * sizeof(double) * (size_t)np * gelim::NB) != hipSuccess) return fail("W buffer");
-  // lookahead (fp64): from 32 blocks (n = 4096) unless GELIM_RBT_LOOKAHEAD says otherwise
-  {
-    const char* e = std::getenv("GELIM_RBT_LOOKAHEAD");
-    p->lookahead = fp64 && (e ? std::atoi(e) != 0 : np >= 4096);
-    const char* ep = std::getenv("GELIM_RBT_PAIRS");
-    p->pairs = ep ? std::atoi(ep) != 0 : 1;
-    const char* ex = std::getenv("GELIM_RBT_AUX");
-    p->aux_on = ex ? std::atoi(ex) != 0 : 0;  // measured slower (profiles/rbt_engine_round3.txt)
-  }
+  // lookahead from 32 blocks (n = 4096): below it the side stream's share is
+  // too small to pay for the cross-stream waits (2048: 2.04 vs 1.76 ms,
+  // profiles/rbt_trace_8192_r4.txt).  The side GEMMs run on an uncapped grid
+  // (8192 15.0 ms vs 18.7 with 64 CUs reserved for the chain); CU masks,
+  // stream priorities, a third stream for the updates the next inverse does
+  // not read, and one-block (instead of pair) lookahead were all measured
+  // slower in rounds 3-4 (profiles/rbt_engine_round3.txt, stream_prio_r4.txt).
+  p->lookahead = np >= 4096;
   if (p->lookahead) {
-    int dev = 0, ncu = 256;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-    // side grid: uncapped by default (the regular dgemm kernel; the one-CU
-    // inverse still gets a CU as the GEMM's short-lived workgroups retire):
-    // 8192 15.0 ms, 16384 87.6 ms vs 18.7 / 122.7 ms with the persistent
-    // kernel capped 64 CUs short, and 16.0 / 91.3 ms without lookahead
-    int reserve = 0;
-    if (const char* e = std::getenv("GELIM_RBT_RESERVE")) reserve = std::max(0, std::atoi(e));
-    p->cap = reserve == 0 ? 0 : ncu > reserve + 8 ? ncu - reserve : std::max(8, ncu / 2);
-    // GELIM_RBT_MASK=<k>: the side stream's GEMMs stay off k CUs (CU-masked
-    // queue; GELIM_RBT_MASK_SPREAD=0 takes the lowest-numbered CUs) and the
-    // chain runs on a stream of its own, so its thin GEMMs and inverses
-    // always find free CUs
-    int mask = 0, spread = 1;
-    if (const char* e = std::getenv("GELIM_RBT_MASK")) mask = std::max(0, std::atoi(e));
-    if (const char* e = std::getenv("GELIM_RBT_MASK_SPREAD")) spread = std::atoi(e) != 0;
-    if (mask > 0) {
-      if (gelim::masked_stream_create(&p->side, mask, spread) != GELIM_OK) return fail("masked side stream");
-    } else if (gelim::side_stream_create(&p->side) != GELIM_OK) {
-      return fail("side stream");
-    }
-    if (mask > 0 || std::getenv("GELIM_CRIT_PRIO")) {
-      const char* ec = std::getenv("GELIM_RBT_MASK_CRIT");  // 1: the chain on the reserved CUs alone
-      if (mask > 0 && ec && std::atoi(ec) != 0) {
-        if (gelim::masked_stream_create(&p->crit, mask, spread, true) != GELIM_OK) return fail("critical stream");
-      } else if (gelim::side_stream_create(&p->crit, 1) != GELIM_OK) {
-        return fail("critical stream");
-      }
-      if (hipEventCreateWithFlags(&p->ef, hipEventDisableTiming) != hipSuccess) return fail("event");
-      if (hipEventCreateWithFlags(&p->ej, hipEventDisableTiming) != hipSuccess) return fail("event");
-    }
+    if (gelim::side_stream_create(&p->side) != GELIM_OK) return fail("side stream");
     if (hipEventCreateWithFlags(&p->e0, hipEventDisableTiming) != hipSuccess) return fail("event");
     if (hipEventCreateWithFlags(&p->e1, hipEventDisableTiming) != hipSuccess) return fail("event");
-    if (p->pairs && p->aux_on) {
-      if (gelim::side_stream_create(&p->aux) != GELIM_OK) return fail("aux stream");
-      if (hipEventCreateWithFlags(&p->ea, hipEventDisableTiming) != hipSuccess) return fail("event");
-      if (hipEventCreateWithFlags(&p->eb, hipEventDisableTiming) != hipSuccess) return fail("event");
-    }
   }
-  if (!fp64 && hipMalloc((void**)&p->A21f, sizeof(float) * (size_t)np * gelim::NB) != hipSuccess) return fail("A21f");
-  if (!fp64 && hipMalloc((void**)&p->Wf, sizeof(float) * (size_t)np * gelim::NB) != hipSuccess) return fail("Wf");
   if (hipMalloc((void**)&p->ud, sizeof(double) * nd) != hipSuccess) return fail("ud");
   if (hipMalloc((void**)&p->vd, sizeof(double) * nd) != hipSuccess) return fail("vd");
   (void)nblk;
@@ -1352,6 +1022,9 @@ extern "C" gelim_mixed_plan* gelim_mixed_plan_create2(int64_t n, const double* u
   if (hipMalloc((void**)&p->y, sizeof(double) * np) != hipSuccess) return fail("y");
   if (hipMalloc((void**)&p->z, sizeof(double) * np) != hipSuccess) return fail("z");
   if (hipMalloc((void**)&p->xs, sizeof(double) * np) != hipSuccess) return fail("xs");
+  if (hipMalloc((void**)&p->hp, sizeof(double) * 2 * gelim::kMaxBlocks * gelim::kMaxHelpers * gelim::NB) !=
+      hipSuccess)
+    return fail("helper partials");
   if (hipMalloc((void**)&p->info, 16) != hipSuccess) return fail("info");
   for (double** b : {&p->rv, &p->wv, &p->dv, &p->xb})
     if (hipMalloc((void**)b, sizeof(double) * (size_t)n) != hipSuccess) return fail("refinement vectors");
@@ -1362,7 +1035,7 @@ extern "C" gelim_mixed_plan* gelim_mixed_plan_create2(int64_t n, const double* u
 }
 
 extern "C" gelim_mixed_plan* gelim_mixed_plan_create(int64_t n, const double* ud, const double* vd) {
-  return gelim_mixed_plan_create2(n, ud, vd, 0);
+  return gelim_mixed_plan_create2(n, ud, vd, 1);
 }
 
 // Transform the augmented fp64 system's matrix (n x n at aug, leading
@@ -1375,31 +1048,14 @@ extern "C" int gelim_mixed_factor(gelim_mixed_plan* p, const double* aug, int64_
   hipStream_t s = (hipStream_t)stream;
   const int64_t np = p->np, h = np / 4, ldm = p->ldm;
   HIP_TRY(hipMemsetAsync(p->info, 0x7f, 4, s));  // INT_MAX-ish: atomicMin keeps the first bad column
-  hipStream_t caller = s;
-  if (p->crit) {  // fork onto the critical-priority stream; joined below
-    HIP_TRY(hipEventRecord(p->ef, s));
-    HIP_TRY(hipStreamWaitEvent(p->crit, p->ef, 0));
-    s = p->crit;
-  }
   const dim3 grid((unsigned)((h + 255) / 256), (unsigned)h);
   hipLaunchKernelGGL(rbt_matrix_kernel<double>, grid, dim3(256), 0, s, aug, ld, (int)p->n, (int)np, p->ud, p->vd,
                      p->M, ldm);
   HIP_TRY(hipGetLastError());
-  if (p->lookahead && p->pairs && p->aux)
-    GELIM_TRY(factor_la3(p->M, ldm, np, p->Dinv, p->W, p->info, s, p->side, p->aux, p->e0, p->e1, p->ea, p->eb,
-                         p->cap));
-  else if (p->lookahead && p->pairs)
-    GELIM_TRY(factor_la2(p->M, ldm, np, p->Dinv, p->W, p->info, s, p->side, p->e0, p->e1, p->cap));
-  else if (p->lookahead)
-    GELIM_TRY(factor_la(p->M, ldm, np, p->Dinv, p->W, p->info, s, p->side, p->e0, p->e1, p->cap));
+  if (p->lookahead)
+    GELIM_TRY(factor_la2(p->M, ldm, np, p->Dinv, p->W, p->info, s, p->side, p->e0, p->e1));
   else
-    GELIM_TRY(factor_impl(p->M, ldm, np, p->Dinv, p->W, p->fp64 ? nullptr : p->A21f, p->fp64 ? nullptr : p->Wf,
-                          p->info, s));
-  if (p->crit) {
-    HIP_TRY(hipEventRecord(p->ej, s));
-    HIP_TRY(hipStreamWaitEvent(caller, p->ej, 0));
-    s = caller;
-  }
+    GELIM_TRY(factor_impl(p->M, ldm, np, p->Dinv, p->W, p->info, s));
   int h_info = 0;
   HIP_TRY(hipMemcpyAsync(&h_info, p->info, 4, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
@@ -1417,7 +1073,7 @@ extern "C" int gelim_mixed_apply(gelim_mixed_plan* p, const double* r, int64_t i
   hipLaunchKernelGGL(rbt_vec_kernel, dim3(g), dim3(256), 0, s, r, incr, (int)p->n, (int)np, p->ud, 1, p->c, (int)np);
   HIP_TRY(hipGetLastError());
   // c -> z (scratch), y (block-unit-lower result) -> xs (the solution of the transformed system)
-  const int rc = solve_impl<double>(p->M, p->ldm, np, p->Dinv, p->c, p->z, p->y, p->xs, p->flags, s);
+  const int rc = solve_impl<double>(p->M, p->ldm, np, p->Dinv, p->c, p->z, p->y, p->xs, p->flags, s, p->hp);
   if (rc != GELIM_OK) return rc;  // < 0: error; kNotResident: the caller falls back
   // x = V xs, only the first n entries are kept (the padding's are zero in exact arithmetic)
   hipLaunchKernelGGL(rbt_vec_kernel, dim3(g), dim3(256), 0, s, p->xs, (int64_t)1, (int)np, (int)np, p->vd, 0, d,

@@ -801,15 +801,11 @@ struct StepArgs {
 };
 
 
-// Panel IO of the fused step: 2 (default) every coalesced load in flight at
-// once + LDS transpose, LDS-staged coalesced stores; 1 direct 16-byte
-// register loads/stores (uncoalesced: 64 cache lines per instruction); 0
-// LDS-staged passes one slot at a time.  GELIM_PANEL_IO overrides (read per
-// launch, for A/B runs).
-int panel_io_mode() {
-  const char* e = std::getenv("GELIM_PANEL_IO");
-  return e ? std::atoi(e) : 2;
-}
+// Panel IO of the fused step: 2 = every coalesced load in flight at once +
+// LDS transpose, LDS-staged coalesced stores (1 = direct 16-byte register
+// loads/stores, 0 = LDS-staged passes one slot at a time measured within
+// noise of it, profiles/headline_2048_r4.md).
+int panel_io_mode() { return 2; }
 
 __device__ __forceinline__ unsigned long long realtime_now() {
   unsigned long long t;
@@ -1268,13 +1264,9 @@ int panel_factor(double* P, int64_t ldp, int64_t m, int64_t w, int64_t row0, int
 // closing step that only finishes the previous update).
 // Rows of the column-major panel buffers (lout / lprev of lu_step): >= NT * R
 // of the first (largest) step, so every early column store lands in bounds.
-bool step_r3() {
-  static const bool on = [] {
-    const char* e = std::getenv("GELIM_STEP_R3");
-    return !(e && std::atoi(e) == 0);
-  }();
-  return on;
-}
+// Steps of <= 1536 rows run on 3 rows per lane (3.76 -> 3.73 ms per 2048
+// solve, profiles/headline_2048_r4.md).
+bool step_r3() { return true; }
 
 int64_t lu_panel_buffer_ld(int64_t n) {
   int64_t r = 512;
@@ -1363,19 +1355,8 @@ extern "C" int gelim_debug_panel_stamps(int64_t m, int64_t w, unsigned long long
   HIP_TRY(hipMemcpy(P, h.data(), h.size() * 8, hipMemcpyHostToDevice));
   HIP_TRY(hipMemset(info, 0, 16));
   constexpr size_t lds = Panel<512, 4, 16, 1, true>::stage_bytes();
-  const char* e256 = std::getenv("GELIM_NT256");
-  const bool nt256 = e256 && std::atoi(e256) != 0 && m <= 1024;
   for (int rep = 0; rep < 3; ++rep) {
-    if (nt256 && m <= 256)
-      hipLaunchKernelGGL((panel_kernel<256, 1, 16, 1, true>), 1, 256, lds, 0, P, 16, (int)m,
-                         (int)w, 0, piv, info, st, nullptr);
-    else if (nt256 && m <= 512)
-      hipLaunchKernelGGL((panel_kernel<256, 2, 16, 1, true>), 1, 256, lds, 0, P, 16, (int)m,
-                         (int)w, 0, piv, info, st, nullptr);
-    else if (nt256)
-      hipLaunchKernelGGL((panel_kernel<256, 4, 16, 1, true>), 1, 256, lds, 0, P, 16, (int)m,
-                         (int)w, 0, piv, info, st, nullptr);
-    else if (m <= 512)
+    if (m <= 512)
       hipLaunchKernelGGL((panel_kernel<512, 1, 16, 1, true>), 1, 512, lds, 0, P, 16, (int)m,
                          (int)w, 0, piv, info, st, nullptr);
     else if (m <= 1024)
@@ -1437,8 +1418,7 @@ extern "C" int gelim_debug_step_stamps(int64_t n, int64_t j, double* out) {
   double* lbuf = nullptr;
   HIP_TRY(hipMalloc((void**)&lbuf, sizeof(double) * 2 * 16 * ldL));
   auto lb = [&](int64_t i) { return lbuf + (i & 1) * 16 * ldL; };
-  const char* en = std::getenv("GELIM_NARROW");
-  const bool nar = !en || std::atoi(en) != 0;
+  const bool nar = true;
   for (int64_t i = 0; i < j; ++i) {
     GELIM_TRY(lu_step(A, lda, n, i ? 16 * (i - 1) : 0, i ? 16 : 0, i ? pairs + (i - 1) * 72 : nullptr,
                       16 * i, 16, GELIM_PIVOT_PARTIAL, piv, info, pairs + i * 72, 0,

@@ -387,23 +387,14 @@ size_t pivot_persist_ws_bytes(int64_t n) { return (size_t)2 * 256 * 16 + (size_t
 // One persistent launch of the per-pivot elimination (the two-kernel loop's
 // outputs: A factored in place LAPACK-style, ipiv, diag, info).  Returns 1
 // (nothing launched) when the order / device does not admit it: n > 2048, or
-// the grid cannot be co-resident (GELIM_FORCE_NONPERSISTENT=1 forces that),
-// or GELIM_PIVOT_PERSIST=0.
+// the grid cannot be co-resident (GELIM_FORCE_NONPERSISTENT=1 forces that).
+// Shape: 256 threads x 8 rows x 9 column slots per thread, 2048 x 2049 on 256
+// CUs (512 threads x 16 rows x 5 slots on 128 CUs -- half the candidate sweep
+// -- measured slower: 2048 fp64 14.0 vs 13.5 ms).
 template <typename T>
 int pivot_persistent(T* A, int64_t lda, int64_t n, int mode, int* info, int* ipiv, double* diag, void* ws,
                      hipStream_t s) {
-  static const int on = [] {
-    const char* e = std::getenv("GELIM_PIVOT_PERSIST");
-    return e ? std::atoi(e) : 1;
-  }();
-  if (!on || n > 2048 || n < 1) return 1;
-  // GELIM_PIVOT_SHAPE (read per call): 1 (default) = 256 threads x 8 rows x 9
-  // column slots per thread, 2048 x 2049 on 256 CUs; 2 = 512 threads x 16 rows
-  // x 5 slots on 128 CUs (half the workgroups: half the candidate sweep and
-  // half the pivot-row broadcast traffic per step)
-  // (measured slower: 2048 fp64 14.0 vs 13.5 ms)
-  const char* e = std::getenv("GELIM_PIVOT_SHAPE");
-  if (e && std::atoi(e) == 2) return launch_pp<T, 512, 16, 5>(A, lda, n, mode, info, ipiv, diag, ws, s);
+  if (n > 2048 || n < 1) return 1;
   return launch_pp<T, 256, 8, 9>(A, lda, n, mode, info, ipiv, diag, ws, s);
 }
 

@@ -102,14 +102,12 @@ struct gelim_gauss_plan {
   int* pairs = nullptr;                  // per-step net row movement
   bool lookahead = false;                // GELIM_LOOKAHEAD=1: side-stream wide updates
   bool fused = true;                     // GELIM_SCHEDULE=classic: separate update kernels
-  bool narrow = true;                    // GELIM_NARROW=0: next strip updated by the panel WG
+  bool narrow = true;                    // next panel's strip updated by the narrow kernel
   bool resident = false;                 // resident LU (rlu.hip): the default for n <= 1024
   int64_t split = 0;                     // hybrid: fused steps for columns < split, then the
                                          // resident LU on the trailing (n - split) system
   void* rws = nullptr;                   // its hand-off workspace
   double* sbuf = nullptr;                // narrow-update strip buffers (2 x 16 x ldL, column-major, ping-pong)
-  bool narrow_fused = false;             // GELIM_NARROW_FUSED=1: the narrow update inside the step launch
-  unsigned* nflags = nullptr;            // fused narrow: 2 hand-off flags per step (zeroed per solve)
   double* lbuf = nullptr;                // fused steps: factored panels, column-major, ping-pong
   int64_t ldL = 0;                       //   (2 x 16 x ldL doubles)
   // wide-panel engine (n > big_tail): columns [0, big_k) are eliminated by
@@ -132,50 +130,21 @@ struct gelim_gauss_plan {
   int* big_net = nullptr;                // an outer panel's composed row movement (side stream)
   hipStream_t big_side = nullptr;
   std::vector<hipEvent_t> big_ev;        // fork, fact[T], next[T], join
-  // GELIM_BIG_SPLIT=1 (lookahead only, default off): after each leaf only the
-  // NEXT leaf's 32 columns are updated on the caller's stream; the rest of the
-  // leaf's update (the panel's L part, the other columns of P_j / P_j+1) runs
-  // on big_rest beside the next leaf.  Measured slower (8192: 34.0 vs 31.6 ms,
-  // profiles/leaf_shape_r4.txt): the rest work beside the leaf delays it more
-  // than the shorter critical update saves
-  bool big_split = false;
-  hipStream_t big_rest = nullptr;
-  std::vector<hipEvent_t> big_rev;       // per leaf: critical part done (leaf_ev) / rest done
   hipGraphExec_t exec = nullptr;
-  hipGraph_t tpl = nullptr;              // template of exec (GELIM_GRAPH_KEEPTPL=1 keeps it alive)
   // the graph is captured ONCE on plan-owned buffers: the input is staged
   // into work and x / bnorm leave through xbuf / bnbuf, by eager copies
-  // outside it (GELIM_GRAPH_LEGACY=1: capture the caller's pointers and
-  // re-capture whenever they change -- see gelim_gauss_plan_solve)
-  bool legacy_graph = false, keep_tpl = false;
+  // outside it (capturing the caller's pointers and re-capturing whenever
+  // they changed corrupted results with two plans alive on ROCm 7.2,
+  // profiles/graph_recapture.txt)
   double* xbuf = nullptr;
   double* bnbuf = nullptr;
   hipGraphExec_t exec_bn[2] = {nullptr, nullptr};  // fixed-pointer graphs without / with bnorm
-  const void* k_src = nullptr;
-  int64_t k_ld = 0;
-  void* k_dx = nullptr;
-  void* k_bn = nullptr;
 };
 
 namespace {
 
-// Retired graph executables are destroyed; GELIM_GRAPH_PARK=1 parks them
-// instead (never destroyed while the process runs) -- the experiment that
-// ruled exec destruction out as the cause of the cross-plan corruption
-// (profiles/graph_recapture.txt: it was the captured memset nodes).
-std::vector<hipGraphExec_t>& exec_graveyard() {
-  static std::vector<hipGraphExec_t> g;
-  return g;
-}
-
 void retire_exec(hipGraphExec_t e) {
-  if (!e) return;
-  static const bool park = [] {
-    const char* v = std::getenv("GELIM_GRAPH_PARK");
-    return v && std::atoi(v) != 0;
-  }();
-  if (park) exec_graveyard().push_back(e);
-  else (void)hipGraphExecDestroy(e);
+  if (e) (void)hipGraphExecDestroy(e);
 }
 
 constexpr int64_t kPairSlot = 72;  // 1 + 4*16 ints, padded
@@ -215,14 +184,7 @@ __global__ void hybrid_perm_kernel(int* __restrict__ perm, int n, int split, int
 // (profiles/big_nb_lookahead.txt): 8192 128 / 256 / 512 -> 34.2 / 34.8 /
 // 41.1 ms; memplus (n = 17758) 169 / 151 ms for 128 / 256; serial 8192:
 // 43.1 / 41.9 / 42.2 ms.
-int64_t big_nb(bool la, int64_t n) {
-  static const int64_t env = [] {
-    const char* e = std::getenv("GELIM_BIG_NB");
-    const int64_t v = e ? std::atoll(e) : 0;
-    return (v == 512 || v == 256 || v == 128) ? v : int64_t(0);
-  }();
-  return env ? env : ((la && n <= 10240) ? int64_t(128) : int64_t(256));
-}
+int64_t big_nb(bool la, int64_t n) { return (la && n <= 10240) ? int64_t(128) : int64_t(256); }
 constexpr int64_t kBigPairSlot = 1 + 4 * 32 + 3;
 
 int enqueue(gelim_gauss_plan* p, const void* src, int64_t src_ld, void* dx, void* bnorm, hipStream_t s);
@@ -292,8 +254,6 @@ int enqueue_big(gelim_gauss_plan* p, double* A, double* x, double* bnorm, hipStr
     HIP_TRY(hipStreamWaitEvent(side, *ev_fork, 0));
   }
   int leaf = 0;
-  const bool split = la && p->big_split;
-  bool rest_pending = false;  // big_rest has work the caller's stream has not waited for
   for (int64_t j = 0; j < T; ++j) {
     const int64_t k = kb(j), kend = kb(j + 1);
     const int64_t cend = la ? kb(j + 2) : n + 1;  // columns the leaves update: P_j (+ P_j+1)
@@ -304,32 +264,6 @@ int enqueue_big(gelim_gauss_plan* p, double* A, double* x, double* bnorm, hipStr
                                  leaf, s));
       // P_j+1 is side j-1's until next[j-1]
       if (la && c0 == k && j > 0 && cend > kend) HIP_TRY(hipStreamWaitEvent(s, ev_next[j - 1], 0));
-      if (split) {
-        // critical: the next leaf's columns [c1, nx) only (swaps, TRSM of
-        // the leaf's U rows, rank-32 GEMM); they may still carry the previous
-        // leaf's rest update, so wait for it first
-        const int64_t c1 = c0 + LW, nx = std::min(c1 + LW, cend);
-        if (rest_pending) HIP_TRY(hipStreamWaitEvent(s, p->big_rev[2 * (leaf - 1) + 1], 0));
-        rest_pending = false;
-        if (nx > c1) {
-          GELIM_TRY(big::laswp_trsm(A + c0 * lda, lda, c0, 0, 0, c1, nx, nx, n - c0, pr, s));
-          GELIM_TRY(dgemm(A + c1 * lda + c1, lda, A + c1 * lda + c0, lda, A + c0 * lda + c1, lda, n - c1, nx - c1, LW,
-                          -1.0, s));
-        }
-        // the rest on big_rest, beside the next leaf: the panel's L part
-        // (swaps) and the columns [nx, cend) (swaps, TRSM, GEMM)
-        if (nx < cend || c0 > k) {
-          HIP_TRY(hipEventRecord(p->big_rev[2 * leaf], s));
-          HIP_TRY(hipStreamWaitEvent(p->big_rest, p->big_rev[2 * leaf], 0));
-          GELIM_TRY(big::laswp_trsm(A + c0 * lda, lda, c0, k, c0, nx, cend, cend, n - c0, pr, p->big_rest));
-          if (nx < cend)
-            GELIM_TRY(dgemm(A + c1 * lda + nx, lda, A + c1 * lda + c0, lda, A + c0 * lda + nx, lda, n - c1, cend - nx,
-                            LW, -1.0, p->big_rest));
-          HIP_TRY(hipEventRecord(p->big_rev[2 * leaf + 1], p->big_rest));
-          rest_pending = true;
-        }
-        continue;
-      }
       // serial: interchanges on every other column (L part, rest of the
       // panel, trailing columns, b), TRSM inside the panel; lookahead: the
       // panel's own L part and P_j, P_j+1 (swaps + TRSM)
@@ -349,10 +283,6 @@ int enqueue_big(gelim_gauss_plan* p, double* A, double* x, double* bnorm, hipStr
     }
     const int nl = leaf - first_leaf;
     const int* pr0 = p->big_pairs + first_leaf * kBigPairSlot;
-    if (rest_pending) {  // the panel is complete only with its last leaf's rest update
-      HIP_TRY(hipStreamWaitEvent(s, p->big_rev[2 * (leaf - 1) + 1], 0));
-      rest_pending = false;
-    }
     HIP_TRY(hipEventRecord(ev_fact[j], s));
     HIP_TRY(hipStreamWaitEvent(side, ev_fact[j], 0));
     // the panel's row movement composed into one permutation (<= 64 rows per
@@ -431,8 +361,8 @@ int enqueue(gelim_gauss_plan* p, const void* src, int64_t src_ld, void* dx, void
     // narrow(i)'s output: read by step i + 1's panel workgroup while the fused
     // narrow(i + 1) of that same launch writes the other buffer
     auto sb = [&](size_t i) { return p->sbuf + (i & 1) * 16 * p->ldL; };
-    const bool fuse = nar && p->narrow_fused;
-    if (fuse) GELIM_TRY(zero_async(p->nflags, sizeof(unsigned) * 2 * (S + 1), s));
+    // (the narrow update fused into the step launch through flag hand-offs
+    // measured equal, 3.77 vs 3.76 ms, profiles/headline_2048_r4.md)
     for (size_t i = 0; i <= S; ++i) {
       const int64_t kp = i ? p->step_k[i - 1] : 0, wp = i ? p->step_w[i - 1] : 0;
       const int64_t k = i < S ? p->step_k[i] : kend, w = i < S ? p->step_w[i] : 0;
@@ -441,9 +371,9 @@ int enqueue(gelim_gauss_plan* p, const void* src, int64_t src_ld, void* dx, void
       const bool nx = nar && i + 1 < S;  // a narrow update of panel i + 1's strip follows step i
       GELIM_TRY(lu_step(A, lda, n, kp, wp, prev, k, w, p->pivot, p->piv, p->info, cur, s,
                         nar && i ? sb(i - 1) : nullptr, i < S ? lb(i) : nullptr, i ? lb(i - 1) : nullptr,
-                        p->ldL, fuse && nx ? p->nflags + 2 * i : nullptr, sb(i), nx ? p->step_k[i + 1] : 0,
+                        p->ldL, nullptr, sb(i), nx ? p->step_k[i + 1] : 0,
                         nx ? p->step_w[i + 1] : 0));
-      if (nx && !fuse)
+      if (nx)
         GELIM_TRY(lu_narrow(A, lda, n, k, w, cur, p->step_k[i + 1], p->step_w[i + 1], sb(i), s,
                             lb(i), p->ldL));
     }
@@ -563,8 +493,6 @@ extern "C" gelim_gauss_plan* gelim_gauss_plan_create(int64_t n, int algo, int pi
   p->pivot = pivot;
   p->eb = dtype_bytes;
   p->use_graph = use_graph != 0;
-  if (const char* e = std::getenv("GELIM_GRAPH_LEGACY")) p->legacy_graph = std::atoi(e) != 0;
-  if (const char* e = std::getenv("GELIM_GRAPH_KEEPTPL")) p->keep_tpl = std::atoi(e) != 0;
   const int64_t align = 64 / dtype_bytes;  // 64-byte rows
   // the wide-panel engine's GEMMs read 16-byte chunks that may reach one
   // column past b: keep at least one padding column
@@ -602,28 +530,18 @@ extern "C" gelim_gauss_plan* gelim_gauss_plan_create(int64_t n, int algo, int pi
       (void)hipGetDevice(&dev);
       (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
       int reserve = 64;  // 8192: 35.4 ms (32: 36.3, 96: 35.5)
-      if (const char* er = std::getenv("GELIM_BIG_RESERVE")) reserve = std::max(0, std::atoi(er));
       // never fewer free CUs than the first (largest) leaf needs at once: a
       // side GEMM holds its CUs for its whole grid-stride loop, and a leaf
       // whose participants cannot all be resident would spin into its timeout
       reserve = std::max(reserve, gelim::big::leaf_cus(n) + 8);
       p->big_cap = ncu > reserve + 8 ? ncu - reserve : std::max(8, ncu / 2);
       if (gelim::side_stream_create(&p->big_side) != GELIM_OK) return fail("side stream");
-      if (std::getenv("GELIM_BIG_NET") == nullptr || std::atoi(std::getenv("GELIM_BIG_NET")) != 0)
-        if (hipMalloc((void**)&p->big_net, sizeof(int) * (1 + 2 * (size_t)gelim::big::laswp_net_max())) != hipSuccess)
-          return fail("net movement");
+      if (hipMalloc((void**)&p->big_net, sizeof(int) * (1 + 2 * (size_t)gelim::big::laswp_net_max())) != hipSuccess)
+        return fail("net movement");
       const int64_t T = (big_k + big_nb(true, n) - 1) / big_nb(true, n);
       p->big_ev.assign((size_t)(2 * T + 2), nullptr);
       for (auto& e : p->big_ev)
         if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return fail("event");
-      const char* es = std::getenv("GELIM_BIG_SPLIT");
-      p->big_split = es ? std::atoi(es) != 0 : false;
-      if (p->big_split) {
-        if (gelim::side_stream_create(&p->big_rest) != GELIM_OK) return fail("rest stream");
-        p->big_rev.assign((size_t)(2 * nleaves), nullptr);
-        for (auto& e : p->big_rev)
-          if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return fail("event");
-      }
     }
     p->tail = gelim_gauss_plan_create(n - big_k, algo, pivot, dtype_bytes, 0);
     if (!p->tail) {
@@ -648,8 +566,6 @@ extern "C" gelim_gauss_plan* gelim_gauss_plan_create(int64_t n, int algo, int pi
   if (const char* e = std::getenv("GELIM_LOOKAHEAD")) p->lookahead = std::atoi(e) != 0;
   if (const char* e = std::getenv("GELIM_SCHEDULE")) p->fused = std::string(e) != "classic";
   if (p->lookahead) p->fused = false;
-  if (const char* e = std::getenv("GELIM_NARROW")) p->narrow = std::atoi(e) != 0;
-  if (const char* e = std::getenv("GELIM_NARROW_FUSED")) p->narrow_fused = std::atoi(e) != 0;
   {
     // GELIM_SCHEDULE: auto (default) | resident | fused | classic.  auto =
     // the resident LU up to n = 1024 (R <= 2 register slots: measured 0.73
@@ -697,8 +613,6 @@ extern "C" gelim_gauss_plan* gelim_gauss_plan_create(int64_t n, int algo, int pi
     if (hipMalloc((void**)&p->pairs, sizeof(int) * kPairSlot * S) != hipSuccess) return fail("pairs");
     p->ldL = gelim::lu_panel_buffer_ld(n);
     if (hipMalloc((void**)&p->sbuf, sizeof(double) * 2 * 16 * p->ldL) != hipSuccess) return fail("sbuf");
-    if (hipMalloc((void**)&p->nflags, sizeof(unsigned) * 2 * (p->step_k.size() + 1)) != hipSuccess)
-      return fail("nflags");
     if (hipMalloc((void**)&p->lbuf, sizeof(double) * 2 * 16 * p->ldL) != hipSuccess) return fail("lbuf");
     if (p->resident && hipMalloc(&p->rws, gelim::rlu_workspace_bytes(n)) != hipSuccess)
       return fail("resident LU workspace");
@@ -714,7 +628,6 @@ extern "C" void gelim_gauss_plan_destroy(gelim_gauss_plan* p) {
   if (!p) return;
   retire_exec(p->exec);
   for (auto& e : p->exec_bn) retire_exec(e);
-  if (p->tpl) (void)hipGraphDestroy(p->tpl);
   (void)hipFree(p->xbuf);
   (void)hipFree(p->bnbuf);
   if (p->cap) (void)hipStreamDestroy(p->cap);
@@ -722,15 +635,11 @@ extern "C" void gelim_gauss_plan_destroy(gelim_gauss_plan* p) {
   if (p->big_side) (void)hipStreamDestroy(p->big_side);
   for (auto& e : p->big_ev)
     if (e) (void)hipEventDestroy(e);
-  if (p->big_rest) (void)hipStreamDestroy(p->big_rest);
-  for (auto& e : p->big_rev)
-    if (e) (void)hipEventDestroy(e);
   for (auto* v : {&p->ev_panel, &p->ev_wide})
     for (auto& e : *v)
       if (e) (void)hipEventDestroy(e);
   (void)hipFree(p->pairs);
   (void)hipFree(p->sbuf);
-  (void)hipFree(p->nflags);
   (void)hipFree(p->lbuf);
   (void)hipFree(p->rws);
   (void)hipFree(p->work);
@@ -762,10 +671,6 @@ extern "C" int gelim_gauss_plan_solve(gelim_gauss_plan* p, const void* src, int6
   auto capture = [&](const void* csrc, int64_t cld, void* cdx, void* cbn) -> int {
     retire_exec(p->exec);
     p->exec = nullptr;
-    if (p->tpl) {
-      HIP_TRY(hipGraphDestroy(p->tpl));
-      p->tpl = nullptr;
-    }
     hipGraph_t g = nullptr;
     HIP_TRY(hipStreamBeginCapture(p->cap, hipStreamCaptureModeThreadLocal));
     int rc = enqueue(p, csrc, cld, cdx, cbn, p->cap);
@@ -776,26 +681,10 @@ extern "C" int gelim_gauss_plan_solve(gelim_gauss_plan* p, const void* src, int6
     }
     HIP_TRY(e);
     e = hipGraphInstantiate(&p->exec, g, nullptr, nullptr, 0);
-    if (p->keep_tpl) p->tpl = g;
-    else (void)hipGraphDestroy(g);
+    (void)hipGraphDestroy(g);
     HIP_TRY(e);
     return GELIM_OK;
   };
-  if (p->legacy_graph) {
-    // round-1 behaviour: the caller's pointers are baked into the graph and
-    // every change re-captures.  With two or more plans alive this corrupts
-    // results and info words on ROCm 7.2 (profiles/graph_recapture.txt)
-    const bool hit = p->exec && p->k_src == src && p->k_ld == src_ld && p->k_dx == dx && p->k_bn == bnorm;
-    if (!hit) {
-      GELIM_TRY(capture(src, src_ld, dx, bnorm));
-      p->k_src = src;
-      p->k_ld = src_ld;
-      p->k_dx = dx;
-      p->k_bn = bnorm;
-    }
-    HIP_TRY(hipGraphLaunch(p->exec, s));
-    return GELIM_OK;
-  }
   // one graph per plan (and per bnorm on/off), on plan-owned buffers only
   const int64_t n = p->n;
   if (!p->xbuf) {

@@ -838,13 +838,10 @@ int64_t rlu_max_n() { return 2048; }
 
 // The np + 1 workgroups of the resident LU hand panels and strips to each
 // other through flags: they must all be resident at once.
-// Workgroup size of the resident LU for order n: 512 threads (1..4 register
-// slots) by default; GELIM_RLU_NT=1024 takes 1024 threads for n > 1024 (2
-// slots instead of 3-4; read per call).
-int rlu_threads(int64_t n) {
-  const char* e = std::getenv("GELIM_RLU_NT");
-  return (e && std::atoi(e) == 1024 && n > 1024) ? 1024 : 512;
-}
+// Workgroup size of the resident LU: 512 threads (1..4 register slots).
+// (1024 threads -- 2 slots instead of 3-4 above 1024 rows -- spilled: 6.8 ms
+// for the 2048 solve, profiles/headline_2048_r4.md.)
+int rlu_threads(int64_t) { return 512; }
 
 bool rlu_coresident(int64_t n) {
   using namespace rlu;
@@ -852,8 +849,7 @@ bool rlu_coresident(int64_t n) {
   if (!L.R) return false;
   int per = 0;
   hipError_t e = hipSuccess;
-  if (L.NT == 1024) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, rlu_kernel<1024, 2, 1>, 1024, 0);
-  else if (L.R == 1) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, rlu_kernel<512, 1, 1>, 512, 0);
+  if (L.R == 1) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, rlu_kernel<512, 1, 1>, 512, 0);
   else if (L.R == 2) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, rlu_kernel<512, 2, 1>, 512, 0);
   else if (L.R == 3) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, rlu_kernel<512, 3, 1>, 512, 0);
   else e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, rlu_kernel<512, 4, 1>, 512, 0);
@@ -890,18 +886,12 @@ int rlu_factor(const double* src, int64_t lds, double* work, int64_t ldw, int64_
   a.ubuf = reinterpret_cast<double*>(base + L.ubuf);
   a.hbuf = reinterpret_cast<double*>(base + L.hbuf);
   a.pslot = reinterpret_cast<int*>(base + L.pslot);
-  {
-    const char* e = std::getenv("GELIM_RLU_PSLOT");
-    a.pslot_mode = e ? std::atoi(e) : 1;
-  }
+  a.pslot_mode = 1;
   a.stamps = stamps;
   GELIM_TRY(zero_async(a.flags, L.lbuf - L.flags, s));
   const dim3 grid((unsigned)(L.np + 1)), block((unsigned)L.NT);
   const bool part = mode == GELIM_PIVOT_PARTIAL;
-  if (L.NT == 1024) {
-    if (part) hipLaunchKernelGGL((rlu_kernel<1024, 2, 1>), grid, block, 0, s, a);
-    else hipLaunchKernelGGL((rlu_kernel<1024, 2, 0>), grid, block, 0, s, a);
-  } else if (L.R == 1) {
+  if (L.R == 1) {
     if (part) hipLaunchKernelGGL((rlu_kernel<512, 1, 1>), grid, block, 0, s, a);
     else hipLaunchKernelGGL((rlu_kernel<512, 1, 0>), grid, block, 0, s, a);
   } else if (L.R == 2) {

@@ -14,27 +14,13 @@
 namespace gelim {
 namespace {
 
-// wt = 1: write-through (agent-scope sc1) stores, so the launch boundary
-// after the copy has no dirty L2 to write back (GELIM_COPY_WT)
+// (Write-through stores here measured within noise of plain ones, round 4,
+// profiles/dgemm_wt_r4.txt.)
 __global__ __launch_bounds__(256) void copy2d_words_kernel(unsigned* __restrict__ d, int64_t dp,
-                                                          const unsigned* __restrict__ sp, int64_t spp, int64_t w,
-                                                          int wt) {
+                                                          const unsigned* __restrict__ sp, int64_t spp, int64_t w) {
   const unsigned* srow = sp + (int64_t)blockIdx.y * spp;
   unsigned* drow = d + (int64_t)blockIdx.y * dp;
-  if (wt) {
-    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < w; i += (int64_t)gridDim.x * 256)
-      __hip_atomic_store(drow + i, srow[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  } else {
-    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < w; i += (int64_t)gridDim.x * 256) drow[i] = srow[i];
-  }
-}
-
-int copy_wt() {
-  static const int v = [] {
-    const char* e = std::getenv("GELIM_COPY_WT");
-    return e ? std::atoi(e) != 0 : 0;
-  }();
-  return v;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < w; i += (int64_t)gridDim.x * 256) drow[i] = srow[i];
 }
 
 // r[i] = aug[i][n] - sum_j aug[i][j] x[j] (fp64; one wave per row); with
@@ -139,7 +125,7 @@ int copy2d_async(void* dst, size_t dpitch, const void* src, size_t spitch, size_
     const size_t nr = std::min<size_t>(65535, rows - r);
     hipLaunchKernelGGL(copy2d_words_kernel, dim3(bx, (unsigned)nr), dim3(256), 0, s,
                        static_cast<unsigned*>(dst) + r * (dpitch / 4), (int64_t)(dpitch / 4),
-                       static_cast<const unsigned*>(src) + r * (spitch / 4), (int64_t)(spitch / 4), w, copy_wt());
+                       static_cast<const unsigned*>(src) + r * (spitch / 4), (int64_t)(spitch / 4), w);
     HIP_TRY(hipGetLastError());
   }
   return GELIM_OK;
@@ -283,32 +269,20 @@ int probe_words(int** w) {
   return GELIM_OK;
 }
 
-// Stream priority of kind 0 (side streams: GELIM_SIDE_PRIO) or 1 (a
-// critical-chain stream: GELIM_CRIT_PRIO), clamped to the device's range
-// (HIP: lower numbers are higher priorities).  The queue arbiter hands CUs
-// that free up to the higher-priority queue's workgroups first.
-int stream_priority(int kind) {
-  const char* e = std::getenv(kind ? "GELIM_CRIT_PRIO" : "GELIM_SIDE_PRIO");
-  int v = e ? std::atoi(e) : 0;
-  int least = 0, greatest = 0;
-  if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) return 0;
-  return std::max(greatest, std::min(least, v));
-}
-
 // A stream concurrent with the default stream and with others[0..nothers):
-// parked streams of earlier searches are tried first (priority 0 only: a
-// parked stream has the default priority), then up to 8 new ones.
-int probed_stream_create(hipStream_t* out, int kind, hipStream_t const* others, int nothers) {
+// parked streams of earlier searches are tried first, then up to 8 new ones.
+// (Stream priorities for the side streams and for hip-rbt's chain were
+// measured without gain in round 4, profiles/stream_prio_r4.txt.)
+int probed_stream_create(hipStream_t* out, hipStream_t const* others, int nothers) {
   *out = nullptr;
-  const int prio = stream_priority(kind);
   if (!probe_enabled()) {
-    HIP_TRY(hipStreamCreateWithPriority(out, hipStreamNonBlocking, prio));
+    HIP_TRY(hipStreamCreateWithFlags(out, hipStreamNonBlocking));
     return GELIM_OK;
   }
   std::lock_guard<std::mutex> lk(g_park_mu);  // one probe at a time (shared words)
   int* w = nullptr;
   GELIM_TRY(probe_words(&w));
-  if (prio == 0) {
+  {
     for (size_t i = 0; i < g_parked.size(); ++i) {
       const int ok = probe_all(g_parked[i], others, nothers, w);
       ++g_side_stats[0];
@@ -324,7 +298,7 @@ int probed_stream_create(hipStream_t* out, int kind, hipStream_t const* others, 
   hipStream_t s = nullptr;
   int rc = GELIM_OK;
   for (int attempt = 0; attempt < 8; ++attempt) {
-    if (hipStreamCreateWithPriority(&s, hipStreamNonBlocking, prio) != hipSuccess) {
+    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) {
       rc = GELIM_FAIL(GELIM_E_HIP, "side stream");
       s = nullptr;
       break;
@@ -340,34 +314,8 @@ int probed_stream_create(hipStream_t* out, int kind, hipStream_t const* others, 
   return s ? GELIM_OK : rc;
 }
 
-int side_stream_create(hipStream_t* out, int kind) { return probed_stream_create(out, kind, nullptr, 0); }
+int side_stream_create(hipStream_t* out) { return probed_stream_create(out, nullptr, 0); }
 
-}  // namespace gelim
-
-namespace gelim {
-// A stream whose kernels may run on every CU but `reserve` of them, which
-// stay free for the other streams' work (a CU mask is a property of the
-// hardware queue behind the stream).  spread = 1 reserves every
-// (ncu / reserve)-th CU -- the same count in every XCD whichever way the
-// mask bits map onto them -- 0 the lowest-numbered ones.  only = true: the
-// stream runs on the reserved CUs alone.
-int masked_stream_create(hipStream_t* out, int reserve, int spread, bool only) {
-  *out = nullptr;
-  int dev = 0, ncu = 0;
-  HIP_TRY(hipGetDevice(&dev));
-  HIP_TRY(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
-  if (reserve <= 0 || reserve >= ncu) return GELIM_FAIL(GELIM_E_ARG, "masked stream: reserve out of range");
-  std::vector<uint32_t> mask((size_t)(ncu + 31) / 32, 0u);
-  const int step = std::max(1, ncu / reserve);
-  int held = 0;
-  for (int c = 0; c < ncu; ++c) {
-    const bool res = spread ? (c % step == 0 && held < reserve) : c < reserve;
-    held += res ? 1 : 0;
-    if (res == only) mask[(size_t)c / 32] |= 1u << (c % 32);
-  }
-  HIP_TRY(hipExtStreamCreateWithCUMask(out, (uint32_t)mask.size(), mask.data()));
-  return GELIM_OK;
-}
 }  // namespace gelim
 
 // A non-blocking stream that runs concurrently with the default stream
@@ -416,7 +364,7 @@ extern "C" int gelim_gpu_stream_probe(void* stream) {
 extern "C" int gelim_gpu_stream_create_probed(void** out, void* const* others, int32_t nothers) {
   if (nothers < 0 || nothers > 16) return GELIM_FAIL(GELIM_E_ARG, "stream_create_probed: nothers");
   hipStream_t s = nullptr;
-  GELIM_TRY(gelim::probed_stream_create(&s, 0, (hipStream_t const*)others, nothers));
+  GELIM_TRY(gelim::probed_stream_create(&s, (hipStream_t const*)others, nothers));
   *out = (void*)s;
   return GELIM_OK;
 }

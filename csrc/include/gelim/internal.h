@@ -19,10 +19,7 @@ int fail(int code, const char* file, int line, const std::string& msg);
 int zero_async(void* p, size_t bytes, struct ihipStream_t* s);
 // A non-blocking stream probed to run concurrently with the default stream
 // (runtime.hip: streams sharing its hardware queue are parked, up to 8 tries).
-// kind 0: a side stream (priority GELIM_SIDE_PRIO), 1: a critical-chain stream (GELIM_CRIT_PRIO)
-int side_stream_create(struct ihipStream_t** out, int kind = 0);
-// a stream kept off `reserve` CUs (spread over the XCDs when spread = 1)
-int masked_stream_create(struct ihipStream_t** out, int reserve, int spread, bool only = false);
+int side_stream_create(struct ihipStream_t** out);
 // Co-residency guard of the persistent (flag hand-off) kernels: true when
 // `grid` workgroups of a kernel that the occupancy API admits `per_cu` times
 // per CU all fit at once (one block of margin per CU above one, as the API

@@ -8,15 +8,18 @@ Backends
                       the whole solve replayed from a captured hipGraph (fp64)
   hip-pivot         : the reference per-pivot algorithm on the GPU
                       (unit-diagonal elimination, fp64 or fp32)
-  hip-mixed         : random butterfly transform + NO-pivoting blocked LU in
-                      fp32 on the matrix cores + fp64 GMRES-IR on the
+  hip-rbt           : random butterfly transform + NO-pivoting blocked LU with
+                      fp64 factors (fp64 MFMA GEMMs, no per-column global
+                      arg-max) + classic fp64 iterative refinement on the
                       original system, falling back to `hip` (fp64, partial
                       pivoting) whenever it does not reach the fp64 error
-                      class (csrc/hip/lu_mixed.hip); explicit opt-in only
-                      (slower than hip-rbt at every benched n)
-  hip-rbt           : the same transform and NO-pivoting blocked LU with fp64
-                      factors (fp64 MFMA GEMMs, no per-column global arg-max)
-                      + classic fp64 iterative refinement, same fallback
+                      class (csrc/hip/lu_mixed.hip)
+
+fp32 elimination + fp64 refinement is `hip-pivot` with
+dtype=float32 and `solve_refined` (stored fp32 factors, O(n^2) per
+correction).  The round-3/4 "hip-mixed" engine (fp32 trailing products +
+GMRES-IR) was removed in round 5: slower than hip-rbt at every n and not
+convergent at 16384 (profiles/trsv_split_r5.txt).
   seq / omp / pthreads-v1 / pthreads-v2 / pthreads-v3 : the reference CPU
                       strategies (csrc/cpu/gauss_cpu.cpp), fp64
 
@@ -35,9 +38,8 @@ from ..ops import lu
 from ..utils.tensors import ptr, row_major_ld, stream_handle
 
 GPU_BACKENDS = {"hip": _native.GPU_BLOCKED, "hip-blocked": _native.GPU_BLOCKED, "hip-pivot": _native.GPU_PIVOT}
-MIXED_BACKEND = "hip-mixed"
 RBT_BACKEND = "hip-rbt"
-RBT_BACKENDS = {MIXED_BACKEND: 0, RBT_BACKEND: 1}  # factor precision: 0 fp32, 1 fp64
+RBT_BACKENDS = {RBT_BACKEND: 1}  # factor precision: fp64
 CPU_BACKENDS = tuple(cpu_ops.CPU_BACKENDS)
 RESOLVE_LDS_BYTES = 160 * 1024  # lower_resolve_kernel (csrc/hip/gauss_pivot.hip)
 BACKENDS = tuple(GPU_BACKENDS) + tuple(RBT_BACKENDS) + CPU_BACKENDS
@@ -56,17 +58,13 @@ class GaussSolver:
         self._mixed = None
         self._fp64 = None
         self.last_steps = 0
-        self.last_inner = 0
         self.last_fallback = None
         self.last_berr = None
         if backend in ("hip", "hip-blocked") and dtype == torch.float32:
-            # round 3 mapped this to hip-mixed, which is slower than hip-rbt at
-            # every benched n (GMRES-IR pays a triangular-solve pair per
-            # iteration): fp32 factors are now an explicit opt-in
             raise ValueError("the blocked LU is fp64 (partial-pivoting accuracy on the reference matrices); "
-                             "for fp32 factors choose backend='hip-mixed' (fp32 trailing products + fp64 "
-                             "GMRES-IR) or backend='hip-pivot' (the reference loop in fp32); the fastest "
-                             "fp64-class solver is backend='hip-rbt'")
+                             "for fp32 elimination choose backend='hip-pivot' (the reference loop in fp32, "
+                             "solve_refined for fp64 accuracy); the fastest fp64-class solver is "
+                             "backend='hip-rbt'")
         self.gpu = backend in GPU_BACKENDS or backend in RBT_BACKENDS
         if backend in RBT_BACKENDS:
             self._init_mixed(device, seed=0x5eed, fp64=RBT_BACKENDS[backend])
@@ -117,168 +115,39 @@ class GaussSolver:
             self._fp64 = GaussSolver(self.n, backend="hip", pivot=self.pivot, device=self.device)
         return self._fp64.solve(aug64, check=check)
 
-    class _NotResident(Exception):
-        """The persistent block solves cannot be co-resident on this device."""
-
-    def _apply(self, r: torch.Tensor, inc: int, out: torch.Tensor, sh) -> None:
-        rc = _native.check(_native.lib().gelim_mixed_apply(self._mixed, ptr(r), inc, ptr(out), sh), "mixed_apply")
-        if rc > 0:
-            raise GaussSolver._NotResident()
-
-    def _gmres(self, aug64: torch.Tensor, r: torch.Tensor, restart: int = 30, tol: float = 1e-6) -> torch.Tensor:
-        """d ~ A^-1 r by left-preconditioned GMRES in fp64 (Carson-Higham
-        GMRES-IR): M^-1 = V (LU)^-1 U^T from the fp32 factors, A v on the
-        fp64 system (native mat-vec), classical Gram-Schmidt with one
-        re-orthogonalisation, Givens rotations on the host.  Stops when the
-        preconditioned residual has dropped by `tol` or after `restart`
-        iterations."""
-        import numpy as np
-
-        n, dev = self.n, self.device
-        lib = _native.lib()
-        sh = stream_handle(dev)
-        ld = aug64.stride(0)
-        Vb = torch.empty((restart + 1, n), dtype=torch.float64, device=dev)
-        w = torch.empty(n, dtype=torch.float64, device=dev)
-        z = torch.empty(n, dtype=torch.float64, device=dev)
-        self._apply(r, 1, z, sh)
-        beta = float(z.norm())
-        if not beta > 0.0 or beta != beta:
-            return torch.zeros(n, dtype=torch.float64, device=dev)
-        Vb[0] = z / beta
-        H = np.zeros((restart + 1, restart))
-        cs, sn = np.zeros(restart), np.zeros(restart)
-        g = np.zeros(restart + 1)
-        g[0] = beta
-        k = 0
-        for j in range(restart):
-            _native.check(lib.gelim_gpu_matvec(ptr(aug64), ld, n, ptr(Vb[j]), ptr(w), sh), "matvec")
-            self._apply(w, 1, z, sh)
-            B = Vb[:j + 1]
-            h = B @ z
-            z -= B.T @ h
-            h2 = B @ z
-            z -= B.T @ h2
-            h += h2
-            hv = torch.cat([h, z.norm().reshape(1)]).cpu().numpy()
-            H[:j + 2, j] = hv
-            self.last_inner += 1
-            k = j + 1
-            if not hv[-1] > 0.0:  # breakdown: the Krylov space holds the solution
-                for i in range(j):
-                    a, b = H[i, j], H[i + 1, j]
-                    H[i, j], H[i + 1, j] = cs[i] * a + sn[i] * b, -sn[i] * a + cs[i] * b
-                break
-            Vb[j + 1] = z / hv[-1]
-            for i in range(j):  # previous rotations on the new column
-                a, b = H[i, j], H[i + 1, j]
-                H[i, j], H[i + 1, j] = cs[i] * a + sn[i] * b, -sn[i] * a + cs[i] * b
-            den = float(np.hypot(H[j, j], H[j + 1, j]))
-            cs[j], sn[j] = H[j, j] / den, H[j + 1, j] / den
-            H[j, j], H[j + 1, j] = den, 0.0
-            g[j + 1] = -sn[j] * g[j]
-            g[j] = cs[j] * g[j]
-            if abs(g[j + 1]) <= tol * beta:
-                break
-        y = np.zeros(k)
-        for i in reversed(range(k)):  # H[:k, :k] upper triangular now
-            y[i] = (g[i] - H[i, i + 1:k] @ y[i + 1:k]) / H[i, i]
-        return Vb[:k].T @ torch.from_numpy(y).to(dev)
-
     def _solve_mixed(self, aug: torch.Tensor, max_steps: int = 6, check: bool = False) -> torch.Tensor:
         """x of the augmented system: RBT + no-pivot LU, then x <- x + d
         until the componentwise backward error max_i |r_i| / (|b| + |A||x|)_i
         is <= 4 eps64 (or <= sqrt(n) eps64 once refinement stagnates), at most
-        max_steps outer corrections (last_berr holds the final value).  d = (LU)^-1 r with fp64 factors (hip-rbt: classic
-        refinement), or from GMRES preconditioned by the fp32 factors
-        (hip-mixed: Carson-Higham GMRES-IR); the residual is always fp64 on
-        the ORIGINAL system.  A stall, a zero pivot or too many steps hand the
+        max_steps outer corrections (last_berr holds the final value), d =
+        (LU)^-1 r with the fp64 factors; the residual is always fp64 on the
+        ORIGINAL system.  A stall, a zero pivot or too many steps hand the
         system to the fp64 partial-pivoting engine (last_fallback says why;
-        last_steps counts outer corrections, last_inner GMRES iterations)."""
+        last_steps counts outer corrections)."""
         n, dev = self.n, self.device
         lib = _native.lib()
         aug64 = aug.to(dev, torch.float64)
         if aug64.shape[0] != n or aug64.shape[1] < n + 1 or aug64.stride(1) != 1:
             aug64 = aug64[:, :n + 1].contiguous()
-        self.last_steps, self.last_inner, self.last_fallback = 0, 0, None
+        self.last_steps, self.last_fallback = 0, None
         if self._mixed is None:
             return self._fallback(aug64, self._mixed_unavailable or "no mixed plan", check)
         ld = aug64.stride(0)
         sh = stream_handle(dev)
-        if self.dtype == torch.float64:
-            # hip-rbt: the whole solve + classic refinement in native code
-            # (csrc/hip/lu_mixed.hip gelim_mixed_solve: one 8-byte read-back
-            # per correction)
-            import ctypes
+        # the whole solve + classic refinement in native code (csrc/hip/
+        # lu_mixed.hip gelim_mixed_solve: one 8-byte read-back per correction)
+        import ctypes
 
-            x = torch.empty(n, dtype=torch.float64, device=dev)
-            st, be = ctypes.c_int(0), ctypes.c_double(0.0)
-            rc = lib.gelim_mixed_solve(self._mixed, ptr(aug64), ld, ptr(x), max_steps, ctypes.byref(st),
-                                       ctypes.byref(be), sh)
-            _native.check(rc, "mixed_solve")
-            self.last_steps, self.last_berr = st.value, be.value
-            if rc == 1:
-                return self._fallback(aug64, f"no-pivot LU: zero pivot or refinement stalled after {st.value} "
-                                             f"corrections (componentwise backward error {be.value:.3e})", check)
-            return x
-        rc = lib.gelim_mixed_factor(self._mixed, ptr(aug64), ld, sh)
-        _native.check(rc, "mixed_factor")
-        if rc > 0:
-            return self._fallback(aug64, f"no-pivot LU: zero or non-finite pivot at column {rc - 1}", check)
-        try:
-            return self._refine_fp32(aug64, max_steps, check)
-        except GaussSolver._NotResident:
-            return self._fallback(aug64, "the persistent block solves cannot be co-resident", check)
-
-    def _refine_fp32(self, aug64: torch.Tensor, max_steps: int, check: bool) -> torch.Tensor:
-        """hip-mixed: x from the fp32-product factors, then GMRES-IR
-        corrections (see _solve_mixed)."""
-        import math
-
-        n, dev = self.n, self.device
-        lib = _native.lib()
-        ld = aug64.stride(0)
-        sh = stream_handle(dev)
-        # the hand-off error word is zeroed once per solve; every apply only
-        # sets it, so the check after each correction covers all of them
-        _native.check(lib.gelim_mixed_reset_error(self._mixed, sh), "mixed_reset_error")
-        b = aug64[:, n]
         x = torch.empty(n, dtype=torch.float64, device=dev)
-        self._apply(b, ld, x, sh)
-        # componentwise backward error w = max_i |r_i| / (|b| + |A||x|)_i (one
-        # native pass gives r and the denominator): refine until w <= 4 eps64;
-        # once a correction stops reducing it by 10 %, accept w <= sqrt(n) eps64.  A
-        # norm-wise test (LAPACK dsgesv's ||r|| <= sqrt(n) eps ||A|| ||x||) is
-        # too weak for badly row-scaled systems: on sherman3 it accepted an x
-        # whose error was ~2e3 (a row of scale 1e10 dominates ||A||).
-        eps = torch.finfo(torch.float64).eps
-        strict, loose = 4.0 * eps, max(math.sqrt(n), 8.0) * eps
-        r = torch.empty(n, dtype=torch.float64, device=dev)
-        wv = torch.empty(n, dtype=torch.float64, device=dev)
-        prev, best = math.inf, None
-        for it in range(max_steps + 1):
-            _native.check(lib.gelim_gpu_residual_cw(ptr(aug64), ld, n, ptr(x), ptr(r), ptr(wv), sh), "residual")
-            om = float((r.abs() / wv.clamp_min(torch.finfo(torch.float64).tiny)).max())
-            self.last_steps = it
-            self.last_berr = om
-            if om <= strict:
-                return x
-            if lib.gelim_mixed_solve_error(self._mixed, sh) != 0:
-                return self._fallback(aug64, "a triangular-solve hand-off timed out", check)
-            if not om < 0.9 * prev or it == max_steps:  # NaN, stagnated or out of steps
-                # the better of the current x and the saved best one, if acceptable
-                if om <= loose and (best is None or om <= best[0]):
-                    return x
-                if best is not None and best[0] <= loose:
-                    self.last_berr = best[0]
-                    return best[1]
-                return self._fallback(aug64, f"refinement stalled after {it} corrections "
-                                             f"(componentwise backward error {om:.3e} > {loose:.3e})", check)
-            if best is None or om < best[0]:
-                best = (om, x.clone())
-            prev = om
-            x += self._gmres(aug64, r)
-        raise AssertionError("unreachable")
+        st, be = ctypes.c_int(0), ctypes.c_double(0.0)
+        rc = lib.gelim_mixed_solve(self._mixed, ptr(aug64), ld, ptr(x), max_steps, ctypes.byref(st),
+                                   ctypes.byref(be), sh)
+        _native.check(rc, "mixed_solve")
+        self.last_steps, self.last_berr = st.value, be.value
+        if rc == 1:
+            return self._fallback(aug64, f"no-pivot LU: zero pivot or refinement stalled after {st.value} "
+                                         f"corrections (componentwise backward error {be.value:.3e})", check)
+        return x
 
     # -- GPU ---------------------------------------------------------------
     def _solve_gpu(self, aug: torch.Tensor, want_bnorm: bool):

@@ -12,7 +12,7 @@ import os
 import sys
 from pathlib import Path
 
-os.environ.setdefault("GELIM_DGEMM_THIN", "0")  # "lds" = dgemm.hip's LDS-tiled kernel
+
 
 import torch
 

@@ -17,6 +17,12 @@ one local GEMV; refinement = 1 + corrections applies, each followed by a
 residual (local |A||x| mat-vec + an all_reduce of 2 np doubles).
 Setup: the butterfly transform (local) and the all_gather of the super-blocks
 (np x 128 P doubles) and of the inverses (np x 128).
+Host issue (round 5, profiles/dist_issue_r5.md): the host must issue a
+block's ~15 launches and 2 collectives; a block then costs
+max(chain_k, side_k, issue) -- issue = 255 us eagerly through
+torch.distributed, 176 us eagerly through libgelim's RCCL communicators, 28 us
+replaying the captured hipGraph (the default; the graph launch overlaps the
+GPU).
 
   python scripts/dist_rbt_critical_path.py [n]
 """
@@ -36,7 +42,10 @@ def t_gemm_thin(m: int) -> float:
     return 9.5 + 2.0 * max(0, m - 1024) / 7040
 
 
-def model(n: int, P: int, lat: float, bw: float, corrections: int = 2) -> dict:
+ISSUE_US = {"torch-eager": 255.0, "native-eager": 176.0, "graph": 28.0}
+
+
+def model(n: int, P: int, lat: float, bw: float, corrections: int = 2, issue: float = 0.0) -> dict:
     NB = 128
     np_ = -(-n // (512 * P)) * 512 * P
     nb = np_ // NB
@@ -53,12 +62,13 @@ def model(n: int, P: int, lat: float, bw: float, corrections: int = 2) -> dict:
         s = 2 * t_gemm_thin(NB) + 2.0 * m * cols * NB / 40e6
         chain += c
         side += s
-        fac += max(c, s)
+        fac += max(c, s, issue)
     fac += T_INV
     S = NB * P
     ns = np_ // S
     t_ss = T_SS.get(P, T_SS[8] * P / 8)
-    per_apply = 2 * ns * (lat + S * 8 * us_per_byte + t_ss + T_GEMV)
+    # the applies are graph-replayed too: ~4 launches + 1 all_reduce per super-block
+    per_apply = 2 * ns * max(lat + S * 8 * us_per_byte + t_ss + T_GEMV, issue / 4)
     resid = lat + 2 * np_ * 8 * us_per_byte + 10.0
     solves = (1 + corrections) * (per_apply + resid)
     gather = (np_ * S * 8 + np_ * NB * 8) * us_per_byte * (P - 1) / P + 2 * lat
@@ -70,12 +80,14 @@ def model(n: int, P: int, lat: float, bw: float, corrections: int = 2) -> dict:
 def main():
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 8192
     print(f"# n = {n}; inverse {T_INV} us, block solves {T_SS} us, GEMV {T_GEMV} us, pack {T_PACK_8192} us/8.4 MB")
-    print("P  lat(us) BW(GB/s)  chain  side-bound  factor  solves  setup   total (ms)")
-    for P in (2, 4, 8):
-        for lat, bw in ((15.0, 100.0), (25.0, 50.0)):
-            r = model(n, P, lat, bw)
-            print(f"{P}  {lat:6.0f} {bw:8.0f} {r['chain'] / 1e3:7.2f} {r['side'] / 1e3:10.2f} {r['factor'] / 1e3:7.2f} "
-                  f"{r['solves'] / 1e3:7.2f} {r['setup'] / 1e3:6.2f} {r['total'] / 1e3:7.2f}")
+    for name, iss in ISSUE_US.items():
+        print(f"# host issue: {name} ({iss:.0f} us per block)")
+        print("P  lat(us) BW(GB/s)  chain  side-bound  factor  solves  setup   total (ms)")
+        for P in (2, 4, 8):
+            for lat, bw in ((15.0, 100.0), (25.0, 50.0)):
+                r = model(n, P, lat, bw, issue=iss)
+                print(f"{P}  {lat:6.0f} {bw:8.0f} {r['chain'] / 1e3:7.2f} {r['side'] / 1e3:10.2f} "
+                      f"{r['factor'] / 1e3:7.2f} {r['solves'] / 1e3:7.2f} {r['setup'] / 1e3:6.2f} {r['total'] / 1e3:7.2f}")
 
 
 if __name__ == "__main__":

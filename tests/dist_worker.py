@@ -234,6 +234,27 @@ def rccl_one_rank(outdir, n_gauss=2048, n_rbt=2048):
         sn = summa_matmul(none, A, B, (1, 1), panels=3)
         res["matmul_summa"] = {"bitwise": bool(torch.equal(sp, sn)),
                                "subgroup_backend": groups[0].backend, "subgroup_pg": groups[0].pg}
+        # libgelim's RCCL communicator directly: every collective x every dtype
+        nc = comm.rccl()
+        cur = torch.cuda.current_stream(dev).cuda_stream
+        native = {}
+        for dt in (torch.float64, torch.float32, torch.int32, torch.int64, torch.uint8):
+            base = (torch.arange(1, 301, device=dev) % 100).to(dt)
+            t = base.clone()
+            nc.bcast(t, 0, cur)
+            native[f"bcast_{dt}"] = bool(torch.equal(t, base))
+            for op in ("sum", "max", "min"):
+                t = base.clone()
+                nc.allreduce(t, op, cur)
+                native[f"allreduce_{op}_{dt}"] = bool(torch.equal(t, base))
+            o = torch.zeros(300, dtype=dt, device=dev)
+            nc.allgather(o, base, cur)
+            native[f"allgather_{dt}"] = bool(torch.equal(o, base))
+            o = torch.zeros(300, dtype=dt, device=dev)
+            nc.sendrecv(base, 0, o, 0, cur)
+            native[f"sendrecv_{dt}"] = bool(torch.equal(o, base))
+        torch.cuda.synchronize(dev)
+        res["native_ops"] = native
         # point-to-point through RCCL: a batched send to / receive from the rank itself
         t = torch.arange(1000, dtype=torch.float64, device=dev)
         r = torch.zeros_like(t)

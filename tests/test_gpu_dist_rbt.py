@@ -143,3 +143,27 @@ def test_dist_rbt_gpu_processes(tmp_path, gelim, cuda, world, n):
     aug = gelim.random_system(n, seed=23, device=cuda)
     ref = torch.linalg.solve(aug[:, :n], aug[:, n]).cpu()
     assert _rel(xs[0], ref) < 1e-9
+
+
+@pytest.mark.parametrize("n", [1000, 2048, 4200])
+def test_graph_replay_matches_eager(gelim, cuda, n):
+    """One rank, no collectives: the factorisation loop and the applies run
+    eagerly on the first solve, are captured into hipGraphs on the second and
+    replayed from the third -- every solve gives the eager bits."""
+    from gelim.parallel import DistributedRBT
+    from gelim.parallel.comm import Communicator
+
+    comm = Communicator(0, 1, cuda, "none")
+    d = DistributedRBT(comm, n, single_fast_path=False)
+    assert d.graph
+    xs = [d.solve_(d.generate_random(seed=n)).cpu() for _ in range(4)]
+    assert set(d._graphs) == {"factor", "apply"} and all(v is not None for v in d._graphs.values())
+    e = DistributedRBT(comm, n, single_fast_path=False, graph=False)
+    xe = e.solve_(e.generate_random(seed=n)).cpu()
+    for x in xs:
+        assert torch.equal(x, xe)
+    aug = gelim.random_system(n, seed=n, device=cuda).cpu()
+    ref = torch.linalg.solve(aug[:, :n], aug[:, n])
+    assert ((xe - ref).abs().max() / ref.abs().max()).item() < 1e-9
+    d.close()
+    e.close()

@@ -191,3 +191,47 @@ def test_block_inverse_matches_torch(gelim, cuda, kind):
                         "block_inverse")
     torch.cuda.synchronize()
     assert info.item() == 385
+
+
+@pytest.mark.parametrize("n", [130, 1000, 4200, 8192])
+def test_split_solves_match_one_workgroup_solves(gelim, cuda, n):
+    """One apply of the factor (V (LU)^-1 U^T r) through the plan -- split
+    triangular solves, K helper workgroups per block row -- against the same
+    apply assembled from the one-workgroup-per-block-row kernel
+    (gelim_rbt_block_solve, lower then upper) and the butterfly vectors: the
+    two sum the off-diagonal products in different orders, so they agree to
+    rounding, not bit for bit."""
+    import ctypes
+
+    from gelim.utils.tensors import ptr, stream_handle
+
+    lib = gelim._native.lib()
+    aug = gelim.random_system(n, seed=n + 17, device=cuda)
+    s = gelim.GaussSolver(n, backend="hip-rbt", device=cuda)
+    s.solve(aug, check=True)
+    plan = s._mixed
+    ptrs = (ctypes.c_void_p * 3)()
+    ldm = int(lib.gelim_mixed_debug_ptrs(plan, ctypes.cast(ptrs, ctypes.c_void_p)))
+    np_ = int(lib.gelim_mixed_plan_np(plan))
+    nblk = np_ // 128
+    sh = stream_handle(cuda)
+    g = torch.Generator(device=cuda).manual_seed(n)
+    r = torch.randn(n, dtype=torch.float64, device=cuda, generator=g)
+    d_split = torch.empty(n, dtype=torch.float64, device=cuda)
+    assert lib.gelim_mixed_apply(plan, ptr(r), 1, ptr(d_split), sh) == 0
+    ud = torch.from_numpy(s._ud).to(cuda)
+    vd = torch.from_numpy(s._vd).to(cuda)
+    c, z, y, x = (torch.empty(np_, dtype=torch.float64, device=cuda) for _ in range(4))
+    err = torch.zeros(1, dtype=torch.int32, device=cuda)
+    gelim._native.check(lib.gelim_rbt_vec(ptr(r), 1, n, np_, ptr(ud), 1, ptr(c), np_, sh), "rbt_vec")
+    gelim._native.check(lib.gelim_rbt_block_solve(ptrs[0], ldm, ptrs[1], nblk, ptr(c), ptr(z), ptr(y), 0, ptr(err),
+                                                  sh), "block_solve lower")
+    gelim._native.check(lib.gelim_rbt_block_solve(ptrs[0], ldm, ptrs[1], nblk, ptr(y), ptr(x), None, 1, ptr(err),
+                                                  sh), "block_solve upper")
+    d_old = torch.empty(n, dtype=torch.float64, device=cuda)
+    gelim._native.check(lib.gelim_rbt_vec(ptr(x), 1, np_, np_, ptr(vd), 0, ptr(d_old), n, sh), "rbt_vec")
+    torch.cuda.synchronize()
+    assert int(err.item()) == 0
+    rel = ((d_split - d_old).abs().max() / d_old.abs().max()).item()
+    assert rel < 1e-10, rel
+    s.close()

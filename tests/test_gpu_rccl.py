@@ -98,3 +98,13 @@ def test_rccl_dist_matmul_bitwise(rccl_run):
 def test_rccl_p2p_self(rccl_run):
     _, res = rccl_run
     assert res["p2p_self"]["ok"], res["p2p_self"]
+
+
+@pytest.mark.parametrize("op", ["bcast", "allreduce_sum", "allreduce_max", "allreduce_min", "allgather", "sendrecv"])
+@pytest.mark.parametrize("dtype", ["torch.float64", "torch.float32", "torch.int32", "torch.int64", "torch.uint8"])
+def test_native_rccl_ops(rccl_run, op, dtype):
+    """libgelim's own RCCL communicator (csrc/comm/rccl_comm.hip, torch's
+    librccl.so, the id through the process group's store): each collective
+    in each supported dtype, one rank, on the current stream."""
+    _, res = rccl_run
+    assert res["native_ops"][f"{op}_{dtype}"], res["native_ops"]

@@ -74,3 +74,13 @@ def test_dedicated_streams_pairwise_concurrent(gelim, cuda):
             assert lib.gelim_gpu_probe_kernel(sb.cuda_stream, ptr(w), 1, 0) == 0
             torch.cuda.synchronize(cuda)
             assert int(w[1].item()) == 1, f"{b} does not run beside {a}"
+
+
+def test_dedicated_stream_roles_are_distinct_and_cached(gelim, cuda):
+    from gelim.utils.tensors import dedicated_stream
+
+    a = dedicated_stream(cuda, "side")
+    b = dedicated_stream(cuda, "comm")
+    assert a is dedicated_stream(cuda, "side") and b is dedicated_stream(cuda, "comm")
+    assert a.cuda_stream != b.cuda_stream
+    assert torch.cuda.default_stream(cuda).cuda_stream not in (a.cuda_stream, b.cuda_stream)

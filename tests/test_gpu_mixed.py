@@ -198,9 +198,13 @@ def test_split_solves_match_one_workgroup_solves(gelim, cuda, n):
     """One apply of the factor (V (LU)^-1 U^T r) through the plan -- split
     triangular solves, K helper workgroups per block row -- against the same
     apply assembled from the one-workgroup-per-block-row kernel
-    (gelim_rbt_block_solve, lower then upper) and the butterfly vectors: the
-    two sum the off-diagonal products in different orders, so they agree to
-    rounding, not bit for bit."""
+    (gelim_rbt_block_solve, lower then upper) and against dense fp64
+    torch.linalg.solve of the same block-triangular systems.  The kernels sum
+    the off-diagonal products in different orders, and the factor's diagonal
+    blocks reach cond ~1e6 without pivoting, so they agree to rounding times
+    that conditioning (3e-8 relative at 8192), not bit for bit: the split
+    solve must be as close to the dense reference as the one-workgroup solve
+    is (an indexing or hand-off error would be O(1))."""
     import ctypes
 
     from gelim.utils.tensors import ptr, stream_handle
@@ -232,6 +236,23 @@ def test_split_solves_match_one_workgroup_solves(gelim, cuda, n):
     gelim._native.check(lib.gelim_rbt_vec(ptr(x), 1, np_, np_, ptr(vd), 0, ptr(d_old), n, sh), "rbt_vec")
     torch.cuda.synchronize()
     assert int(err.item()) == 0
-    rel = ((d_split - d_old).abs().max() / d_old.abs().max()).item()
-    assert rel < 1e-10, rel
+    # dense reference: forward L_full z = c (block lower part of the factor,
+    # its Schur diagonal blocks included), y = Ldiag z, backward U_full x = y
+    Mbuf = torch.empty(np_ * ldm, dtype=torch.float64, device=cuda)
+    gelim._native.check(lib.gelim_mixed_debug_copy(Mbuf.data_ptr(), ptrs[0], Mbuf.numel() * 8), "copy")
+    M = Mbuf.view(np_, ldm)[:, :np_]
+    blk = torch.arange(np_, device=cuda) // 128
+    lower = blk.view(-1, 1) >= blk.view(1, -1)
+    upper = blk.view(-1, 1) <= blk.view(1, -1)
+    diag = lower & upper
+    zr = torch.linalg.solve(torch.where(lower, M, 0.0), c)
+    xr = torch.linalg.solve(torch.where(upper, M, 0.0), torch.where(diag, M, 0.0) @ zr)
+    d_ref = torch.empty(n, dtype=torch.float64, device=cuda)
+    gelim._native.check(lib.gelim_rbt_vec(ptr(xr), 1, np_, np_, ptr(vd), 0, ptr(d_ref), n, sh), "rbt_vec")
+    torch.cuda.synchronize()
+    scale = d_ref.abs().max()
+    e_split = ((d_split - d_ref).abs().max() / scale).item()
+    e_old = ((d_old - d_ref).abs().max() / scale).item()
+    assert e_split <= max(4 * e_old, 1e-12), (e_split, e_old)
+    assert ((d_split - d_old).abs().max() / scale).item() < 1e-6
     s.close()

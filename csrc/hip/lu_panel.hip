@@ -1266,7 +1266,6 @@ int panel_factor(double* P, int64_t ldp, int64_t m, int64_t w, int64_t row0, int
 // of the first (largest) step, so every early column store lands in bounds.
 // Steps of <= 1536 rows run on 3 rows per lane (3.76 -> 3.73 ms per 2048
 // solve, profiles/headline_2048_r4.md).
-bool step_r3() { return true; }
 
 int64_t lu_panel_buffer_ld(int64_t n) {
   int64_t r = 512;
@@ -1306,8 +1305,8 @@ int lu_step(double* A, int64_t lda, int64_t n, int64_t kp, int64_t wp, const int
   if (m <= 512 && w <= 16) return launch_step<512, 1, 16>(a, mode, blocks, s);
   if (m <= 1024 && w <= 16) return launch_step<512, 2, 16>(a, mode, blocks, s);
   // 3 rows per lane below 1536 rows: the column loop is VALU-issue bound and
-  // its per-row work shrinks by a quarter (GELIM_STEP_R3=0: 4 rows up to 2048)
-  if (m <= 1536 && w <= 16 && step_r3()) return launch_step<512, 3, 16>(a, mode, blocks, s);
+  // its per-row work shrinks by a quarter (round 4: 3.76 -> 3.73 ms at 2048)
+  if (m <= 1536 && w <= 16) return launch_step<512, 3, 16>(a, mode, blocks, s);
   if (m <= 2048 && w <= 16) return launch_step<512, 4, 16>(a, mode, blocks, s);
   if (m <= 4096 && w <= 8) return launch_step<512, 8, 8>(a, mode, blocks, s);
   if (m <= 8192 && w <= 4) return launch_step<512, 16, 4>(a, mode, blocks, s);

@@ -54,8 +54,7 @@ def main() -> None:
         A.copy_(A0)
 
     t_leaf = timeit(leaf) - timeit(copy_only)
-    import os
-    print(f"leaf m={m} (GELIM_LEAF_SHAPE={os.environ.get('GELIM_LEAF_SHAPE', 'default')}, "
+    print(f"leaf m={m} ("
           f"{lib.gelim_gpu_leaf_participants(m)} participants): {t_leaf:.1f} us ({t_leaf / 32:.2f} us/column)")
     if "--time-only" in sys.argv:
         return

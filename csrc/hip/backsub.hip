@@ -2,17 +2,16 @@
 // Pthreads/Version-1/gauss_internal_input.c:212-227, a serial O(n^2) loop
 // there).
 //
-// Default: ONE persistent launch (backsub_persist_kernel).  Row block b (64
-// equations) belongs to workgroup b and x is produced bottom-up.  Every
-// workgroup preloads its 64x64 diagonal triangle into wave 0's registers,
-// then takes the solved x blocks below it in order (last block first): for
-// each it prefetches the matching 64x64 block of U BEFORE polling that
-// block's flag, so after the hand-off only x_c (512 B) is read, and
-// subtracts U[b, c] x_c (wave per row, shuffle sums).  After the last one,
-// wave 0 solves the triangle (rows in lanes, x_i broadcast with v_readlane:
-// mul -> readlane -> fma per step) and publishes x_b (sc1 stores, drain,
-// flag).  The critical path per block is one hand-off + one block mat-vec +
-// the 64-step chain, instead of one dependent kernel launch per block.
+// Default: ONE persistent launch (backsub_persist_kernel), row block b (64
+// equations) in workgroup b, x produced bottom-up.  Round 5 form: every
+// workgroup first forms W = T^-1 U[b, b+1] and W2 = T^-1 U[b, b+2] (T its
+// diagonal triangle; all workgroups at once, off the chain); its compute
+// waves accumulate U[b, c] x_c for c > b + 2 as the x_c land; a poller wave
+// solves T v' = y_b - sum two chain steps ahead, and the chain itself is
+// two 64 x 64 mat-vecs, x_b = v' - W2 x_{b+2} - W x_{b+1}.  x itself is the
+// hand-off: pre-filled with a signalling-NaN sentinel, each value stored sc1
+// and polled sc1 (no flag).  2048: 155 -> ~75 us per solve (4.8 -> ~1.8 us
+// per block), profiles/backsub_r5.txt.
 // Spins are bounded (200 ms) and report through an error word.
 //
 // Rows may be indirect: perm[i] is the row of U (and of y) that holds
@@ -91,103 +90,326 @@ __device__ __forceinline__ double solve_diag(const double (&row)[kBS], double ri
   return xv;
 }
 
-// Bounded poll of flag c by lane 0 of the calling wave (wave-uniform result).
-__device__ __forceinline__ bool poll_flag(unsigned* flags, int c, int* err, bool nap) {
-  int good = 1;
-  if (__lane_id() == 0) {
-    if (__hip_atomic_load(&flags[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
-      const unsigned long long t0 = rtc();
-      while (__hip_atomic_load(&flags[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
-        if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0 || rtc() - t0 > kSpinTicks) {
-          __hip_atomic_store(err, 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          good = 0;
-          break;
-        }
-        if (nap) __builtin_amdgcn_s_sleep(1);
+// ---- persistent form ---------------------------------------------------------
+// x is pre-filled with a signalling-NaN sentinel (arithmetic only ever makes
+// quiet NaNs), and every x value is its own hand-off: stored sc1 by its
+// producer, polled with sc1 loads by its consumers (a data-tagged granule, no
+// separate flag: one hop instead of payload -> drain -> flag -> poll).
+constexpr uint64_t kXSent = 0x7ff4dead7ff4deadull;
+
+__global__ void fill_sent_kernel(uint64_t* __restrict__ x, int n, int* __restrict__ err) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) x[i] = kXSent;
+  if (i == 0 && err) *err = 0;
+}
+
+// Wave-wide bounded poll until lanes < cw of x[c0 ..] are published; returns
+// this lane's value.  false (and the error word set) when the spin ran out or
+// another workgroup already gave up.
+__device__ __forceinline__ bool poll_x(const double* __restrict__ x, int c0, int cw, int* err, bool nap,
+                                       double& xl) {
+  const int lane = __lane_id();
+  const unsigned long long* p = reinterpret_cast<const unsigned long long*>(x + c0 + min(lane, cw - 1));
+  uint64_t v = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (__ballot(v == kXSent) != 0) {
+    const unsigned long long t0 = rtc();
+    for (int it = 0;; ++it) {
+      if (nap) __builtin_amdgcn_s_sleep(1);
+      v = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (__ballot(v == kXSent) == 0) break;
+      // every 16th probe: another workgroup gave up, or this spin ran out
+      // (not every probe: the extra load would double each probe's round trip)
+      if ((it & 15) == 15 &&
+          (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0 || rtc() - t0 > kSpinTicks)) {
+        if (lane == 0) __hip_atomic_store(err, 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return false;
       }
     }
   }
-  return __builtin_amdgcn_readfirstlane(good) != 0;  // lane 0's verdict (no ds_bpermute round trip)
+  xl = lane < cw ? __builtin_bit_cast(double, v) : 0.0;
+  return true;
 }
 
-// acc -= U[rows of this block, block c] . x_c, row = lane: the U block was
-// prefetched into u[] before the poll; x_c (stored write-through by its
-// producer) is read with one agent-scope load per lane and broadcast with
-// readlane.
-template <typename T>
-__device__ __forceinline__ bool apply_block(const T* __restrict__ U, int64_t ldu, int pr, int c, int n,
-                                            const double* __restrict__ x, unsigned* flags, int* err, bool nap,
-                                            double& acc) {
-  const int lane = __lane_id();
-  const int c0 = c * kBS, cw = min(kBS, n - c0);
-  double u[kBS];
-  const T* urow = U + (int64_t)pr * ldu + c0;
+// Swizzled 64 x 64 fp64 tile in LDS: element (i, j) at row i, 16-byte chunk
+// (j / 2) ^ (i & 31) -- row-per-lane reads and column-per-lane writes of one
+// row are both conflict-free.
+__device__ __forceinline__ int swz64(int i, int j) { return i * kBS + ((((j >> 1) ^ (i & 31))) << 1) + (j & 1); }
+
+// T^-1 B for the upper-triangular 64 x 64 T (tT holds T transposed, rd the
+// reciprocals of its diagonal), one column of B per lane: column-oriented
+// back substitution over all 64 right-hand sides at once.  acc holds the
+// lane's column of B on entry, of T^-1 B on exit.
+__device__ __forceinline__ void tri_inv_apply(const double (*tT)[kBS], const double* rd, double (&acc)[kBS]) {
 #pragma unroll
-  for (int k = 0; k < kBS; ++k) u[k] = (double)urow[min(k, cw - 1)];
-  if (!poll_flag(flags, c, err, nap)) return false;
-  const double xl = __builtin_bit_cast(
-      double, __hip_atomic_load(reinterpret_cast<const unsigned long long*>(x + c0 + min(lane, cw - 1)),
-                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-  const uint64_t xb = __builtin_bit_cast(uint64_t, xl);
-  const int xlo = (int)(unsigned)xb, xhi = (int)(unsigned)(xb >> 32);
+  for (int k = kBS - 1; k >= 0; --k) {
+    const double xk = acc[k] * rd[k];
+    acc[k] = xk;
 #pragma unroll
-  for (int k = 0; k < kBS; ++k) {
-    if (k < cw) {
-      const double xk = __builtin_bit_cast(double, ((uint64_t)(unsigned)__builtin_amdgcn_readlane(xhi, k) << 32) |
-                                                        (unsigned)__builtin_amdgcn_readlane(xlo, k));
-      acc = fma(-u[k], xk, acc);
+    for (int i = 0; i < k; i += 2) {
+      const double2 t = *reinterpret_cast<const double2*>(&tT[k][i]);  // T[i][k], T[i+1][k] (uniform)
+      acc[i] = fma(-t.x, xk, acc[i]);
+      if (i + 1 < k) acc[i + 1] = fma(-t.y, xk, acc[i + 1]);
     }
+  }
+}
+
+// Bounded wait (LDS spin) until *p >= want or the poller gave up.
+__device__ __forceinline__ bool lds_wait(const int* p, int want, const int* abort_flag) {
+  if (__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= want) return true;
+  const unsigned long long t0 = rtc();
+  while (__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < want) {
+    if (__hip_atomic_load(abort_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != 0 || rtc() - t0 > kSpinTicks)
+      return false;
   }
   return true;
 }
 
-// Block b (64 equations, lane = equation) of the persistent back
-// substitution.  Wave 0 owns the critical path: it keeps the diagonal
-// triangle in registers, takes the LAST hand-off (block b+1) itself and then
-// solves the triangle; waves 1..3 take the blocks below b+1 (their x are
-// published earlier) round-robin in the background and hand their partial
-// sums over through LDS behind one barrier.  Every load of a U block is
-// issued before its flag is polled.
+constexpr int kRing = 16;  // x vectors in flight between the poller and the compute waves
+constexpr int kPf = 4;     // U slices in flight per compute wave
+constexpr int kBsThreads = 5 * 64;
+
 template <typename T>
-__global__ __launch_bounds__(256) void backsub_persist_kernel(const T* __restrict__ U, int64_t ldu,
-                                                              const T* __restrict__ y, int64_t incy,
-                                                              const int* __restrict__ perm,
-                                                              double* __restrict__ x,
-                                                              double* __restrict__ bnorm, int n,
-                                                              int unit, unsigned* flags, int* err) {
+__device__ __forceinline__ void load_slice(double (&us)[16], const T* __restrict__ urow, int c, int n, int w) {
+  const int c0 = c * kBS, cw = min(kBS, n - c0);
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const int j = 16 * w + q;
+    us[q] = (double)dev::load_sel(urow + c0 + min(j, cw - 1), j < cw, T(0));
+  }
+}
+
+// Row `lane` of a swizzled LDS tile into registers: the 32 reads issued as
+// one group (the scheduler otherwise takes them four at a time, one LDS round
+// trip per group).
+__device__ __forceinline__ void load_tile_row(const double* tile, int lane, double (&m)[kBS]) {
+#pragma unroll
+  for (int k = 0; k < kBS; k += 2) {
+    const double2 v2 = *reinterpret_cast<const double2*>(&tile[swz64(lane, k)]);
+    m[k] = v2.x;
+    m[k + 1] = v2.y;
+  }
+  __builtin_amdgcn_sched_group_barrier(0x100, 32, 0);
+}
+
+// sum_k m[k] z_k with z broadcast from LDS (uniform ds_read_b128, two values
+// per read), 16 reads per group.
+__device__ __forceinline__ double row_dot_bcast(const double (&m)[kBS], const double* zv) {
+  double a[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int h = 0; h < kBS; h += 32) {
+    double z[32];
+#pragma unroll
+    for (int k = 0; k < 32; k += 2) {
+      const double2 v2 = *reinterpret_cast<const double2*>(&zv[h + k]);
+      z[k] = v2.x;
+      z[k + 1] = v2.y;
+    }
+    __builtin_amdgcn_sched_group_barrier(0x100, 16, 1);
+#pragma unroll
+    for (int k = 0; k < 32; ++k) a[k & 3] = fma(m[h + k], z[k], a[k & 3]);
+    __builtin_amdgcn_sched_group_barrier(0x002, 32, 1);
+  }
+  return (a[0] + a[1]) + (a[2] + a[3]);
+}
+
+// One wave solves T v = r, row per lane: the lane's row of T is read from
+// T^T in LDS into registers first (64 independent reads), then per step the
+// lane-k value is broadcast with v_readlane and the rows above update.
+__device__ __forceinline__ double tri_solve_wave(const double (*tT)[kBS], double rdl, double r, int lane) {
+  double tr[kBS];
+#pragma unroll
+  for (int k = 0; k < kBS; ++k) tr[k] = tT[k][lane];
+#pragma unroll
+  for (int k = kBS - 1; k > 0; --k) {
+    const double xl = r * rdl;  // meaningful in lane k
+    const uint64_t bb = __builtin_bit_cast(uint64_t, xl);
+    const double xk = __builtin_bit_cast(double, ((uint64_t)(unsigned)__builtin_amdgcn_readlane((int)(bb >> 32), k) << 32) |
+                                                     (unsigned)__builtin_amdgcn_readlane((int)bb, k));
+    r = lane < k ? fma(-tr[k], xk, r) : r;
+  }
+  // lane i's r stopped changing at step i: x_i = r_i / T[i][i], no select chain
+  return r * rdl;
+}
+
+// Block b (64 equations) of the persistent back substitution: 4 compute waves
+// + 1 poller wave.  With T = U[b, b], U1 = U[b, b+1], U2 = U[b, b+2]:
+//   x_b = T^-1 (y_b - sum_{c >= b+3} U[b, c] x_c) - W2 x_{b+2} - W x_{b+1},
+//   W = T^-1 U1, W2 = T^-1 U2 (column back substitutions, backward stable).
+// T^-1 itself is never formed: applying an explicit inverse to the running
+// right-hand side loses accuracy on ill-conditioned diagonal blocks (the
+// zero-pivot rule's U: 2-4x the error of a plain solve), the two W products
+// do not (profiles/backsub_r5.txt).
+//  prologue (all workgroups at once): T^T, U1, U2 staged in LDS; wave 0 forms
+//  W, wave 1 W2;
+//  background: the poller polls x_c, c = nb-1 .. b+3, as they land and passes
+//  each into an LDS ring; compute wave w accumulates its 16-column slice of
+//  U[b, c] x_c from U slices loaded kPf blocks ahead (the poller is the only
+//  wave with a global load in flight when it polls, so a poll never waits
+//  behind a prefetch -- vmcnt retires loads in order); the poller then solves
+//  T v' = y_b - sum (one wave, 64 steps) -- two chain steps before x_b is due;
+//  chain: v = v' - W2 x_{b+2} once x_{b+2} lands, x_b = v - W x_{b+1} once
+//  x_{b+1} lands (one mat-vec each, the next poll issued before the mat-vec),
+//  then x_b is stored sc1: each x value is its own hand-off.
+template <typename T>
+__global__ __launch_bounds__(kBsThreads) void backsub_persist_kernel(const T* __restrict__ U, int64_t ldu,
+                                                                     const T* __restrict__ y, int64_t incy,
+                                                                     const int* __restrict__ perm,
+                                                                     double* __restrict__ x,
+                                                                     double* __restrict__ bnorm, int n,
+                                                                     int unit, int* err) {
+  __shared__ __attribute__((aligned(16))) double tT[kBS][kBS];  // T^T
+  __shared__ __attribute__((aligned(16))) double u1[kBS * kBS];  // U1, then W (swizzled)
+  __shared__ __attribute__((aligned(16))) double u2[kBS * kBS];  // U2, then W2 (swizzled)
+  __shared__ __attribute__((aligned(16))) double xs[kRing][kBS];
+  __shared__ __attribute__((aligned(16))) double zb[2][kBS];  // poller: broadcast vectors
   __shared__ double part[4][kBS];
+  __shared__ double rd[kBS];
+  __shared__ double ys[kBS];  // y_b: the poller's only global loads are its probes
+  __shared__ double vb[kBS];  // wave 0 -> poller: v = v' - W2 x_{b+2}
+  __shared__ int xseq, done[4], abort_flag, vready;
   const int b = blockIdx.x, nb = gridDim.x;
-  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int r0 = b * kBS, rows = min(kBS, n - r0);
-  const int i = r0 + min(lane, rows - 1);
-  const int pr = rowof(perm, i, n);
-  if (wv == 0 && perm && lane < rows && perm[i] != pr)
-    __hip_atomic_store(err, 7, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  double acc = 0.0;
-  bool ok = true;
-  if (wv == 0) {
-    double drow[kBS];
-    double rinv = 1.0;
-    load_diag<T>(U, ldu, perm, n, r0, rows, unit, drow, rinv);
-    const double v = (double)y[(int64_t)pr * incy];
-    if (bnorm && lane < rows) bnorm[i] = unit ? v : v / (double)U[(int64_t)pr * ldu + i];
-    if (b + 1 < nb) ok = apply_block<T>(U, ldu, pr, b + 1, n, x, flags, err, false, acc);
-    __syncthreads();
+  const bool has1 = b + 1 < nb, has2 = b + 2 < nb;
+  const int c1 = r0 + kBS, cw1 = has1 ? min(kBS, n - c1) : 0;
+  const int c2 = r0 + 2 * kBS, cw2 = has2 ? min(kBS, n - c2) : 0;
+  const int nbg = nb - b - 3 > 0 ? nb - b - 3 : 0;  // background blocks c = nb-1 .. b+3
+
+  // ---- stage T (transposed, identity-padded), U1, U2 (zero-padded) ---------
+  if (t == 0) {
+    xseq = 0;
+    abort_flag = 0;
+    vready = 0;
+  }
+  if (t < 4) done[t] = 0;
+  if (t < 256) {
+    const int i = t >> 2, q0 = (t & 3) * 16;  // row i, columns q0 .. q0+15
+    const int pr = rowof(perm, r0 + min(i, rows - 1), n);
+    if (perm && q0 == 0 && i < rows && perm[r0 + i] != pr)
+      __hip_atomic_store(err, 7, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (q0 == 0) ys[i] = i < rows ? (double)y[(int64_t)pr * incy] : 0.0;
+    const T* src = U + (int64_t)pr * ldu;
+    double tv[16], uv[16], vv[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int j = q0 + q;
+      tv[q] = dev::load_sel(src + r0 + min(j, rows - 1), i < rows && j < rows && j >= i, T(0));
+      uv[q] = has1 ? (double)dev::load_sel(src + c1 + min(j, cw1 - 1), i < rows && j < cw1, T(0)) : 0.0;
+      vv[q] = has2 ? (double)dev::load_sel(src + c2 + min(j, cw2 - 1), i < rows && j < cw2, T(0)) : 0.0;
+    }
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int j = q0 + q;
+      double d = tv[q];
+      if (j == i) {
+        d = (i >= rows || unit) ? 1.0 : d;
+        rd[i] = 1.0 / d;
+        if (bnorm && i < rows) {
+          const double yv = (double)y[(int64_t)pr * incy];
+          bnorm[r0 + i] = unit ? yv : yv / d;
+        }
+      }
+      tT[j][i] = d;
+      u1[i * kBS + j] = uv[q];
+      u2[i * kBS + j] = vv[q];
+    }
+  }
+  __syncthreads();
+  // ---- wave 0: W = T^-1 U1; wave 1: W2 = T^-1 U2 (one column per lane) -----
+  if ((w == 0 && has1) || (w == 1 && has2)) {
+    double* m = w == 0 ? u1 : u2;
+    double acc[kBS];
+#pragma unroll
+    for (int i = 0; i < kBS; ++i) acc[i] = m[i * kBS + lane];
+    tri_inv_apply(tT, rd, acc);
+    // only this wave touches m: overwrite it in place, swizzled
+#pragma unroll
+    for (int i = 0; i < kBS; ++i) m[swz64(i, lane)] = acc[i];
+  }
+  __syncthreads();
+  const int pr = rowof(perm, r0 + min(lane, rows - 1), n);
+
+  if (w < 4) {
+    // ---- compute waves: this wave's 16-column slice of U[b, c] x_c ---------
+    const T* urow = U + (int64_t)pr * ldu;
+    double us[kPf][16];
+#pragma unroll
+    for (int d = 0; d < kPf; ++d)
+      if (d < nbg) load_slice<T>(us[d], urow, nb - 1 - d, n, w);
+    double ra = 0.0, rb = 0.0;
+    bool ok = true;
+    for (int s0 = 0; s0 < nbg && ok; s0 += kPf) {
+#pragma unroll
+      for (int d = 0; d < kPf; ++d) {
+        const int sq = s0 + d;
+        if (sq < nbg && ok) {
+          ok = lds_wait(&xseq, sq + 1, &abort_flag);
+          if (ok) {
+            const double* xv = &xs[sq % kRing][16 * w];
+#pragma unroll
+            for (int q = 0; q < 16; q += 2) {
+              const double2 xx = *reinterpret_cast<const double2*>(xv + q);
+              ra = fma(us[d][q], xx.x, ra);
+              rb = fma(us[d][q + 1], xx.y, rb);
+            }
+            if (lane == 0) __hip_atomic_store(&done[w], sq + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (sq + kPf < nbg) load_slice<T>(us[d], urow, nb - 1 - (sq + kPf), n, w);
+          }
+        }
+      }
+    }
+    part[w][lane] = ra + rb;
+    if (lane == 0) __hip_atomic_store(&done[w], nbg + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (w != 0) return;
+    // ---- wave 0: T v' = y_b - sum, then v = v' - W2 x_{b+2} -----------------
+    for (int q = 1; q < 4 && ok; ++q) ok = lds_wait(&done[q], nbg + 1, &abort_flag);
     if (!ok) return;
-    double yv = v + acc + part[1][lane] + part[2][lane] + part[3][lane];
-    const double xv = solve_diag(drow, rinv, yv, rows);
-    if (lane < rows)
-      __hip_atomic_store(reinterpret_cast<unsigned long long*>(x + r0 + lane), __builtin_bit_cast(unsigned long long, xv),
-                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (lane == 0) __hip_atomic_store(&flags[b], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const double r = ys[lane] - ((part[0][lane] + part[1][lane]) + (part[2][lane] + part[3][lane]));
+    double v = tri_solve_wave(tT, rd[lane], r, lane);
+    if (has2) {
+      double m[kBS];
+      load_tile_row(u2, lane, m);
+      if (!lds_wait(&xseq, nbg + 1, &abort_flag)) return;  // x_{b+2}: the ring's last entry
+      v -= row_dot_bcast(m, xs[nbg % kRing]);
+    }
+    vb[lane] = v;
+    if (lane == 0) __hip_atomic_store(&vready, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     return;
   }
-  // background waves: blocks nb-1 .. b+2, wave 1 + (nb-1-c) % 3
-  for (int c = nb - 1 - (wv - 1); c >= b + 2 && ok; c -= 3)
-    ok = apply_block<T>(U, ldu, pr, c, n, x, flags, err, true, acc);
-  part[wv][lane] = acc;  // 0 when the wave had no block
-  __syncthreads();
+
+  // ---- poller wave: x_c, c = nb-1 .. b+2, into the ring; then the chain ----
+  double wrow[kBS];  // row `lane` of W
+  if (has1) load_tile_row(u1, lane, wrow);
+  bool ok = true;
+  const int nring = has2 ? nbg + 1 : 0;
+  for (int sq = 0; sq < nring && ok; ++sq) {
+    const int c = nb - 1 - sq;
+    if (sq >= kRing) {  // the ring slot is free once every compute wave used x of sq - kRing
+      const int need = sq - kRing + 1;
+      for (int q = 0; q < 4 && ok; ++q) ok = lds_wait(&done[q], need, &abort_flag);
+    }
+    double xl = 0.0;
+    ok = ok && poll_x(x, c * kBS, min(kBS, n - c * kBS), err, false, xl);
+    if (ok) {
+      xs[sq % kRing][lane] = xl;
+      if (lane == 0) __hip_atomic_store(&xseq, sq + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+  }
+  double xl1 = 0.0;
+  if (has1 && ok) ok = poll_x(x, c1, cw1, err, false, xl1);
+  if (ok) ok = lds_wait(&vready, 1, &abort_flag);
+  if (!ok) {
+    if (lane == 0) __hip_atomic_store(&abort_flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    return;
+  }
+  double v = vb[lane];
+  if (has1) {
+    zb[1][lane] = xl1;
+    v -= row_dot_bcast(wrow, zb[1]);
+  }
+  if (lane < rows)
+    __hip_atomic_store(reinterpret_cast<unsigned long long*>(x + r0 + lane), __builtin_bit_cast(unsigned long long, v),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // ---- fallback: one launch per block ----------------------------------------
@@ -262,20 +484,17 @@ int backsub_impl(const T* U, int64_t ldu, const T* y, int64_t incy, double* x, d
   bool persist = nblk <= kMaxPersistBlocks;
   if (persist) {
     int per = 0;
-    persist = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, backsub_persist_kernel<T>, 256, 0) == hipSuccess &&
+    persist = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, backsub_persist_kernel<T>, kBsThreads, 0) == hipSuccess &&
               coresident(per, nblk);
   }
   if (persist) {
-    // flags (+ the error word when the caller has none) live in yw
-    unsigned* flags = reinterpret_cast<unsigned*>(yw);
-    int* e = err ? err : reinterpret_cast<int*>(flags + nblk);
-    // (nblk + 1) words always fit in yw's n doubles; round to 16 bytes when
-    // that still fits (a 16-byte multiple is the fast memset path)
-    const size_t bytes = ((size_t)nblk + 1) * 4;
-    const size_t rounded = (bytes + 15) / 16 * 16;
-    GELIM_TRY(zero_async(flags, rounded <= (size_t)n * sizeof(double) ? rounded : bytes, s));
-    hipLaunchKernelGGL(backsub_persist_kernel<T>, dim3((unsigned)nblk), dim3(256), 0, s, U, ldu, y, incy,
-                       perm, x, bnorm, (int)n, unit, flags, e);
+    // the error word lives in yw when the caller has none
+    int* e = err ? err : reinterpret_cast<int*>(yw);
+    hipLaunchKernelGGL(fill_sent_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s,
+                       reinterpret_cast<uint64_t*>(x), (int)n, e);
+    HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(backsub_persist_kernel<T>, dim3((unsigned)nblk), dim3(kBsThreads), 0, s, U, ldu, y, incy,
+                       perm, x, bnorm, (int)n, unit, e);
     HIP_TRY(hipGetLastError());
     return GELIM_OK;
   }

@@ -104,6 +104,28 @@ def test_backsub(gelim, cuda, n, unit):
     assert torch.allclose(x.cpu(), ref, rtol=1e-10, atol=1e-10)
 
 
+@pytest.mark.parametrize("n", [130, 4200, 8192])
+def test_backsub_block_inverse_form(gelim, cuda, n, monkeypatch):
+    """The persistent back substitution (backsub.hip, round 5) reads only the
+    upper triangle of a full matrix (LU storage: multipliers below), inverts
+    its 64 x 64 diagonal blocks and chains x_b = v - W x_{b+1}; it must agree
+    with torch's triangular solve and with the one-launch-per-block fallback
+    (forced with GELIM_FORCE_NONPERSISTENT=1) to fp64 rounding."""
+    g = torch.Generator(device=cuda).manual_seed(n)
+    A = torch.randn(n, n, dtype=torch.float64, device=cuda, generator=g)
+    A += (2.0 + torch.rand(n, dtype=torch.float64, device=cuda, generator=g)).diag() * n ** 0.5
+    y = torch.randn(n, dtype=torch.float64, device=cuda, generator=g)
+    ref = torch.linalg.solve_triangular(torch.triu(A), y[:, None], upper=True)[:, 0]
+    x = gelim.ops.lu.backsub(A, y)
+    torch.cuda.synchronize()
+    scale = ref.abs().max().item()
+    assert (x - ref).abs().max().item() <= 1e-12 * scale
+    monkeypatch.setenv("GELIM_FORCE_NONPERSISTENT", "1")
+    x2 = gelim.ops.lu.backsub(A, y)
+    torch.cuda.synchronize()
+    assert (x - x2).abs().max().item() <= 1e-12 * scale
+
+
 def test_device_random_matches_host(gelim, cuda):
     h = gelim.random_system(130, seed=42)
     d = gelim.random_system(130, seed=42, device=cuda)

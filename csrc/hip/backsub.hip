@@ -135,22 +135,77 @@ __device__ __forceinline__ bool poll_x(const double* __restrict__ x, int c0, int
 // row are both conflict-free.
 __device__ __forceinline__ int swz64(int i, int j) { return i * kBS + ((((j >> 1) ^ (i & 31))) << 1) + (j & 1); }
 
-// T^-1 B for the upper-triangular 64 x 64 T (tT holds T transposed, rd the
-// reciprocals of its diagonal), one column of B per lane: column-oriented
-// back substitution over all 64 right-hand sides at once.  acc holds the
-// lane's column of B on entry, of T^-1 B on exit.
-__device__ __forceinline__ void tri_inv_apply(const double (*tT)[kBS], const double* rd, double (&acc)[kBS]) {
-#pragma unroll
-  for (int k = kBS - 1; k >= 0; --k) {
-    const double xk = acc[k] * rd[k];
-    acc[k] = xk;
-#pragma unroll
-    for (int i = 0; i < k; i += 2) {
-      const double2 t = *reinterpret_cast<const double2*>(&tT[k][i]);  // T[i][k], T[i+1][k] (uniform)
-      acc[i] = fma(-t.x, xk, acc[i]);
-      if (i + 1 < k) acc[i + 1] = fma(-t.y, xk, acc[i + 1]);
-    }
+// T^-1 B for the upper-triangular 64 x 64 T (tT holds T transposed, rdv
+// lane k = 1 / T[k][k]), one column of B per lane: column-oriented back
+// substitution over all 64 right-hand sides at once.  acc holds the lane's
+// column of B on entry, of T^-1 B on exit.  The uniform T values come from
+// LDS in 8-value chunks, software-pipelined one chunk ahead (the reads of
+// chunk n+1 are issued before the FMAs of chunk n): without it the compiler
+// waited on nearly every broadcast read (~15 us per 64 columns).
+constexpr int tri_chunks() {
+  int c = 0;
+  for (int k = kBS - 1; k >= 1; --k) c += (k + 7) / 8;
+  return c;
+}
+constexpr int kTriChunks = tri_chunks();
+constexpr int tri_chunk_k(int nth) {
+  for (int k = kBS - 1; k >= 1; --k) {
+    const int c = (k + 7) / 8;
+    if (nth < c) return k;
+    nth -= c;
   }
+  return 0;
+}
+constexpr int tri_chunk_i0(int nth) {
+  for (int k = kBS - 1; k >= 1; --k) {
+    const int c = (k + 7) / 8;
+    if (nth < c) return nth * 8;
+    nth -= c;
+  }
+  return 0;
+}
+
+__device__ __forceinline__ double lane_value(double v, int k) {
+  const uint64_t b = __builtin_bit_cast(uint64_t, v);
+  return __builtin_bit_cast(double, ((uint64_t)(unsigned)__builtin_amdgcn_readlane((int)(b >> 32), k) << 32) |
+                                        (unsigned)__builtin_amdgcn_readlane((int)b, k));
+}
+
+template <int N>
+__device__ __forceinline__ void tri_read_chunk(const double (*tT)[kBS], double (&c)[8]) {
+  constexpr int k = tri_chunk_k(N), i0 = tri_chunk_i0(N);
+#pragma unroll
+  for (int q = 0; q < 8; q += 2)
+    if (i0 + q < k) {
+      const double2 t = *reinterpret_cast<const double2*>(&tT[k][i0 + q]);  // T[i][k], T[i+1][k] (uniform)
+      c[q] = t.x;
+      c[q + 1] = t.y;
+    }
+}
+
+template <int N>
+__device__ __forceinline__ void tri_chunks_from(const double (*tT)[kBS], double rdv, double (&acc)[kBS],
+                                                const double (&cur)[8], double xk) {
+  if constexpr (N < kTriChunks) {
+    constexpr int k = tri_chunk_k(N), i0 = tri_chunk_i0(N);
+    double nxt[8];
+    if constexpr (N + 1 < kTriChunks) tri_read_chunk<N + 1>(tT, nxt);
+    if constexpr (i0 == 0) {  // first chunk of column k: x_k is final
+      xk = acc[k] * lane_value(rdv, k);
+      acc[k] = xk;
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+      if (i0 + q < k) acc[i0 + q] = fma(-cur[q], xk, acc[i0 + q]);
+    tri_chunks_from<N + 1>(tT, rdv, acc, nxt, xk);
+  }
+}
+
+__device__ __forceinline__ void tri_inv_apply(const double (*tT)[kBS], double rdv, double (&acc)[kBS]) {
+  double c0[8];
+  tri_read_chunk<0>(tT, c0);
+  tri_chunks_from<0>(tT, rdv, acc, c0, 0.0);
+  acc[0] *= lane_value(rdv, 0);
 }
 
 // Bounded wait (LDS spin) until *p >= want or the poller gave up.
@@ -321,7 +376,7 @@ __global__ __launch_bounds__(kBsThreads) void backsub_persist_kernel(const T* __
     double acc[kBS];
 #pragma unroll
     for (int i = 0; i < kBS; ++i) acc[i] = m[i * kBS + lane];
-    tri_inv_apply(tT, rd, acc);
+    tri_inv_apply(tT, rd[lane], acc);
     // only this wave touches m: overwrite it in place, swizzled
 #pragma unroll
     for (int i = 0; i < kBS; ++i) m[swz64(i, lane)] = acc[i];

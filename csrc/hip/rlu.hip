@@ -324,7 +324,7 @@ struct Engine {
   template <int J>
   static __device__ __forceinline__ void col(double (&a)[R][kW], bool (&live)[R], int (&pos)[R], Shared& sh,
                                              int t, int lane, int wave, int w, int k0, int* info,
-                                             unsigned long long* cs) {
+                                             unsigned long long* cs, unsigned* pend) {
     if (J >= w) return;  // uniform
     // diagnostics: shader-clock stamps of column 4 (cs != null only when stamping)
     auto mark = [&](int k) {
@@ -426,7 +426,16 @@ struct Engine {
     }
     if (lane == 0) sh.ckey[par][wave] = u32x4{hmax, wlo, wrow, 0u};
     mark(2);
+    // the previous step's multiplier stores (issued > 1 us ago) drain here,
+    // behind this column's barrier, instead of on the engine's path between
+    // steps; its flag follows the barrier
+    if constexpr (J == 1) {
+      if (pend != nullptr) drain();
+    }
     __syncthreads();
+    if constexpr (J == 1) {
+      if (pend != nullptr && t == 0) set_flag(pend);
+    }
     mark(3);
 
     // 3. merge the waves' candidates (lanes 0..7): max high key, exact on ties
@@ -526,8 +535,9 @@ struct Engine {
   template <int... J>
   static __device__ __forceinline__ void factor(double (&a)[R][kW], bool (&live)[R], int (&pos)[R], Shared& sh,
                                                 int t, int lane, int wave, int w, int k0, int* info,
-                                                unsigned long long* cs, std::integer_sequence<int, J...>) {
-    (col<J>(a, live, pos, sh, t, lane, wave, w, k0, info, cs), ...);
+                                                unsigned long long* cs, unsigned* pend,
+                                                std::integer_sequence<int, J...>) {
+    (col<J>(a, live, pos, sh, t, lane, wave, w, k0, info, cs, pend), ...);
   }
 };
 
@@ -553,6 +563,7 @@ __device__ __forceinline__ void engine(const Args& g, Shared& sh) {
   }
   const __amdgpu_buffer_rsrc_t rpiv = rsrc(g.piv, (uint32_t)n * 4);
   const __amdgpu_buffer_rsrc_t rps = rsrc(g.pslot, (uint32_t)np * 128);
+  unsigned* pend = nullptr;  // the previous step's flag, set inside this step's column 1
   for (int j = 0; j < np; ++j) {
     const int k0 = kW * j;
     const int w = min(kW, n - k0);
@@ -563,8 +574,14 @@ __device__ __forceinline__ void engine(const Args& g, Shared& sh) {
     unsigned pre = 1;
     if (more && t == 0) pre = __hip_atomic_load(&g.flags[np + j + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     unsigned long long* cs = (g.stamps != nullptr && j == 10) ? g.stamps + 8 * np + 2 * (np + 1) * np : nullptr;
-    Engine<NT, R, MODE>::factor(a, live, pos, sh, t, lane, wave, w, k0, g.info, cs,
+    Engine<NT, R, MODE>::factor(a, live, pos, sh, t, lane, wave, w, k0, g.info, cs, w >= 2 ? pend : nullptr,
                                 std::make_integer_sequence<int, kW>{});
+    if (w < 2) {  // no column 1 in this (last, narrow) panel: the flag goes now
+      if (pend != nullptr) drain();
+      __syncthreads();
+      if (pend != nullptr && t == 0) set_flag(pend);
+    }
+    pend = nullptr;
     if (more && t == 0) {
       int ok = 1;
       if (pre == 0) {  // not published yet: bounded poll
@@ -680,9 +697,7 @@ __device__ __forceinline__ void engine(const Args& g, Shared& sh) {
       for (int c = 0; c < kW; ++c) a[i][c] = s[c];
     });
     stamp(g, j * 8 + 5);
-    drain();
-    __syncthreads();
-    if (t == 0) set_flag(&g.flags[j]);
+    pend = &g.flags[j];  // drained and set behind column 1 of the next panel
     stamp(g, j * 8 + 6);
   }
 }

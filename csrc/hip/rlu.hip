@@ -245,12 +245,13 @@ __device__ __forceinline__ void rank16_col(double (&s)[kW], const double (&L)[kW
   if (C < ws) {  // uniform (narrow strips: the b column)
     f64x8 u0, u1;
     sload16<C * 128>(ut, s[C > 0 ? C - 1 : 0], u0, u1);
-    double acc = s[C];
+    double a0 = s[C], a1 = 0.0;
 #pragma unroll
-    for (int I = 0; I < 8; ++I) acc = fma(-L[I], u0[I], acc);
-#pragma unroll
-    for (int I = 0; I < 8; ++I) acc = fma(-L[8 + I], u1[I], acc);
-    s[C] = acc;
+    for (int I = 0; I < 8; ++I) {
+      a0 = fma(-L[I], u0[I], a0);
+      a1 = fma(-L[8 + I], u1[I], a1);
+    }
+    s[C] = a0 + a1;
   }
 }
 

@@ -45,6 +45,18 @@ def main():
                                               "dgemm"))
             print(f"dgemm f64 M={M} N={N} K={K}: {dt * 1e6:8.1f} us  {2 * M * N * K / dt * 1e-12:6.1f} TFLOP/s",
                   flush=True)
+    if what in ("f64acc", "all"):
+        # the C read's share: C += A B against C = A B (C not read) at the LU's trailing-update shapes
+        for M, N, K in [(8192, 8192, 256), (8192, 8192, 128), (4096, 4096, 256), (4096, 4096, 128)]:
+            ld = N + 2
+            C = torch.randn(M, ld, dtype=torch.float64, device=dev)
+            A = torch.randn(M, K, dtype=torch.float64, device=dev)
+            B = torch.randn(K, ld, dtype=torch.float64, device=dev)
+            for acc in (1, 0):
+                dt = timeit(lambda: _native.check(lib.gelim_gpu_dgemm_ex(ptr(C), ld, ptr(A), K, ptr(B), ld, M, N, K,
+                                                                         -1.0, acc, 0, sh), "dgemm_ex"))
+                print(f"dgemm f64 M={M} N={N} K={K} accumulate={acc}: {dt * 1e6:8.1f} us  "
+                      f"{2 * M * N * K / dt * 1e-12:6.1f} TFLOP/s", flush=True)
     if what in ("f32", "all"):
         for n in (2048, 4096, 8192, 16384):
             A = torch.randn(n, n, device=dev)

@@ -179,12 +179,17 @@ __global__ void hybrid_perm_kernel(int* __restrict__ perm, int n, int split, int
 }
 
 // outer panel width of the wide-panel engine: 128 under the lookahead
-// schedule up to n = 10240, 256 above it and under the serial schedule
-// (GELIM_BIG_NB = 128 | 256 | 512 overrides).  Measured with lookahead
-// (profiles/big_nb_lookahead.txt): 8192 128 / 256 / 512 -> 34.2 / 34.8 /
-// 41.1 ms; memplus (n = 17758) 169 / 151 ms for 128 / 256; serial 8192:
-// 43.1 / 41.9 / 42.2 ms.
-int64_t big_nb(bool la, int64_t n) { return (la && n <= 10240) ? int64_t(128) : int64_t(256); }
+// schedule up to n = 10240, 256 above it and under the serial schedule, 1024
+// from n = 24576 on.  Measured with lookahead (profiles/big_nb_lookahead.txt):
+// 8192 128 / 256 / 512 -> 34.2 / 34.8 / 41.1 ms; memplus (n = 17758) 169 /
+// 151 ms for 128 / 256; serial 8192: 43.1 / 41.9 / 42.2 ms; round 5, 256 /
+// 512 / 1024: 20480 219.3 / 227.4 / 229.6 ms, 24576 362.5 / 356.5 / 356.1 ms,
+// 32768 845.0 / 797.5 / 785.8 ms (the K = nb trailing updates read and write
+// all of C once per outer panel: 17 GB per update at 32768).
+int64_t big_nb(bool la, int64_t n) {
+  if (n >= 24576) return 1024;
+  return (la && n <= 10240) ? int64_t(128) : int64_t(256);
+}
 constexpr int64_t kBigPairSlot = 1 + 4 * 32 + 3;
 
 int enqueue(gelim_gauss_plan* p, const void* src, int64_t src_ld, void* dx, void* bnorm, hipStream_t s);

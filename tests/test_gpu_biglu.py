@@ -340,6 +340,20 @@ def test_panel_trsm_matches_torch(gelim, cuda, nb, ncols, cap):
     assert torch.equal(Cg.cpu()[:, ncols:], C[:, ncols:])
 
 
+def test_big_solver_1024_outer_panels(gelim, cuda):
+    """n = 24576: the first order on 1024-column outer panels (plan.hip big_nb;
+    K = 1024 trailing updates, profiles/big_nb_lookahead.txt)."""
+    n = 24576
+    aug = gelim.random_system(n, seed=6, device=cuda)
+    s = gelim.GaussSolver(n, backend="hip", device=cuda)
+    x = s.solve(aug, check=True)
+    s.close()
+    ref = torch.linalg.solve(aug[:, :n], aug[:, n].clone())
+    assert ((x - ref).abs().max() / ref.abs().max()).item() < 1e-7
+    del aug, ref
+    torch.cuda.empty_cache()
+
+
 def test_big_solver_past_old_leaf_cap(gelim, cuda):
     """n = 40000 (12.8 GB): past the round-2 cap of 32768 rows per leaf."""
     n = 40000

@@ -659,11 +659,9 @@ __device__ __forceinline__ void panel_body(double* __restrict__ P, int64_t ldp, 
   }
   unsigned long long tr = 0;
   if constexpr (STAMP) tr = stamp_now();
-  // early column stores complete before any fix-up store to the same rows
-  if (Lout != nullptr) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   unsigned long long ta = 0, tb = 0, tc = 0;
   if constexpr (STAMP) ta = stamp_now();
-  __syncthreads();
+  __syncthreads();  // the replay's pos_of / sel are in LDS
   if constexpr (STAMP) tb = stamp_now();
 
   // final position of every physical row
@@ -686,6 +684,11 @@ __device__ __forceinline__ void panel_body(double* __restrict__ P, int64_t ldp, 
   }
   if constexpr (STAMP) tc = stamp_now();
   if (Lout != nullptr) {
+    // every lane's early column stores complete before any fix-up store to
+    // the same rows (another lane's): drained only now, so the destination
+    // computation above ran while the last columns' stores were in flight
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
     // rows that moved overwrite their final position's early store; the
     // rows landing in the top w (U11) also go to P for the back substitution
     const __amdgpu_buffer_rsrc_t urs = dev::buffer_rsrc(P, (uint64_t)W * (uint64_t)ldp * 8);

@@ -532,7 +532,7 @@ __global__ __launch_bounds__(256) void backsub_step_kernel(const T* __restrict__
 
 template <typename T>
 int backsub_impl(const T* U, int64_t ldu, const T* y, int64_t incy, double* x, double* bnorm,
-                 int64_t n, int unit, double* yw, hipStream_t s, const int* perm, int* err) {
+                 int64_t n, int unit, double* yw, hipStream_t s, const int* perm, int* err, bool x_ready) {
   const int64_t nblk = (n + kBS - 1) / kBS;
   // the persistent form needs every block resident (flag hand-offs);
   // checked once per (type, block count)
@@ -543,11 +543,17 @@ int backsub_impl(const T* U, int64_t ldu, const T* y, int64_t incy, double* x, d
               coresident(per, nblk);
   }
   if (persist) {
-    // the error word lives in yw when the caller has none
+    // the error word lives in yw when the caller has none (zeroed here); a
+    // caller's word is the caller's to clear: it may already carry an
+    // upstream code (resident LU abort, row map), which stops this kernel
+    // at its first poll and must reach the host
     int* e = err ? err : reinterpret_cast<int*>(yw);
-    hipLaunchKernelGGL(fill_sent_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s,
-                       reinterpret_cast<uint64_t*>(x), (int)n, e);
-    HIP_TRY(hipGetLastError());
+    if (x_ready && !err) return GELIM_FAIL(GELIM_E_ARG, "backsub: a prefilled x needs the caller's error word");
+    if (!x_ready) {
+      hipLaunchKernelGGL(fill_sent_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s,
+                         reinterpret_cast<uint64_t*>(x), (int)n, err ? nullptr : e);
+      HIP_TRY(hipGetLastError());
+    }
     hipLaunchKernelGGL(backsub_persist_kernel<T>, dim3((unsigned)nblk), dim3(kBsThreads), 0, s, U, ldu, y, incy,
                        perm, x, bnorm, (int)n, unit, e);
     HIP_TRY(hipGetLastError());
@@ -575,14 +581,16 @@ int backsub_impl(const T* U, int64_t ldu, const T* y, int64_t incy, double* x, d
 
 int backsub_f64(const double* U, int64_t ldu, const double* y, int64_t incy, double* x,
                 double* bnorm, int64_t n, int unit, double* yw, hipStream_t s, const int* perm,
-                int* err) {
-  return backsub_impl<double>(U, ldu, y, incy, x, bnorm, n, unit, yw, s, perm, err);
+                int* err, bool x_ready) {
+  return backsub_impl<double>(U, ldu, y, incy, x, bnorm, n, unit, yw, s, perm, err, x_ready);
 }
+
+unsigned backsub_sentinel_word() { return (unsigned)(kXSent & 0xffffffffu); }
 
 int backsub_f32(const float* U, int64_t ldu, const float* y, int64_t incy, double* x,
                 double* bnorm, int64_t n, int unit, double* yw, hipStream_t s, const int* perm,
                 int* err) {
-  return backsub_impl<float>(U, ldu, y, incy, x, bnorm, n, unit, yw, s, perm, err);
+  return backsub_impl<float>(U, ldu, y, incy, x, bnorm, n, unit, yw, s, perm, err, false);
 }
 
 }  // namespace gelim
@@ -593,7 +601,7 @@ extern "C" int gelim_gpu_backsub(const double* dU, int64_t ldu, const double* dy
   hipStream_t s = (hipStream_t)stream;
   double* yw = nullptr;
   HIP_TRY(hipMallocAsync((void**)&yw, sizeof(double) * (n + 2), s));
-  int rc = gelim::backsub_f64(dU, ldu, dy, incy, dx, dbnorm, n, unit, yw, s, nullptr, nullptr);
+  int rc = gelim::backsub_f64(dU, ldu, dy, incy, dx, dbnorm, n, unit, yw, s, nullptr, nullptr, false);
   HIP_TRY(hipFreeAsync(yw, s));
   return rc;
 }

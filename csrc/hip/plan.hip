@@ -31,9 +31,12 @@ int swap_trsm(double* C, int64_t ldc, int64_t ncols, const double* L, int64_t ld
               const int* piv, double* tmp, hipStream_t s);
 int gemm_update(double* C, int64_t ldc, const double* L, int64_t ldl, const double* U,
                 int64_t ldu, int64_t M, int64_t N, int64_t K, hipStream_t s);
+// x_ready: x already holds the hand-off sentinel (backsub_sentinel_word() in
+// both halves of every value) and err is the caller's, cleared by the caller
 int backsub_f64(const double* U, int64_t ldu, const double* y, int64_t incy, double* x,
                 double* bnorm, int64_t n, int unit, double* yw, hipStream_t s,
-                const int* perm = nullptr, int* err = nullptr);
+                const int* perm = nullptr, int* err = nullptr, bool x_ready = false);
+unsigned backsub_sentinel_word();
 int backsub_f32(const float* U, int64_t ldu, const float* y, int64_t incy, double* x,
                 double* bnorm, int64_t n, int unit, double* yw, hipStream_t s,
                 const int* perm = nullptr, int* err = nullptr);
@@ -69,7 +72,11 @@ int64_t rlu_max_n();
 bool rlu_coresident(int64_t n);
 size_t rlu_workspace_bytes(int64_t n);
 int rlu_factor(const double* src, int64_t lds, double* work, int64_t ldw, int64_t n, int mode,
-               int* piv, int* info, void* ws, hipStream_t s, unsigned long long* stamps = nullptr);
+               int* piv, int* info, void* ws, hipStream_t s, unsigned long long* stamps = nullptr,
+               bool flags_ready = false);
+// the hand-off flag words rlu_factor clears before its launch (a caller that
+// clears them in its own prologue passes flags_ready)
+WordFill rlu_flags_fill(int64_t n, void* ws);
 template <typename T>
 int pivot_elimination(T* A, int64_t lda, int64_t n, int mode, T* mcol, int* info, hipStream_t s, int* ipiv,
                       double* diag);
@@ -343,7 +350,16 @@ int enqueue(gelim_gauss_plan* p, const void* src, int64_t src_ld, void* dx, void
   }
   if (src)
     GELIM_TRY(copy2d_async(p->work, lda * p->eb, src, src_ld * p->eb, (n + 1) * p->eb, n, s));
-  GELIM_TRY(zero_async(p->info, 16, s));
+  const bool fused_hyb = p->algo == GELIM_GPU_BLOCKED && p->fused && p->split > 0 && p->split < n;
+  if (fused_hyb) {
+    // one prologue launch: the status words, the resident LU's flags and the
+    // back substitution's sentinel-filled x (each its own launch otherwise)
+    const unsigned sw = backsub_sentinel_word();
+    const WordFill f[3] = {{p->info, 16, 0u}, rlu_flags_fill(n - p->split, p->rws), {dx, sizeof(double) * n, sw}};
+    GELIM_TRY(fill_words_async(f, 3, s));
+  } else {
+    GELIM_TRY(zero_async(p->info, 16, s));
+  }
   if (p->algo == GELIM_GPU_BLOCKED && p->fused) {
     // One fused launch per step (lu_step): workgroup 0 finishes step i-1 on
     // panel i's columns and factors panel i while the other workgroups apply
@@ -389,12 +405,12 @@ int enqueue(gelim_gauss_plan* p, const void* src, int64_t src_ld, void* dx, void
       // substitution over both parts through the merged row map
       const int64_t K = p->split;
       GELIM_TRY(rlu_factor(nullptr, 0, A + K * lda + K, lda, n - K, p->pivot, p->piv + K, p->info + 2,
-                           p->rws, s));
+                           p->rws, s, nullptr, /*flags_ready=*/true));
       hipLaunchKernelGGL(hybrid_perm_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, p->piv,
                          (int)n, (int)K, p->info);
       HIP_TRY(hipGetLastError());
       return backsub_f64(A, lda, A + n, lda, static_cast<double*>(dx), static_cast<double*>(bnorm), n, 0,
-                         p->yw, s, p->piv, p->info + 1);
+                         p->yw, s, p->piv, p->info + 1, /*x_ready=*/true);
     }
     return backsub_f64(A, lda, A + n, lda, static_cast<double*>(dx),
                        static_cast<double*>(bnorm), n, 0, p->yw, s);

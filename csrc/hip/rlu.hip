@@ -881,8 +881,13 @@ size_t rlu_workspace_bytes(int64_t n) {
 // holds it) into work (U rows at their physical positions, y in column n),
 // with the pivot row of every column in piv.  ws: rlu_workspace_bytes(n)
 // bytes of device memory.  info must be zeroed by the caller.
+WordFill rlu_flags_fill(int64_t n, void* ws) {
+  const rlu::Layout L = rlu::layout(n, rlu_threads(n));
+  return WordFill{static_cast<char*>(ws) + L.flags, L.R ? (size_t)(L.lbuf - L.flags) : 0, 0u};
+}
+
 int rlu_factor(const double* src, int64_t lds, double* work, int64_t ldw, int64_t n, int mode,
-               int* piv, int* info, void* ws, hipStream_t s, unsigned long long* stamps) {
+               int* piv, int* info, void* ws, hipStream_t s, unsigned long long* stamps, bool flags_ready) {
   using namespace rlu;
   const Layout L = layout(n, rlu_threads(n));
   if (!L.R) return GELIM_FAIL(GELIM_E_ARG, "rlu: n out of range (1..2048)");
@@ -904,7 +909,7 @@ int rlu_factor(const double* src, int64_t lds, double* work, int64_t ldw, int64_
   a.pslot = reinterpret_cast<int*>(base + L.pslot);
   a.pslot_mode = 1;
   a.stamps = stamps;
-  GELIM_TRY(zero_async(a.flags, L.lbuf - L.flags, s));
+  if (!flags_ready) GELIM_TRY(zero_async(a.flags, L.lbuf - L.flags, s));
   const dim3 grid((unsigned)(L.np + 1)), block((unsigned)L.NT);
   const bool part = mode == GELIM_PIVOT_PARTIAL;
   if (L.R == 1) {
@@ -950,7 +955,7 @@ extern "C" int gelim_debug_rlu_stamps(int64_t n, unsigned long long* out, int64_
   GELIM_TRY(gelim_gpu_init_rhs(A, ld, n, nullptr));
   for (int rep = 0; rep < 2; ++rep) {
     HIP_TRY(hipMemset(info, 0, 16));
-    GELIM_TRY(rlu_factor(A, ld, W, ld, n, GELIM_PIVOT_PARTIAL, piv, info, ws, nullptr, rep ? st : nullptr));
+    GELIM_TRY(rlu_factor(A, ld, W, ld, n, GELIM_PIVOT_PARTIAL, piv, info, ws, nullptr, rep ? st : nullptr, false));
     HIP_TRY(hipDeviceSynchronize());
   }
   HIP_TRY(hipMemcpy(out, st, sizeof(unsigned long long) * need, hipMemcpyDeviceToHost));

@@ -23,6 +23,27 @@ __global__ __launch_bounds__(256) void copy2d_words_kernel(unsigned* __restrict_
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < w; i += (int64_t)gridDim.x * 256) drow[i] = srow[i];
 }
 
+// 8-byte elements (fp64 rows: the solvers' input staging), four per thread in
+// flight, coalesced: 2048 x 2049 in ~6k workgroups instead of ~35k 4-byte ones
+constexpr int kCopyPer = 4;
+__global__ __launch_bounds__(256) void copy2d_u64_kernel(uint64_t* __restrict__ d, int64_t dp,
+                                                         const uint64_t* __restrict__ sp, int64_t spp, int64_t w) {
+  const uint64_t* srow = sp + (int64_t)blockIdx.y * spp;
+  uint64_t* drow = d + (int64_t)blockIdx.y * dp;
+  const int64_t base = (int64_t)blockIdx.x * 256 * kCopyPer + threadIdx.x;
+  uint64_t v[kCopyPer];
+#pragma unroll
+  for (int k = 0; k < kCopyPer; ++k) {
+    const int64_t i = base + 256 * k;
+    v[k] = i < w ? srow[i] : 0;
+  }
+#pragma unroll
+  for (int k = 0; k < kCopyPer; ++k) {
+    const int64_t i = base + 256 * k;
+    if (i < w) drow[i] = v[k];
+  }
+}
+
 // r[i] = aug[i][n] - sum_j aug[i][j] x[j] (fp64; one wave per row); with
 // matvec set, r[i] = sum_j aug[i][j] x[j] (the GMRES products of the mixed
 // engine).  With w, also w[i] = |b_i| + sum_j |a_ij| |x_j| in the same pass
@@ -51,6 +72,19 @@ __global__ __launch_bounds__(256) void residual_kernel(const double* __restrict_
     else r[row] = a[n] - s;
     if (w) w[row] = sa + (matvec ? 0.0 : fabs(a[n]));
   }
+}
+
+struct FillSet {
+  unsigned* p[kMaxFills];
+  int64_t nw[kMaxFills];
+  unsigned v[kMaxFills];
+  int nf;
+};
+
+__global__ __launch_bounds__(256) void fill_words_kernel(FillSet fs) {
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  for (int f = 0; f < fs.nf; ++f)
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < fs.nw[f]; i += stride) fs.p[f][i] = fs.v[f];
 }
 
 __global__ __launch_bounds__(256) void zero_words_kernel(unsigned* __restrict__ p, int64_t nwords) {
@@ -119,13 +153,22 @@ int copy2d_async(void* dst, size_t dpitch, const void* src, size_t spitch, size_
   if (width == 0 || rows == 0) return GELIM_OK;
   if ((width | dpitch | spitch) % 4 || ((uintptr_t)dst | (uintptr_t)src) % 4)
     return GELIM_FAIL(GELIM_E_ARG, "copy2d_async: not 4-byte aligned");
-  const int64_t w = (int64_t)(width / 4);
-  const unsigned bx = (unsigned)std::min<int64_t>((w + 255) / 256, 64);
+  const bool u64 = (width | dpitch | spitch) % 8 == 0 && ((uintptr_t)dst | (uintptr_t)src) % 8 == 0;
   for (size_t r = 0; r < rows; r += 65535) {  // grid.y limit: one launch per 65535 rows
     const size_t nr = std::min<size_t>(65535, rows - r);
-    hipLaunchKernelGGL(copy2d_words_kernel, dim3(bx, (unsigned)nr), dim3(256), 0, s,
-                       static_cast<unsigned*>(dst) + r * (dpitch / 4), (int64_t)(dpitch / 4),
-                       static_cast<const unsigned*>(src) + r * (spitch / 4), (int64_t)(spitch / 4), w);
+    if (u64) {
+      const int64_t w = (int64_t)(width / 8);
+      const unsigned bx = (unsigned)((w + 256 * kCopyPer - 1) / (256 * kCopyPer));
+      hipLaunchKernelGGL(copy2d_u64_kernel, dim3(bx, (unsigned)nr), dim3(256), 0, s,
+                         static_cast<uint64_t*>(dst) + r * (dpitch / 8), (int64_t)(dpitch / 8),
+                         static_cast<const uint64_t*>(src) + r * (spitch / 8), (int64_t)(spitch / 8), w);
+    } else {
+      const int64_t w = (int64_t)(width / 4);
+      const unsigned bx = (unsigned)std::min<int64_t>((w + 255) / 256, 64);
+      hipLaunchKernelGGL(copy2d_words_kernel, dim3(bx, (unsigned)nr), dim3(256), 0, s,
+                         static_cast<unsigned*>(dst) + r * (dpitch / 4), (int64_t)(dpitch / 4),
+                         static_cast<const unsigned*>(src) + r * (spitch / 4), (int64_t)(spitch / 4), w);
+    }
     HIP_TRY(hipGetLastError());
   }
   return GELIM_OK;
@@ -147,6 +190,25 @@ bool coresident(int per_cu, int64_t grid) {
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return false;
   const int64_t usable = per_cu > 1 ? per_cu - 1 : per_cu;
   return usable * (int64_t)cus >= grid;
+}
+
+int fill_words_async(const WordFill* f, int nf, struct ihipStream_t* s) {
+  if (nf < 0 || nf > kMaxFills) return GELIM_FAIL(GELIM_E_ARG, "fill_words_async: too many ranges");
+  FillSet fs{};
+  int64_t most = 0;
+  for (int k = 0; k < nf; ++k) {
+    if (f[k].bytes % 4 || (uintptr_t)f[k].p % 4) return GELIM_FAIL(GELIM_E_ARG, "fill_words_async: not 4-byte aligned");
+    fs.p[fs.nf] = static_cast<unsigned*>(f[k].p);
+    fs.nw[fs.nf] = (int64_t)(f[k].bytes / 4);
+    fs.v[fs.nf] = f[k].value;
+    most = std::max(most, fs.nw[fs.nf]);
+    fs.nf += f[k].bytes ? 1 : 0;
+  }
+  if (!fs.nf) return GELIM_OK;
+  const unsigned blocks = (unsigned)std::min<int64_t>((most + 255) / 256, 1024);
+  hipLaunchKernelGGL(fill_words_kernel, dim3(blocks), dim3(256), 0, s, fs);
+  HIP_TRY(hipGetLastError());
+  return GELIM_OK;
 }
 
 int zero_async(void* p, size_t bytes, struct ihipStream_t* s) {

@@ -30,6 +30,16 @@ bool coresident(int per_cu, int64_t grid);
 // for the same reason (no memcpy nodes in captured graphs).
 int copy2d_async(void* dst, size_t dpitch, const void* src, size_t spitch, size_t width, size_t rows,
                  struct ihipStream_t* s);
+// Up to kMaxFills word ranges set to a 32-bit pattern in ONE launch: a
+// solve's prologue (status words, flag arrays, sentinel-filled outputs)
+// without a launch per buffer.
+struct WordFill {
+  void* p;
+  size_t bytes;  // a multiple of 4
+  unsigned value;
+};
+constexpr int kMaxFills = 4;
+int fill_words_async(const WordFill* f, int nf, struct ihipStream_t* s);
 
 }  // namespace gelim
 

@@ -596,8 +596,10 @@ __global__ __launch_bounds__(kDT) void blk_trsv_split_kernel(const T* __restrict
                                                             const double* __restrict__ Dinv,
                                                             const double* __restrict__ c, double* __restrict__ x,
                                                             double* __restrict__ ysave, double* __restrict__ hpart,
-                                                            int nblk, int K, int* __restrict__ err) {
+                                                            int nblk, int K, int* __restrict__ err,
+                                                            const double* __restrict__ G) {
   __shared__ double part[4][NB];
+  __shared__ double partf[4][NB];
   __shared__ double rb[NB];
   __shared__ int bad;
   const int t = threadIdx.x, r = t & (NB - 1), lane = t & 63;
@@ -676,6 +678,83 @@ __global__ __launch_bounds__(kDT) void blk_trsv_split_kernel(const T* __restrict
                         : 0ull;
     }
   };
+  if (G != nullptr && w > 0) {
+    // x_b = v - G x_{w-1}: v = Dinv_b (c_b - sum_{i < w-1} F_bi x_i) is formed
+    // while x_{w-1} is on its way, and the step after the last hand-off is one
+    // 128 x 128 mat-vec with G = Dinv_b F_{b,w-1} (gprod_kernel) and one
+    // barrier, instead of two mat-vecs and four barriers
+    double gv[kQW];
+    {
+      const double* gp = G + (((int64_t)(UPPER ? 1 : 0) * nblk + b) * NB + r) * NB + kQW * q;
+#pragma unroll
+      for (int j = 0; j < kQW; ++j) gv[j] = gp[j];
+    }
+    if (w >= 2) {
+      load_blk(ua, blk(w - 2));
+      ok = step(ua, issue_x(x, xidx(w - 2)), w - 2, true);
+    }
+    prefetch_h();
+    part[q][r] = acc;
+    if (!ok && lane == 0) bad = 1;
+    __syncthreads();
+    if (bad) return;
+    double y0 = 0.0;
+    if (q == 0) {
+      y0 = cv + part[0][r] + part[1][r] + part[2][r] + part[3][r];
+#pragma unroll
+      for (int hh = 0; hh < kMaxHelpers; ++hh) {
+        if (hh >= K || !ok) break;
+        double hpv = __builtin_bit_cast(double, hb[hh]);
+        if (__ballot(hb[hh] == kSentinel) != 0) ok = settle_own(hpart + ((int64_t)w * K + hh) * NB + r, err, hpv);
+        y0 += hpv;
+      }
+      if (!ok && lane == 0) bad = 1;
+      rb[r] = y0;
+    }
+    __syncthreads();
+    if (bad) return;
+    double xs = 0.0;
+#pragma unroll
+    for (int j = 0; j < kQW; ++j) xs = fma(dv[j], rb[kQW * q + j], xs);
+    __syncthreads();
+    part[q][r] = xs;
+    __syncthreads();
+    const double v = q == 0 ? part[0][r] + part[1][r] + part[2][r] + part[3][r] : 0.0;
+    __syncthreads();  // part is rewritten below
+    double xl;
+    ok = settle_x(x, xidx(w - 1), issue_x(x, xidx(w - 1)), err, xl, false);
+    double s0 = 0.0, s1 = 0.0;
+#pragma unroll
+    for (int j = 0; j < kQW; j += 2) {
+      s0 = fma(gv[j], bcast_lane(xl, j), s0);
+      s1 = fma(gv[j + 1], bcast_lane(xl, j + 1), s1);
+    }
+    part[q][r] = s0 + s1;
+    if (!ok && lane == 0) bad = 1;
+    __syncthreads();
+    if (bad) return;
+    if (q == 0) {
+      double xv = v - (part[0][r] + part[1][r] + part[2][r] + part[3][r]);
+      if (__builtin_bit_cast(unsigned long long, xv) == kSentinel) xv = __builtin_nan("");
+      __hip_atomic_store(reinterpret_cast<unsigned long long*>(x + row), __builtin_bit_cast(unsigned long long, xv),
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (ysave) {
+      // y_b = y0 - F_{b,w-1} x_{w-1} for the backward solve, after the
+      // publish (its F loads stay off the chain)
+      load_blk(ua, blk(w - 1));
+      double f0 = 0.0, f1 = 0.0;
+#pragma unroll
+      for (int j = 0; j < kQW; j += 2) {
+        f0 = fma((double)ua[j], bcast_lane(xl, j), f0);
+        f1 = fma((double)ua[j + 1], bcast_lane(xl, j + 1), f1);
+      }
+      partf[q][r] = f0 + f1;
+      __syncthreads();
+      if (q == 0) ysave[row] = y0 - (partf[0][r] + partf[1][r] + partf[2][r] + partf[3][r]);
+    }
+    return;
+  }
   // the last kChainOwn (= 2) blocks, in chain order
   if (own0 + 1 < w) {
     load_blk(ua, blk(own0));
@@ -724,6 +803,45 @@ __global__ __launch_bounds__(kDT) void blk_trsv_split_kernel(const T* __restrict
     __hip_atomic_store(reinterpret_cast<unsigned long long*>(x + row), __builtin_bit_cast(unsigned long long, xv),
                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
+}
+
+// G[d][b] = Dinv_b F_{b,b-1} (d = 0, the forward solve's last block) and
+// Dinv_b F_{b,b+1} (d = 1, the backward solve's), row-major 128 x 128, on
+// the fp64 matrix cores: 4 waves of 64 x 64 (4 x 4 v_mfma_f64_16x16x4f64
+// blocks), operands straight from L2 (one launch per factorisation).
+__global__ __launch_bounds__(256) void gprod_kernel(const double* __restrict__ F, int64_t ldf,
+                                                    const double* __restrict__ Dinv, double* __restrict__ G,
+                                                    int nblk) {
+  const int b = blockIdx.x, d = blockIdx.y;
+  const int nb = d == 0 ? b - 1 : b + 1;
+  if (nb < 0 || nb >= nblk) return;
+  const double* A = Dinv + (int64_t)b * NB * NB;
+  const double* B = F + (int64_t)b * NB * ldf + (int64_t)nb * NB;
+  double* C = G + ((int64_t)d * nblk + b) * NB * NB;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64, r16 = lane & 15, q = lane >> 4;
+  dev::d4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = dev::d4{0.0, 0.0, 0.0, 0.0};
+  for (int k0 = 0; k0 < NB; k0 += 4) {
+    double af[4], bf[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) af[i] = A[(wm + 16 * i + r16) * NB + k0 + q];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bf[j] = B[(int64_t)(k0 + q) * ldf + wn + 16 * j + r16];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[i], bf[j], acc[i][j], 0, 0, 0);
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) C[(wm + 16 * i + q + 4 * r) * NB + wn + 16 * j + r16] = acc[i][j][r];
 }
 
 __global__ __launch_bounds__(256) void fill_sentinel2_kernel(unsigned long long* __restrict__ a, int na,
@@ -849,7 +967,7 @@ constexpr int kNotResident = 1;
 
 template <typename T>
 int solve_impl(const T* M, int64_t ldm, int64_t np, const double* Dinv, const double* c, double* z, double* y,
-               double* x, unsigned* flags, hipStream_t s, double* hp = nullptr) {
+               double* x, unsigned* flags, hipStream_t s, double* hp = nullptr, const double* G = nullptr) {
   const int nblk = (int)(np / NB);
   // the split form (blk_trsv_split_kernel) when its grid of nblk (K + 1)
   // workgroups fits at once, with as many helpers per block row as fit
@@ -877,7 +995,7 @@ int solve_impl(const T* M, int64_t ldm, int64_t np, const double* Dinv, const do
     HIP_TRY(hipGetLastError());
     const unsigned grid = (unsigned)(nblk * (K + 1));
     hipLaunchKernelGGL((blk_trsv_split_kernel<T, false>), dim3(grid), dim3(kDT), 0, s, M, ldm, Dinv, c, z, y, hp,
-                       nblk, K, err);
+                       nblk, K, err, G);
     HIP_TRY(hipGetLastError());
     if (alias) {
       hipLaunchKernelGGL(fill_sentinel_kernel, dim3((unsigned)((np + 255) / 256)), dim3(256), 0, s,
@@ -885,7 +1003,7 @@ int solve_impl(const T* M, int64_t ldm, int64_t np, const double* Dinv, const do
       HIP_TRY(hipGetLastError());
     }
     hipLaunchKernelGGL((blk_trsv_split_kernel<T, true>), dim3(grid), dim3(kDT), 0, s, M, ldm, Dinv, y, x,
-                       (double*)nullptr, hp + nh, nblk, K, err);
+                       (double*)nullptr, hp + nh, nblk, K, err, G);
     HIP_TRY(hipGetLastError());
     return GELIM_OK;
   }
@@ -940,6 +1058,7 @@ struct gelim_mixed_plan {
   double* vd = nullptr;     // V's
   unsigned* flags = nullptr;  // [0]: the solves' error word
   double* hp = nullptr;       // split solves' helper partials (2 x kMaxBlocks x kMaxHelpers x NB)
+  double* G = nullptr;        // 2 x nblk x NB x NB: Dinv_b F_{b,b-1}, Dinv_b F_{b,b+1} (gprod_kernel)
   double* c = nullptr;      // U^T r (np)
   double* y = nullptr;      // L^-1 c (np)
   double* z = nullptr;      // U^-1 y (np)
@@ -962,7 +1081,7 @@ extern "C" void gelim_mixed_plan_destroy(gelim_mixed_plan* p) {
   if (!p) return;
   for (void* q : {(void*)p->M, (void*)p->Dinv, (void*)p->W, (void*)p->ud, (void*)p->vd,
                   (void*)p->rv, (void*)p->wv, (void*)p->dv, (void*)p->xb, (void*)p->om, (void*)p->flags, (void*)p->c,
-                  (void*)p->y, (void*)p->z, (void*)p->xs, (void*)p->info, (void*)p->hp})
+                  (void*)p->y, (void*)p->z, (void*)p->xs, (void*)p->info, (void*)p->hp, (void*)p->G})
     (void)hipFree(q);
   if (p->e0) (void)hipEventDestroy(p->e0);
   if (p->e1) (void)hipEventDestroy(p->e1);
@@ -1025,6 +1144,7 @@ extern "C" gelim_mixed_plan* gelim_mixed_plan_create2(int64_t n, const double* u
   if (hipMalloc((void**)&p->hp, sizeof(double) * 2 * gelim::kMaxBlocks * gelim::kMaxHelpers * gelim::NB) !=
       hipSuccess)
     return fail("helper partials");
+  if (hipMalloc((void**)&p->G, 2 * sizeof(double) * (size_t)np * gelim::NB) != hipSuccess) return fail("G blocks");
   if (hipMalloc((void**)&p->info, 16) != hipSuccess) return fail("info");
   for (double** b : {&p->rv, &p->wv, &p->dv, &p->xb})
     if (hipMalloc((void**)b, sizeof(double) * (size_t)n) != hipSuccess) return fail("refinement vectors");
@@ -1056,6 +1176,12 @@ extern "C" int gelim_mixed_factor(gelim_mixed_plan* p, const double* aug, int64_
     GELIM_TRY(factor_la2(p->M, ldm, np, p->Dinv, p->W, p->info, s, p->side, p->e0, p->e1));
   else
     GELIM_TRY(factor_impl(p->M, ldm, np, p->Dinv, p->W, p->info, s));
+  // the solves' last-block products (split solves only read them)
+  if (np > NB) {
+    hipLaunchKernelGGL(gprod_kernel, dim3((unsigned)(np / NB), 2), dim3(256), 0, s, p->M, ldm, p->Dinv, p->G,
+                       (int)(np / NB));
+    HIP_TRY(hipGetLastError());
+  }
   int h_info = 0;
   HIP_TRY(hipMemcpyAsync(&h_info, p->info, 4, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
@@ -1073,7 +1199,8 @@ extern "C" int gelim_mixed_apply(gelim_mixed_plan* p, const double* r, int64_t i
   hipLaunchKernelGGL(rbt_vec_kernel, dim3(g), dim3(256), 0, s, r, incr, (int)p->n, (int)np, p->ud, 1, p->c, (int)np);
   HIP_TRY(hipGetLastError());
   // c -> z (scratch), y (block-unit-lower result) -> xs (the solution of the transformed system)
-  const int rc = solve_impl<double>(p->M, p->ldm, np, p->Dinv, p->c, p->z, p->y, p->xs, p->flags, s, p->hp);
+  const int rc = solve_impl<double>(p->M, p->ldm, np, p->Dinv, p->c, p->z, p->y, p->xs, p->flags, s, p->hp,
+                                    np > NB ? p->G : nullptr);
   if (rc != GELIM_OK) return rc;  // < 0: error; kNotResident: the caller falls back
   // x = V xs, only the first n entries are kept (the padding's are zero in exact arithmetic)
   hipLaunchKernelGGL(rbt_vec_kernel, dim3(g), dim3(256), 0, s, p->xs, (int64_t)1, (int)np, (int)np, p->vd, 0, d,

@@ -597,9 +597,9 @@ __global__ __launch_bounds__(kDT) void blk_trsv_split_kernel(const T* __restrict
                                                             const double* __restrict__ c, double* __restrict__ x,
                                                             double* __restrict__ ysave, double* __restrict__ hpart,
                                                             int nblk, int K, int* __restrict__ err,
-                                                            const double* __restrict__ G) {
+                                                            const double* __restrict__ G,
+                                                            const double* __restrict__ zlast) {
   __shared__ double part[4][NB];
-  __shared__ double partf[4][NB];
   __shared__ double rb[NB];
   __shared__ int bad;
   const int t = threadIdx.x, r = t & (NB - 1), lane = t & 63;
@@ -662,6 +662,22 @@ __global__ __launch_bounds__(kDT) void blk_trsv_split_kernel(const T* __restrict
     for (int j = 0; j < kQW; ++j) dv[j] = d[j];
   }
   double cv = c[row];
+  if (zlast != nullptr && b > 0) {
+    // the forward solve (G form) left y_b without its last block's product:
+    // c_b -= F_{b,b-1} z_{b-1}, formed here while this row waits its turn
+    load_blk(ua, F + (int64_t)row * ldf + (int64_t)(b - 1) * NB + kQW * q);
+    const double* zp = zlast + (int64_t)(b - 1) * NB + kQW * q;
+    double f0 = 0.0, f1 = 0.0;
+#pragma unroll
+    for (int j = 0; j < kQW; j += 2) {
+      f0 = fma((double)ua[j], zp[j], f0);
+      f1 = fma((double)ua[j + 1], zp[j + 1], f1);
+    }
+    part[q][r] = f0 + f1;
+    __syncthreads();
+    cv -= part[0][r] + part[1][r] + part[2][r] + part[3][r];
+    __syncthreads();  // part is reused below
+  }
 #pragma unroll
   for (int j = 0; j < kQW; ++j) asm volatile("" : "+v"(dv[j]));
   asm volatile("" : "+v"(cv));
@@ -710,6 +726,9 @@ __global__ __launch_bounds__(kDT) void blk_trsv_split_kernel(const T* __restrict
       }
       if (!ok && lane == 0) bad = 1;
       rb[r] = y0;
+      // the forward solve keeps y_b less its last product (the backward
+      // solve's chain adds F_{b,b-1} z_{b-1} itself: zlast)
+      if (ysave) ysave[row] = y0;
     }
     __syncthreads();
     if (bad) return;
@@ -738,20 +757,6 @@ __global__ __launch_bounds__(kDT) void blk_trsv_split_kernel(const T* __restrict
       if (__builtin_bit_cast(unsigned long long, xv) == kSentinel) xv = __builtin_nan("");
       __hip_atomic_store(reinterpret_cast<unsigned long long*>(x + row), __builtin_bit_cast(unsigned long long, xv),
                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    if (ysave) {
-      // y_b = y0 - F_{b,w-1} x_{w-1} for the backward solve, after the
-      // publish (its F loads stay off the chain)
-      load_blk(ua, blk(w - 1));
-      double f0 = 0.0, f1 = 0.0;
-#pragma unroll
-      for (int j = 0; j < kQW; j += 2) {
-        f0 = fma((double)ua[j], bcast_lane(xl, j), f0);
-        f1 = fma((double)ua[j + 1], bcast_lane(xl, j + 1), f1);
-      }
-      partf[q][r] = f0 + f1;
-      __syncthreads();
-      if (q == 0) ysave[row] = y0 - (partf[0][r] + partf[1][r] + partf[2][r] + partf[3][r]);
     }
     return;
   }
@@ -995,7 +1000,7 @@ int solve_impl(const T* M, int64_t ldm, int64_t np, const double* Dinv, const do
     HIP_TRY(hipGetLastError());
     const unsigned grid = (unsigned)(nblk * (K + 1));
     hipLaunchKernelGGL((blk_trsv_split_kernel<T, false>), dim3(grid), dim3(kDT), 0, s, M, ldm, Dinv, c, z, y, hp,
-                       nblk, K, err, G);
+                       nblk, K, err, G, (const double*)nullptr);
     HIP_TRY(hipGetLastError());
     if (alias) {
       hipLaunchKernelGGL(fill_sentinel_kernel, dim3((unsigned)((np + 255) / 256)), dim3(256), 0, s,
@@ -1003,7 +1008,7 @@ int solve_impl(const T* M, int64_t ldm, int64_t np, const double* Dinv, const do
       HIP_TRY(hipGetLastError());
     }
     hipLaunchKernelGGL((blk_trsv_split_kernel<T, true>), dim3(grid), dim3(kDT), 0, s, M, ldm, Dinv, y, x,
-                       (double*)nullptr, hp + nh, nblk, K, err, G);
+                       (double*)nullptr, hp + nh, nblk, K, err, G, G ? (const double*)z : nullptr);
     HIP_TRY(hipGetLastError());
     return GELIM_OK;
   }

@@ -166,8 +166,12 @@ template <bool FULL, int T = 128>
 __device__ __forceinline__ void tile_body(const Args& g, int m0, int n0, double* lds, int t, bool store = true) {
   using G = Geo<T>;
   constexpr int SA = G::SA, SB = G::SB, WM = G::WM, WN = G::WN, MB = G::MB, NB = G::NB;
-  double* As[2] = {lds, lds + BK * SA};
-  double* Bs[2] = {lds + 2 * BK * SA, lds + 2 * BK * SA + BK * SB};
+  // stage b of the double buffer as offsets from lds (an array of the two
+  // pointers indexed at run time lost the LDS address space: every fragment
+  // read became a flat load counted in vmcnt, so each k-tile's first wait
+  // also drained the next tile's global prefetch)
+  auto As = [&](int b) { return lds + b * (BK * SA); };
+  auto Bs = [&](int b) { return lds + 2 * BK * SA + b * (BK * SB); };
   const int lane = t & 63, wave = t >> 6;
   const int wm = (wave >> 1) * WM, wn = (wave & 1) * WN;
   const int r16 = lane & 15, q = lane >> 4;
@@ -191,14 +195,14 @@ __device__ __forceinline__ void tile_body(const Args& g, int m0, int n0, double*
       }
     }
 
-  store_stage<T>(st, As[0], Bs[0], g.alpha, t);
+  store_stage<T>(st, As(0), Bs(0), g.alpha, t);
   __syncthreads();
   const int nk = (g.K + BK - 1) / BK;
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
     if (kt + 1 < nk) load_stage<FULL, T>(st, g, m0, n0, (kt + 1) * BK, t);
-    const double* a_s = As[cur] + wm;
-    const double* b_s = Bs[cur] + wn + r16;
+    const double* a_s = As(cur) + wm;
+    const double* b_s = Bs(cur) + wn + r16;
 #pragma unroll
     for (int kk = 0; kk < BK; kk += 4) {
       const int k = kk + q;
@@ -214,7 +218,7 @@ __device__ __forceinline__ void tile_body(const Args& g, int m0, int n0, double*
         for (int j = 0; j < NB; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[i], bf[j], acc[i][j], 0, 0, 0);
     }
-    if (kt + 1 < nk) store_stage<T>(st, As[cur ^ 1], Bs[cur ^ 1], g.alpha, t);
+    if (kt + 1 < nk) store_stage<T>(st, As(cur ^ 1), Bs(cur ^ 1), g.alpha, t);
     __syncthreads();
   }
 

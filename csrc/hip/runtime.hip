@@ -24,23 +24,29 @@ __global__ __launch_bounds__(256) void copy2d_words_kernel(unsigned* __restrict_
 }
 
 // 8-byte elements (fp64 rows: the solvers' input staging), four per thread in
-// flight, coalesced: 2048 x 2049 in ~6k workgroups instead of ~35k 4-byte ones
+// flight, coalesced; rows grid-strided so a large copy is a few thousand
+// workgroups, not one per (row, 1024 columns): 8192 x 8193 was dispatch-bound
+// at 2.4 TB/s with 74k workgroups
 constexpr int kCopyPer = 4;
+constexpr int kCopyRowsGrid = 1024;
 __global__ __launch_bounds__(256) void copy2d_u64_kernel(uint64_t* __restrict__ d, int64_t dp,
-                                                         const uint64_t* __restrict__ sp, int64_t spp, int64_t w) {
-  const uint64_t* srow = sp + (int64_t)blockIdx.y * spp;
-  uint64_t* drow = d + (int64_t)blockIdx.y * dp;
+                                                         const uint64_t* __restrict__ sp, int64_t spp, int64_t w,
+                                                         int64_t rows) {
   const int64_t base = (int64_t)blockIdx.x * 256 * kCopyPer + threadIdx.x;
-  uint64_t v[kCopyPer];
+  for (int64_t r = blockIdx.y; r < rows; r += gridDim.y) {
+    const uint64_t* srow = sp + r * spp;
+    uint64_t* drow = d + r * dp;
+    uint64_t v[kCopyPer];
 #pragma unroll
-  for (int k = 0; k < kCopyPer; ++k) {
-    const int64_t i = base + 256 * k;
-    v[k] = i < w ? srow[i] : 0;
-  }
+    for (int k = 0; k < kCopyPer; ++k) {
+      const int64_t i = base + 256 * k;
+      v[k] = i < w ? srow[i] : 0;
+    }
 #pragma unroll
-  for (int k = 0; k < kCopyPer; ++k) {
-    const int64_t i = base + 256 * k;
-    if (i < w) drow[i] = v[k];
+    for (int k = 0; k < kCopyPer; ++k) {
+      const int64_t i = base + 256 * k;
+      if (i < w) drow[i] = v[k];
+    }
   }
 }
 
@@ -154,15 +160,19 @@ int copy2d_async(void* dst, size_t dpitch, const void* src, size_t spitch, size_
   if ((width | dpitch | spitch) % 4 || ((uintptr_t)dst | (uintptr_t)src) % 4)
     return GELIM_FAIL(GELIM_E_ARG, "copy2d_async: not 4-byte aligned");
   const bool u64 = (width | dpitch | spitch) % 8 == 0 && ((uintptr_t)dst | (uintptr_t)src) % 8 == 0;
+  if (u64) {
+    const int64_t w = (int64_t)(width / 8);
+    const unsigned bx = (unsigned)((w + 256 * kCopyPer - 1) / (256 * kCopyPer));
+    const unsigned by = (unsigned)std::min<size_t>(rows, kCopyRowsGrid);
+    hipLaunchKernelGGL(copy2d_u64_kernel, dim3(bx, by), dim3(256), 0, s, static_cast<uint64_t*>(dst),
+                       (int64_t)(dpitch / 8), static_cast<const uint64_t*>(src), (int64_t)(spitch / 8), w,
+                       (int64_t)rows);
+    HIP_TRY(hipGetLastError());
+    return GELIM_OK;
+  }
   for (size_t r = 0; r < rows; r += 65535) {  // grid.y limit: one launch per 65535 rows
     const size_t nr = std::min<size_t>(65535, rows - r);
-    if (u64) {
-      const int64_t w = (int64_t)(width / 8);
-      const unsigned bx = (unsigned)((w + 256 * kCopyPer - 1) / (256 * kCopyPer));
-      hipLaunchKernelGGL(copy2d_u64_kernel, dim3(bx, (unsigned)nr), dim3(256), 0, s,
-                         static_cast<uint64_t*>(dst) + r * (dpitch / 8), (int64_t)(dpitch / 8),
-                         static_cast<const uint64_t*>(src) + r * (spitch / 8), (int64_t)(spitch / 8), w);
-    } else {
+    {
       const int64_t w = (int64_t)(width / 4);
       const unsigned bx = (unsigned)std::min<int64_t>((w + 255) / 256, 64);
       hipLaunchKernelGGL(copy2d_words_kernel, dim3(bx, (unsigned)nr), dim3(256), 0, s,

@@ -254,6 +254,29 @@ __global__ __launch_bounds__(kThreads, 2) void dgemm_kernel(Args g) {
     tile_body<false, T>(g, m0, n0, lds, threadIdx.x);
 }
 
+// Two independent products in ONE launch (the block-LDU engine's pairs of
+// thin updates on its critical stream: a block column and a block row that
+// read the same operands and write disjoint parts of the matrix): tiles
+// [0, g1.ntiles) are g1's, the rest g2's, dealt to XCDs as one range.
+template <int T>
+__global__ __launch_bounds__(kThreads, 2) void dgemm2_kernel(Args g1, Args g2) {
+  __shared__ __attribute__((aligned(16))) double lds[Geo<T>::kLds];
+  const int total = g1.ntiles + g2.ntiles;
+  const int orig = blockIdx.x;
+  const int q = total / 8, rem = total % 8, xcd = orig % 8;
+  const int t0 = (xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q) + orig / 8;
+  const bool second = t0 >= g1.ntiles;
+  const Args g = second ? g2 : g1;
+  const int tile = second ? t0 - g1.ntiles : t0;
+  int tr, tc;
+  tile_coords(g, tile, tr, tc);
+  const int m0 = tr * T, n0 = tc * T;
+  if (m0 + T <= g.M && n0 + T <= g.N && (g.K % BK) == 0)
+    tile_body<true, T>(g, m0, n0, lds, threadIdx.x);
+  else
+    tile_body<false, T>(g, m0, n0, lds, threadIdx.x);
+}
+
 // Persistent form for a grid capped below the CU count (the lookahead side
 // stream of plan.hip enqueue_big, which must leave CUs free for the leaf
 // chain): 512 threads = two tile engines (2 waves per SIMD, as two of the
@@ -366,6 +389,45 @@ int dgemm(double* C, int64_t ldc, const double* A, int64_t lda, const double* B,
 int dgemm_ex(double* C, int64_t ldc, const double* A, int64_t lda, const double* B, int64_t ldb, int64_t M,
              int64_t N, int64_t K, double alpha, int accumulate, hipStream_t s) {
   return dgemm_capped(C, ldc, A, lda, B, ldb, M, N, K, alpha, 0, s, accumulate);
+}
+
+// Two independent C += alpha A B products (same alpha / accumulate) in one
+// launch (dgemm2_kernel); either may be empty.  Same operand contract as
+// dgemm_launch.
+int dgemm_pair(const GemmOp& p1, const GemmOp& p2, double alpha, int accumulate, hipStream_t s) {
+  const GemmOp* ops[2] = {&p1, &p2};
+  for (const GemmOp* o : ops) {
+    if (o->M <= 0 || o->N <= 0 || o->K <= 0) continue;
+    if (o->M > INT32_MAX || o->N > INT32_MAX || o->K > INT32_MAX)
+      return GELIM_FAIL(GELIM_E_ARG, "dgemm_pair: dimension > 2^31");
+    if ((o->K & 1) || (o->lda & 1) || (o->ldb & 1) || (((uintptr_t)o->A | (uintptr_t)o->B) & 15) ||
+        ((o->N & 1) && o->ldb <= o->N) || o->lda < o->K || o->ldb < o->N || o->ldc < o->N)
+      return GELIM_FAIL(GELIM_E_ARG, "dgemm_pair: unsupported alignment / leading dimensions");
+  }
+  const bool e1 = p1.M <= 0 || p1.N <= 0 || p1.K <= 0, e2 = p2.M <= 0 || p2.N <= 0 || p2.K <= 0;
+  if (e1 && e2) return GELIM_OK;
+  if (e1) return dgemm_ex(p2.C, p2.ldc, p2.A, p2.lda, p2.B, p2.ldb, p2.M, p2.N, p2.K, alpha, accumulate, s);
+  if (e2) return dgemm_ex(p1.C, p1.ldc, p1.A, p1.lda, p1.B, p1.ldb, p1.M, p1.N, p1.K, alpha, accumulate, s);
+  static const int ncu = [] {
+    int dev = 0, cus = 256;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    return cus;
+  }();
+  auto args = [&](const GemmOp& o, int T) {
+    const int tm = (int)((o.M + T - 1) / T), tn = (int)((o.N + T - 1) / T);
+    return Args{o.C, o.ldc, o.A, o.lda, o.B, o.ldb, (int)o.M, (int)o.N, (int)o.K, tn, tm * tn, alpha,
+                accumulate ? 1 : 0, 1};
+  };
+  const Args a1 = args(p1, 128), a2 = args(p2, 128);
+  if ((int64_t)a1.ntiles + a2.ntiles < (int64_t)ncu) {  // thin: 64-tiles, as dgemm_launch
+    const Args b1 = args(p1, 64), b2 = args(p2, 64);
+    hipLaunchKernelGGL(dgemm2_kernel<64>, dim3((unsigned)(b1.ntiles + b2.ntiles)), dim3(kThreads), 0, s, b1, b2);
+  } else {
+    hipLaunchKernelGGL(dgemm2_kernel<128>, dim3((unsigned)(a1.ntiles + a2.ntiles)), dim3(kThreads), 0, s, a1, a2);
+  }
+  HIP_TRY(hipGetLastError());
+  return GELIM_OK;
 }
 
 }  // namespace gelim

@@ -925,11 +925,12 @@ int factor_la2(double* M, int64_t ldm, int64_t np, double* Dinv, double* W4, int
     double* Wp = W4 + (pair & 1) * 2 * NB * np;    // 2 NB rows, ld r1
     double* Ak = M + (k0 + NB) * ldm + k0;         // A[k+1:, k]
     GELIM_TRY(dgemm_ex(Wp, r1, Dinv + k * NB * NB, NB, M + k0 * ldm + k0 + NB, ldm, NB, r1, NB, 1.0, 0, s));
-    // step k on block k+1: its column (rows k+1..), its row (columns k+2..)
-    GELIM_TRY(dgemm_ex(M + (k0 + NB) * ldm + k0 + NB, ldm, Ak, ldm, Wp, r1, r1, NB, NB, -1.0, 1, s));
+    // step k on block k+1: its column (rows k+1..), its row (columns k+2..),
+    // one launch (disjoint outputs, shared operands)
     const int64_t r2 = r1 - NB;  // columns right of block k+1
-    if (r2 > 0)
-      GELIM_TRY(dgemm_ex(M + (k0 + NB) * ldm + k0 + 2 * NB, ldm, Ak, ldm, Wp + NB, r1, NB, r2, NB, -1.0, 1, s));
+    GELIM_TRY(dgemm_pair(GemmOp{M + (k0 + NB) * ldm + k0 + NB, ldm, Ak, ldm, Wp, r1, r1, NB, NB},
+                         GemmOp{M + (k0 + NB) * ldm + k0 + 2 * NB, ldm, Ak, ldm, Wp + NB, r1, r2 > 0 ? NB : 0, r2, NB},
+                         -1.0, 1, s));
     GELIM_TRY(diag_inv(M, ldm, k0 + NB, Dinv + (k + 1) * NB * NB, info, s));
     if (r2 <= 0) break;  // block k+1 was the last
     GELIM_TRY(dgemm_ex(Wp + NB * r1 + NB, r1, Dinv + (k + 1) * NB * NB, NB, M + (k0 + NB) * ldm + k0 + 2 * NB, ldm,
@@ -940,10 +941,12 @@ int factor_la2(double* M, int64_t ldm, int64_t np, double* Dinv, double* W4, int
     const int64_t pw = std::min<int64_t>(2 * NB, r2);   // panel width
     const int64_t r4 = r2 - pw;                        // columns right of the panel
     double* A2 = M + (k0 + 2 * NB) * ldm + k0;         // A[k+2:, k:k+2]
-    GELIM_TRY(dgemm_ex(M + (k0 + 2 * NB) * ldm + k0 + 2 * NB, ldm, A2, ldm, Wp + NB, r1, r2, pw, 2 * NB, -1.0, 1, s));
-    if (r4 > 0) {
-      GELIM_TRY(dgemm_ex(M + (k0 + 2 * NB) * ldm + k0 + 2 * NB + pw, ldm, A2, ldm, Wp + NB + pw, r1, pw, r4, 2 * NB,
+    // the panel's block columns and block rows: one launch
+    GELIM_TRY(dgemm_pair(GemmOp{M + (k0 + 2 * NB) * ldm + k0 + 2 * NB, ldm, A2, ldm, Wp + NB, r1, r2, pw, 2 * NB},
+                         GemmOp{M + (k0 + 2 * NB) * ldm + k0 + 2 * NB + pw, ldm, A2, ldm, Wp + NB + pw, r1,
+                                r4 > 0 ? pw : 0, r4, 2 * NB},
                          -1.0, 1, s));
+    if (r4 > 0) {
       HIP_TRY(hipEventRecord(e0, s));
       HIP_TRY(hipStreamWaitEvent(side, e0, 0));
       GELIM_TRY(dgemm_ex(M + (k0 + 2 * NB + pw) * ldm + k0 + 2 * NB + pw, ldm, M + (k0 + 2 * NB + pw) * ldm + k0, ldm,

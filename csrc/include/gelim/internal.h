@@ -39,6 +39,18 @@ struct WordFill {
   unsigned value;
 };
 constexpr int kMaxFills = 4;
+// One row-major fp64 product C (M x N, ldc) += alpha A (M x K) B (K x N) of a
+// grouped launch (dgemm.hip dgemm_pair: two independent products, one grid)
+struct GemmOp {
+  double* C;
+  int64_t ldc;
+  const double* A;
+  int64_t lda;
+  const double* B;
+  int64_t ldb;
+  int64_t M, N, K;
+};
+int dgemm_pair(const GemmOp& p1, const GemmOp& p2, double alpha, int accumulate, struct ihipStream_t* s);
 int fill_words_async(const WordFill* f, int nf, struct ihipStream_t* s);
 
 }  // namespace gelim

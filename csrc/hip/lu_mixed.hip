@@ -1128,14 +1128,14 @@ extern "C" gelim_mixed_plan* gelim_mixed_plan_create2(int64_t n, const double* u
   if (hipMalloc((void**)&p->M, sizeof(double) * (size_t)np * p->ldm) != hipSuccess) return fail("matrix");
   if (hipMalloc((void**)&p->Dinv, sizeof(double) * (size_t)np * gelim::NB) != hipSuccess) return fail("inverses");
   if (hipMalloc((void**)&p->W, 4 * sizeof(double) * (size_t)np * gelim::NB) != hipSuccess) return fail("W buffer");
-  // lookahead from 32 blocks (n = 4096): below it the side stream's share is
-  // too small to pay for the cross-stream waits (2048: 2.04 vs 1.76 ms,
-  // profiles/rbt_trace_8192_r4.txt).  The side GEMMs run on an uncapped grid
+  // lookahead from 24 blocks (n = 3072; round 5, with the grouped critical
+  // GEMMs: 3072 2.72 vs 2.83 ms, 2048 1.70 vs 1.65, trsv_split_r5.txt): below
+  // it the side stream's share is too small to pay for the cross-stream waits.  The side GEMMs run on an uncapped grid
   // (8192 15.0 ms vs 18.7 with 64 CUs reserved for the chain); CU masks,
   // stream priorities, a third stream for the updates the next inverse does
   // not read, and one-block (instead of pair) lookahead were all measured
   // slower in rounds 3-4 (profiles/rbt_engine_round3.txt, stream_prio_r4.txt).
-  p->lookahead = np >= 4096;
+  p->lookahead = np >= 3072;
   if (p->lookahead) {
     if (gelim::side_stream_create(&p->side) != GELIM_OK) return fail("side stream");
     if (hipEventCreateWithFlags(&p->e0, hipEventDisableTiming) != hipSuccess) return fail("event");

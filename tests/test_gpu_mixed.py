@@ -33,13 +33,13 @@ def test_fp32_factor_engine_is_gone(gelim, cuda):
     assert "removed" in gelim._native.last_error()
 
 
-@pytest.mark.parametrize("n", [130, 1000, 4200])
+@pytest.mark.parametrize("n", [130, 1000, 3000, 4200])
 def test_diag_inverses_and_factor(gelim, cuda, n):
     """Every stored diagonal-block inverse (Gauss-Jordan, fp64, two steps per
     barrier) inverts the Schur diagonal block the block-LDU factor left in
-    place -- without lookahead (< 4096) and with the pair lookahead on two
-    streams (4200 = 33 blocks: the pair loop ends on a single block); fp64
-    oracle."""
+    place -- without lookahead (padded order < 3072) and with the pair
+    lookahead on two streams (3000 -> 24 blocks, an even count; 4200 = 33
+    blocks: the pair loop ends on a single block); fp64 oracle."""
     import ctypes
 
     aug = gelim.random_system(n, seed=3, device=cuda)

@@ -25,6 +25,9 @@ between device syncs + barriers, max over ranks):
   dist_gauss_8192_rbt(_s) the same system over ALL N ranks on the randomised
                         block-LDU engine (no pivot chain; parallel/dist_rbt.py)
   dist_gauss_2048(_s)   the headline's 2048^2 system over ALL N ranks (strong)
+  dist_gauss_32768(_s)  ONE 32768^2 system over ALL N ranks, partial pivoting
+                        (strong; the trailing update dominates at this size)
+  dist_rbt_16384(_s)    ONE 16384^2 system over ALL N ranks, randomised engine
   dist_matmul_16384(_s) 16384^2 fp32 over ALL N ranks (strong scaling)
   gauss_8192_1gpu(_s)   one 8192^2 system per GPU on the single-GPU solver
   hip_pivot_2048        the per-pivot algorithm (fp64, fp32)
@@ -74,6 +77,10 @@ def parse():
     p.add_argument("--budget", type=float, default=400.0,
                    help="seconds the sections after the headline may take before the line is printed without "
                         "the missing ones (a hung collective never costs the headline)")
+    p.add_argument("--hang-exit-code", type=int, default=0,
+                   help="exit status when the budget watchdog fires after a complete headline (the JSON line then "
+                        "carries a 'watchdog' field and stderr says which sections hung); 0 keeps a scaling point "
+                        "whose headline is complete, CI can ask for non-zero")
     p.add_argument("--measure-seq", action="store_true",
                    help="time the reference sequential loops on this host (slow)")
     return p.parse_args()
@@ -182,10 +189,11 @@ def main() -> None:
 
     # a watchdog prints whatever has been measured if a section hangs (a
     # stuck collective), so the headline line is never lost.  The line then
-    # carries a "watchdog" field naming the unfinished sections; the exit
-    # status stays 0 because the headline measurement itself is complete
-    # (a multi-GPU point of the scaling curve is not voided by an optional
-    # section), while a failure of the headline raises before this is armed.
+    # carries a "watchdog" field naming the unfinished sections and stderr
+    # says so; the exit status is --hang-exit-code (default 0: the headline
+    # measurement itself is complete, and a multi-GPU point of the scaling
+    # curve is not voided by an optional section), while a failure of the
+    # headline raises before this is armed.
     import threading
 
     result: dict = {}
@@ -202,7 +210,8 @@ def main() -> None:
                               f"(finished: {', '.join(done) or 'none'}); the headline above is complete")
         emit()
         sys.stdout.flush()
-        os._exit(0)
+        print(f"bench.py: WATCHDOG: {result['watchdog']}", file=sys.stderr, flush=True)
+        os._exit(args.hang_exit_code)
 
     # -- headline: one independent 2048^2 system per GPU ----------------------
     src = gelim.random_system(n, seed=1234 + rank, device=dev)
@@ -293,6 +302,11 @@ def main() -> None:
             "panels": bench_dist_gauss(comm, gelim, torch, 2048, tail=0),
             "tail_engine": bench_dist_gauss(comm, gelim, torch, 2048)})
         _section(result, "dist_matmul_16384", lambda: bench_dist_matmul(comm, gelim, torch, 16384))
+        # large-n strong scaling (one system over ALL ranks), where the trailing
+        # update -- not the pivot chain -- dominates: the points of the curve
+        # where more GPUs should visibly win (one timed solve each)
+        _section(result, "dist_gauss_32768", lambda: bench_dist_gauss(comm, gelim, torch, 32768))
+        _section(result, "dist_rbt_16384", lambda: bench_dist_rbt(comm, gelim, torch, 16384))
         # single-GPU large systems (each rank its own: weak)
         _section(result, "gauss_8192_1gpu", lambda: bench_single(comm, gelim, torch, 8192, seed=77 + rank))
         # past the round-2 cap of 32768 rows per leaf (8.6 GB per system)
@@ -304,6 +318,7 @@ def main() -> None:
     if isinstance(hf, dict) and "time_s" in hf:
         result["headline_fresh_systems_s"] = hf["time_s"]
     for key, short in (("dist_gauss_8192", "dist_gauss_8192_s"), ("dist_gauss_8192_rbt", "dist_gauss_8192_rbt_s"),
+                       ("dist_gauss_32768", "dist_gauss_32768_s"), ("dist_rbt_16384", "dist_rbt_16384_s"),
                        ("dist_matmul_16384", "dist_matmul_16384_s"),
                        ("gauss_8192_1gpu", "gauss_8192_1gpu_s"), ("gauss_32768_1gpu", "gauss_32768_1gpu_s")):
         v = result.get(key)

@@ -209,10 +209,14 @@ __device__ __forceinline__ void tri_inv_apply(const double (*tT)[kBS], double rd
 }
 
 // Bounded wait (LDS spin) until *p >= want or the poller gave up.
+// The LDS hand-offs inside a workgroup (xseq -> xs[], done[] -> part[],
+// vready -> vb[]) are release stores / acquire loads at workgroup scope: the
+// plain LDS data a flag guards is then ordered before the flag store and
+// after the flag load (on gfx950 this costs an lgkmcnt wait, no cache work).
 __device__ __forceinline__ bool lds_wait(const int* p, int want, const int* abort_flag) {
-  if (__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= want) return true;
+  if (__hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) >= want) return true;
   const unsigned long long t0 = rtc();
-  while (__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < want) {
+  while (__hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < want) {
     if (__hip_atomic_load(abort_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != 0 || rtc() - t0 > kSpinTicks)
       return false;
   }
@@ -407,14 +411,14 @@ __global__ __launch_bounds__(kBsThreads) void backsub_persist_kernel(const T* __
               ra = fma(us[d][q], xx.x, ra);
               rb = fma(us[d][q + 1], xx.y, rb);
             }
-            if (lane == 0) __hip_atomic_store(&done[w], sq + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (lane == 0) __hip_atomic_store(&done[w], sq + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
             if (sq + kPf < nbg) load_slice<T>(us[d], urow, nb - 1 - (sq + kPf), n, w);
           }
         }
       }
     }
     part[w][lane] = ra + rb;
-    if (lane == 0) __hip_atomic_store(&done[w], nbg + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (lane == 0) __hip_atomic_store(&done[w], nbg + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
     if (w != 0) return;
     // ---- wave 0: T v' = y_b - sum, then v = v' - W2 x_{b+2} -----------------
     for (int q = 1; q < 4 && ok; ++q) ok = lds_wait(&done[q], nbg + 1, &abort_flag);
@@ -428,7 +432,7 @@ __global__ __launch_bounds__(kBsThreads) void backsub_persist_kernel(const T* __
       v -= row_dot_bcast(m, xs[nbg % kRing]);
     }
     vb[lane] = v;
-    if (lane == 0) __hip_atomic_store(&vready, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (lane == 0) __hip_atomic_store(&vready, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
     return;
   }
 
@@ -447,14 +451,21 @@ __global__ __launch_bounds__(kBsThreads) void backsub_persist_kernel(const T* __
     ok = ok && poll_x(x, c * kBS, min(kBS, n - c * kBS), err, false, xl);
     if (ok) {
       xs[sq % kRing][lane] = xl;
-      if (lane == 0) __hip_atomic_store(&xseq, sq + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      if (lane == 0) __hip_atomic_store(&xseq, sq + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
   }
   double xl1 = 0.0;
   if (has1 && ok) ok = poll_x(x, c1, cw1, err, false, xl1);
   if (ok) ok = lds_wait(&vready, 1, &abort_flag);
   if (!ok) {
-    if (lane == 0) __hip_atomic_store(&abort_flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    // x_b is never written: make sure the host hears of it even when no
+    // other workgroup is left to time out on it (block 0)
+    if (lane == 0) {
+      __hip_atomic_store(&abort_flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      int zero = 0;
+      __hip_atomic_compare_exchange_strong(err, &zero, 3, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+    }
     return;
   }
   double v = vb[lane];

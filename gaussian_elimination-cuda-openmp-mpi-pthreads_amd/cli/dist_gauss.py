@@ -130,10 +130,15 @@ def main(argv=None) -> int:
         dev = args.device or ("cuda:0" if torch.cuda.is_available() else "cpu")
         return max(run_emulated(args.emulate, lambda comm: run(args, comm), device=dev))
     comm = C.init_from_env(device=args.device)
+    ok = False
     try:
-        return run(args, comm)
+        rc = run(args, comm)
+        ok = True
+        return rc
     finally:
-        C.destroy()
+        # a failed rank (exception, CommFailure from the watchdog) aborts its
+        # communicators instead of waiting for peers that may be gone
+        C.destroy(abort=not ok)
 
 
 def run(args, comm) -> int:

@@ -38,6 +38,7 @@ def main(argv=None) -> int:
     args = parse(argv)
     comm = C.init_from_env(device=args.device)
     dev, P, r, n = comm.device, comm.world_size, comm.rank, args.size
+    ok = False
     try:
         A, B = reference_inputs(n)
         if args.algo in ("ring", "allgather"):
@@ -93,8 +94,9 @@ def main(argv=None) -> int:
                 json_line({"program": "dist_matmul", "algo": args.algo, "n": n, "ranks": P,
                                  "time_s": dt.item(), "tflops": 2 * n ** 3 / dt.item() * 1e-12,
                                  "max_rel_err": rel, "backend": comm.backend, "device": dev.type})
+        ok = True
     finally:
-        C.destroy()
+        C.destroy(abort=not ok)  # a failed rank does not wait for peers that may be gone
     return 0
 
 

@@ -17,8 +17,11 @@ resolve).
 """
 from __future__ import annotations
 
+import ctypes
 import datetime
 import os
+import threading
+import time
 from dataclasses import dataclass, field
 
 import torch
@@ -57,8 +60,9 @@ class _Event:
     """Handle of a collective issued on the communicator's own stream:
     wait() makes the CURRENT stream wait for it (no host block)."""
 
-    def __init__(self, ev: torch.cuda.Event):
+    def __init__(self, ev: torch.cuda.Event, what: str = "collective"):
         self.ev = ev
+        _watch(ev, what)
 
     def wait(self) -> bool:
         torch.cuda.current_stream().wait_event(self.ev)
@@ -68,9 +72,209 @@ class _Event:
         return self.ev.query()
 
 
+class CommFailure(RuntimeError):
+    """A device collective did not complete: a peer died or hung (no
+    progress within the watchdog's timeout), or RCCL reported an
+    asynchronous communicator error.  Every native communicator of the
+    process has been aborted (ncclCommAbort) when this is raised; the
+    process cannot issue further collectives and should exit."""
+
+
+class CommWatchdog:
+    """Failure detection for libgelim's native RCCL collectives (SURVEY §5.3:
+    async-error polling + a watchdog timeout).  The reference's MPI program
+    has none -- MPI_ERRORS_ARE_FATAL, no handler
+    (OpenMP_and_MPI/gauss_mpi/gauss_internal_input.c:289-297) -- and a dead
+    peer there ends the job; here a dead or stuck peer must not leave the
+    surviving ranks blocked forever in a device wait.
+
+    One daemon thread per process (started with the first native
+    communicator).  Every `poll_s` it
+      * asks each live communicator for its asynchronous error
+        (ncclCommGetAsyncError through gelim_rccl_async_error);
+      * queries the completion events of the outstanding collectives
+        (recorded after every native collective issued outside a hipGraph
+        capture) and fails when the oldest is older than `timeout_s`.
+    Failing = ncclCommAbort on every native communicator (RCCL kernels in
+    flight poll the abort flag and exit, so a blocked device wait returns),
+    then the error is raised on the main thread: directly by the solvers'
+    wait points (`Communicator.synchronize` / `Communicator.item`, event-query
+    loops with the same deadline), otherwise asynchronously
+    (PyThreadState_SetAsyncExc) once the main thread runs Python again.
+    The thread pauses while a hipGraph is being captured (`paused()`):
+    nothing it could query exists yet, and queries during a capture are
+    not safe."""
+
+    def __init__(self, timeout_s: float, poll_s: float = 0.05):
+        self.timeout_s = float(timeout_s)
+        self.poll_s = poll_s
+        self.error: CommFailure | None = None
+        self._raised = False
+        self._pending: list[tuple[float, torch.cuda.Event, str]] = []
+        self._lock = threading.Lock()
+        self._pause = 0
+        self._in_wait = 0
+        self._stop = threading.Event()
+        self._main = threading.main_thread().ident
+        self._thread = threading.Thread(target=self._run, name="gelim-rccl-watchdog", daemon=True)
+        self._thread.start()
+
+    # -- bookkeeping ----------------------------------------------------------
+    def track(self, ev: torch.cuda.Event, what: str) -> None:
+        with self._lock:
+            self._pending.append((time.monotonic(), ev, what))
+
+    def paused(self):
+        wd = self
+
+        class _P:
+            def __enter__(self):
+                with wd._lock:
+                    wd._pause += 1
+
+            def __exit__(self, *exc):
+                with wd._lock:
+                    wd._pause -= 1
+                    # ages restart: a capture's own host time is not a stall
+                    now = time.monotonic()
+                    wd._pending = [(now, e, w) for _, e, w in wd._pending]
+                return False
+
+        return _P()
+
+    def check(self) -> None:
+        """Raise the recorded failure (once per failure on the main path)."""
+        if self.error is not None:
+            self._raised = True
+            raise self.error
+
+    def fail(self, msg: str) -> None:
+        """Record the failure; the watchdog thread aborts the communicators
+        (ncclCommAbort can wait for the device to drain, so the raise on the
+        main thread never waits for it: from here on every native call
+        raises the recorded error instead of touching a communicator)."""
+        with self._lock:
+            if self.error is not None:
+                return
+            self.error = CommFailure(msg)
+            self._pending.clear()
+
+    def _abort_all(self) -> None:
+        for nc in list(_NATIVE):
+            try:
+                nc.destroy(abort=True)
+            except Exception:  # noqa: BLE001 - aborting is best effort
+                pass
+
+    def wait_event(self, ev: torch.cuda.Event, what: str) -> None:
+        """Host wait for ev as an event-query loop: raises CommFailure when
+        the watchdog failed, or when ev is not complete after timeout_s."""
+        t0 = time.monotonic()
+        spins = 0
+        with self._lock:
+            self._in_wait += 1
+        try:
+            while not ev.query():
+                self.check()
+                if time.monotonic() - t0 > self.timeout_s:
+                    self.fail(f"{what}: device work (collectives included) not finished after "
+                              f"{self.timeout_s:.1f} s -- a peer rank died or hung")
+                    self.check()
+                spins += 1
+                if spins > 2000:  # ~2 ms of spinning, then yield the CPU
+                    time.sleep(1e-4)
+            self.check()
+        finally:
+            with self._lock:
+                self._in_wait -= 1
+
+    def stop(self) -> None:
+        self._stop.set()
+
+    # -- the thread -----------------------------------------------------------
+    def _run(self) -> None:
+        aborted = False
+        while not self._stop.wait(self.poll_s):
+            if self.error is not None:
+                self._deliver()  # first: the raise does not wait for the abort
+                if not aborted:
+                    aborted = True
+                    self._abort_all()
+                continue
+            with self._lock:
+                if self._pause:
+                    continue
+                pending = list(self._pending)
+            try:
+                for nc in list(_NATIVE):
+                    rc = nc.async_error()
+                    if rc:
+                        self.fail(f"RCCL asynchronous error on communicator {nc.key!r}: {rc}")
+                        break
+                if self.error is None and pending:
+                    now = time.monotonic()
+                    done = set()
+                    for t, ev, what in pending:
+                        if ev.query():
+                            done.add(id(ev))
+                        elif now - t > self.timeout_s:
+                            self.fail(f"{what}: not complete after {now - t:.1f} s (timeout {self.timeout_s:.1f} "
+                                      "s) -- a peer rank died or hung")
+                            break
+                    with self._lock:
+                        self._pending = [p for p in self._pending if id(p[1]) not in done]
+            except Exception as e:  # noqa: BLE001 - a failing query is itself a failure
+                if self.error is None:
+                    self.fail(f"watchdog query failed: {e!r}")
+
+    def _deliver(self) -> None:
+        """Raise the failure in the main thread if no wait point did."""
+        with self._lock:
+            if self._raised or self._in_wait or self._main is None:
+                return
+            self._raised = True
+        ctypes.pythonapi.PyThreadState_SetAsyncExc(ctypes.c_ulong(self._main), ctypes.py_object(CommFailure))
+
+
+_WATCHDOG: list[CommWatchdog] = []  # the process's watchdog (at most one)
+_WATCHDOG_TIMEOUT = [600.0]         # init_from_env's timeout_s
+
+
+def watchdog() -> CommWatchdog | None:
+    return _WATCHDOG[0] if _WATCHDOG else None
+
+
+def start_watchdog(timeout_s: float | None = None, poll_s: float = 0.05) -> CommWatchdog:
+    """The process's watchdog (created on first use; timeout_s defaults to
+    init_from_env's)."""
+    if not _WATCHDOG:
+        _WATCHDOG.append(CommWatchdog(_WATCHDOG_TIMEOUT[0] if timeout_s is None else timeout_s, poll_s))
+    elif timeout_s is not None:
+        _WATCHDOG[0].timeout_s = float(timeout_s)
+    return _WATCHDOG[0]
+
+
+def _tracking() -> CommWatchdog | None:
+    """The watchdog if collectives are to be tracked now: not while a capture
+    is in progress (Communicator.capturing): the event would be a graph node,
+    and a graph's replay is waited for by the wait points.  (The pause flag,
+    not a runtime capture query per collective: the only Python-level
+    capture of collectives is DistributedRBT._replay, which sets it.)"""
+    wd = watchdog()
+    return wd if wd is not None and not wd._pause else None
+
+
+def _watch(ev: torch.cuda.Event, what: str) -> None:
+    """Track a native collective's completion event."""
+    wd = _tracking()
+    if wd is not None:
+        wd.track(ev, what)
+
+
 _DTYPE = {torch.float64: 0, torch.float32: 1, torch.int32: 2, torch.int64: 3, torch.uint8: 4}
 _OP = {"sum": 0, "max": 1, "min": 2}
 _NATIVE: list = []  # every live NativeRccl of the process (destroy() releases them)
+_NATIVE_LOCK = threading.RLock()  # destroy vs the watchdog's async-error queries
 
 
 class NativeRccl:
@@ -102,12 +306,36 @@ class NativeRccl:
         with torch.cuda.device(device):
             _native.check(lib.gelim_rccl_comm_create(ctypes.byref(h), idb, nranks, rank), "rccl_comm_create")
         self.handle, self.nranks, self.rank, self.device = h.value, nranks, rank, device
+        self.key = key
         _NATIVE.append(self)
+        start_watchdog()
 
     def check(self, rc: int, what: str) -> None:
         from .. import _native
 
         _native.check(rc, what)
+        wd = _tracking()
+        if wd is not None:
+            # synchronous collectives: their completion is tracked like the
+            # asynchronous ones' (an event on the stream they were issued on)
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(self.device))
+            wd.track(ev, what)
+
+    def _h(self):
+        """The live handle; after a failure (abort pending or done), the
+        failure that caused it."""
+        wd = watchdog()
+        if wd is not None and wd.error is not None:
+            raise wd.error
+        if not self.handle:
+            raise CommFailure(f"RCCL communicator {self.key!r} was destroyed")
+        return self.handle
+
+    def async_error(self) -> int:
+        with _NATIVE_LOCK:  # never on a communicator being destroyed
+            h = self.handle
+            return self.lib.gelim_rccl_async_error(h) if h else 0
 
     @staticmethod
     def dtype(t: torch.Tensor) -> int:
@@ -117,30 +345,31 @@ class NativeRccl:
             raise TypeError(f"RCCL collective on {t.dtype}") from None
 
     def bcast(self, t: torch.Tensor, root: int, stream: int) -> None:
-        self.check(self.lib.gelim_rccl_bcast(self.handle, t.data_ptr(), t.numel(), self.dtype(t), root, stream),
+        self.check(self.lib.gelim_rccl_bcast(self._h(), t.data_ptr(), t.numel(), self.dtype(t), root, stream),
                    "rccl_bcast")
 
     def allreduce(self, t: torch.Tensor, op: str, stream: int) -> None:
-        self.check(self.lib.gelim_rccl_allreduce(self.handle, t.data_ptr(), t.data_ptr(), t.numel(), self.dtype(t),
+        self.check(self.lib.gelim_rccl_allreduce(self._h(), t.data_ptr(), t.data_ptr(), t.numel(), self.dtype(t),
                                                  _OP[op], stream), "rccl_allreduce")
 
     def allgather(self, out: torch.Tensor, t: torch.Tensor, stream: int) -> None:
-        self.check(self.lib.gelim_rccl_allgather(self.handle, t.data_ptr(), out.data_ptr(), t.numel(),
+        self.check(self.lib.gelim_rccl_allgather(self._h(), t.data_ptr(), out.data_ptr(), t.numel(),
                                                  self.dtype(t), stream), "rccl_allgather")
 
     def sendrecv(self, send_t: torch.Tensor | None, dst: int, recv_t: torch.Tensor | None, src: int,
                  stream: int) -> None:
         ref = send_t if send_t is not None else recv_t
         self.check(self.lib.gelim_rccl_sendrecv(
-            self.handle, send_t.data_ptr() if send_t is not None else None,
+            self._h(), send_t.data_ptr() if send_t is not None else None,
             send_t.numel() if send_t is not None else 0, dst,
             recv_t.data_ptr() if recv_t is not None else None, recv_t.numel() if recv_t is not None else 0, src,
             self.dtype(ref), stream), "rccl_sendrecv")
 
     def destroy(self, abort: bool = False) -> None:
-        if self.handle:
-            self.lib.gelim_rccl_comm_destroy(self.handle, int(abort))
-            self.handle = None
+        with _NATIVE_LOCK:
+            h, self.handle = self.handle, None
+            if h:
+                self.lib.gelim_rccl_comm_destroy(h, int(abort))
         if self in _NATIVE:
             _NATIVE.remove(self)
 
@@ -308,9 +537,13 @@ class Communicator:
         """Send to dst and receive from src as ONE batched p2p operation
         (batch_isend_irecv: RCCL group semantics, so a ring of such calls
         cannot deadlock on serialised send kernels).  Returns the requests."""
-        if self.native:  # one grouped RCCL send/recv on the current stream
-            self.rccl().sendrecv(send_t, dst, recv_t, src, self._cur())
-            return [_Done(), _Done()]
+        if self.native:
+            # one grouped RCCL send/recv on the communicator stream (after the
+            # work queued so far on the current one), so a ring step's
+            # transfer overlaps the compute queued behind it; wait() makes the
+            # current stream wait for it
+            nc = self.rccl()
+            return [self._on_comm_stream(lambda s: nc.sendrecv(send_t, dst, recv_t, src, s), send_t, recv_t)]
         if self.staged:
             hs = send_t.detach().cpu()
             hr = torch.empty(recv_t.shape, dtype=recv_t.dtype)
@@ -321,6 +554,39 @@ class Communicator:
         ops = [dist.P2POp(dist.isend, send_t, self.global_rank(dst), self.group),
                dist.P2POp(dist.irecv, recv_t, self.global_rank(src), self.group)]
         return dist.batch_isend_irecv(ops)
+
+    # -- host waits (the wait points of the distributed solvers) ---------------
+    def synchronize(self) -> None:
+        """Host wait for the work queued on the current stream.  On the
+        native RCCL path this is an event-query loop under the watchdog
+        (CommWatchdog.wait_event): a collective that a dead or stuck peer
+        never completes raises CommFailure after the timeout instead of
+        blocking forever in hipDeviceSynchronize."""
+        if self.device.type != "cuda":
+            return
+        wd = watchdog() if self.native else None
+        if wd is None:
+            torch.cuda.synchronize(self.device)
+            return
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.device))
+        wd.wait_event(ev, f"rank {self.rank}: host wait")
+
+    def item(self, t: torch.Tensor):
+        """t.item() behind synchronize() (a guarded wait point)."""
+        if t.device.type == "cuda" and self.native:
+            self.synchronize()
+        return t.item()
+
+    def capturing(self):
+        """Context for a hipGraph capture of this rank's collectives: the
+        watchdog pauses (its event queries are not safe during a capture)."""
+        wd = watchdog()
+        if wd is None:
+            import contextlib
+
+            return contextlib.nullcontext()
+        return wd.paused()
 
     def global_rank(self, r: int) -> int:
         if self.group is None:
@@ -385,6 +651,9 @@ def init_from_env(backend: str | None = None, device: str | None = None,
     process group (an in-memory store, no rendezvous), so the distributed
     schedules run their collectives through RCCL on a single GPU."""
     rank, world, local = env_world()
+    _WATCHDOG_TIMEOUT[0] = float(timeout_s)
+    if _WATCHDOG:
+        _WATCHDOG[0].timeout_s = float(timeout_s)
     use_gpu = device != "cpu" and (device is not None or torch.cuda.is_available())
     want = backend or os.environ.get("GELIM_DIST_BACKEND")
     if use_gpu:
@@ -410,9 +679,12 @@ def init_from_env(backend: str | None = None, device: str | None = None,
         return Communicator(0, 1, dev, backend, pg=True)
     backend = backend or os.environ.get("GELIM_DIST_BACKEND") or ("nccl" if use_gpu else "gloo")
     # failure detection: a rank that dies or hangs must not leave the others
-    # blocked forever.  RCCL's async error handling turns a collective that
-    # exceeds `timeout_s` (or a communicator error) into an abort + host
-    # exception on every surviving rank; gloo raises on the same timeout.
+    # blocked forever.  ProcessGroupNCCL's async error handling turns a
+    # collective that exceeds `timeout_s` (or a communicator error) into an
+    # abort on every surviving rank; gloo raises on the same timeout; the
+    # solvers' own RCCL communicators are covered by CommWatchdog (same
+    # timeout: ncclCommGetAsyncError polling, completion-event ages, guarded
+    # host waits, ncclCommAbort + CommFailure).
     os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", "29511")
@@ -426,8 +698,20 @@ def init_from_env(backend: str | None = None, device: str | None = None,
 
 def destroy(abort: bool = False) -> None:
     """Release the native RCCL communicators (abort=True: ncclCommAbort,
-    after a failed peer) and the process group."""
+    after a failed peer -- also what happens when the watchdog has failed)
+    and the process group."""
+    wd = watchdog()
+    if wd is not None:
+        abort = abort or wd.error is not None
+        wd.stop()
+        _WATCHDOG.clear()
     for nc in list(_NATIVE):
         nc.destroy(abort)
     if dist.is_initialized():
+        if abort:
+            try:
+                dist.distributed_c10d._abort_process_group()  # type: ignore[attr-defined]
+                return
+            except Exception:  # noqa: BLE001 - older torch: plain destroy
+                pass
         dist.destroy_process_group()

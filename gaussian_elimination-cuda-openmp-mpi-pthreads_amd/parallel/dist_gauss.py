@@ -538,7 +538,7 @@ class DistributedGauss:
         the factors are incomplete."""
         v = self._info[1:2].clone().to(torch.int64)
         self.comm.all_reduce(v, "max")
-        return int(v.item())
+        return int(self.comm.item(v))
 
     def info(self) -> int:
         """First zero-pivot column + 1 over all ranks (0 = non-singular): each
@@ -548,7 +548,7 @@ class DistributedGauss:
         sentinel = self.n_pad + 1
         v = torch.where(v == 0, torch.full_like(v, sentinel), v)
         self.comm.all_reduce(v, "min")
-        val = int(v.item())
+        val = int(self.comm.item(v))
         return 0 if val == sentinel else val
 
     # -- back substitution ----------------------------------------------------

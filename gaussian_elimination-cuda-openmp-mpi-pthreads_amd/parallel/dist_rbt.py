@@ -313,7 +313,7 @@ class DistributedRBT:
             self._factor_serial()
         v = self._info.to(torch.int64)
         self.comm.all_reduce(v, "min")
-        val = int(v.item())
+        val = int(self.comm.item(v))
         return 0 if val == 0x7F7F7F7F else val
 
     def _factor_serial(self) -> None:
@@ -466,7 +466,7 @@ class DistributedRBT:
         if ent is None:
             g = torch.cuda.CUDAGraph()
             try:
-                with torch.cuda.graph(g, capture_error_mode="thread_local"):
+                with self.comm.capturing(), torch.cuda.graph(g, capture_error_mode="thread_local"):
                     out = fn()
             except Exception as e:  # noqa: BLE001 - a transport that cannot be captured: stay eager
                 import warnings
@@ -528,7 +528,7 @@ class DistributedRBT:
         one rank raising while the others block in the next collective."""
         v = self._serr.to(torch.int64)
         self.comm.all_reduce(v, "max")
-        if int(v.item()) == 0:
+        if int(self.comm.item(v)) == 0:
             return False
         self._serr.zero_()
         return True
@@ -556,7 +556,7 @@ class DistributedRBT:
         tiny = torch.finfo(torch.float64).tiny
         rn = r[:n]
         om = torch.where(w > 0, rn.abs() / w.clamp_min(tiny), torch.where(rn != 0, torch.full_like(rn, math.inf), rn))
-        return r, float(om.max())
+        return r, float(self.comm.item(om.max()))
 
     # -- the solve --------------------------------------------------------------
     def solve_(self, loc: torch.Tensor) -> torch.Tensor:

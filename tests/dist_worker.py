@@ -274,3 +274,217 @@ def rccl_one_rank(outdir, n_gauss=2048, n_rbt=2048):
     (out / "res.json").write_text(json.dumps(res, indent=1, default=str))
     if not res["ok"]:
         raise SystemExit(1)
+
+
+def rccl_watchdog(outdir):
+    """Failure detection on the native RCCL path, on ONE GPU:
+    a one-rank native broadcast queued behind a bounded 2 s spin kernel
+    stands in for a collective whose peer never arrives.  With the watchdog
+    at timeout 0.5 s:
+      wait_point  the guarded host wait (Communicator.synchronize, the
+                  solvers' wait points) raises CommFailure after ~0.5 s;
+      async       with the main thread in plain Python (no wait point), the
+                  watchdog thread raises CommFailure in it asynchronously.
+    Both times every native communicator is aborted (ncclCommAbort) and a
+    further collective raises at once.  A one-rank in-place broadcast
+    queues no RCCL kernel, so the abort has no device work to cancel; the
+    spin kernel ends on its own and the process exits normally."""
+    import json
+    import time
+
+    import torch
+
+    from gelim import _native
+    from gelim.parallel import comm as C
+    from gelim.utils.tensors import ptr
+
+    out = Path(outdir)
+    res = {}
+    try:
+        comm = _init(0, 1, 0, "nccl", timeout_s=120)
+        dev = comm.device
+        res["native"] = comm.native
+        lib = _native.lib()
+        t = torch.zeros(4096, dtype=torch.float64, device=dev)
+        words = torch.zeros(2, dtype=torch.int32, device=dev)
+        spin_ticks = 200_000_000  # 2 s of s_memrealtime (100 MHz)
+
+        steps = {}
+
+        def stall_then_bcast():
+            a = time.perf_counter()
+            comm.broadcast(t, 0)  # creates the communicator (and the watchdog)
+            steps["create_bcast"] = time.perf_counter() - a
+            comm.synchronize()
+            # the communicator stream exists before the stall: creating it
+            # probes it against the default stream, which would wait for the
+            # spin kernel (utils/tensors.dedicated_stream)
+            comm.comm_stream()
+            steps["sync"] = time.perf_counter() - a
+            C.start_watchdog(timeout_s=0.5, poll_s=0.02)
+            words.zero_()
+            steps["zero"] = time.perf_counter() - a
+            _native.check(lib.gelim_gpu_probe_kernel(torch.cuda.current_stream(dev).cuda_stream, ptr(words), 0,
+                                                     spin_ticks), "probe_kernel")
+            steps["spin_launch"] = time.perf_counter() - a
+            h = comm.broadcast_async(t, 0)
+            steps["bcast_async"] = time.perf_counter() - a
+            return h
+
+        # 1. the guarded wait point
+        ts = time.perf_counter()
+        h = stall_then_bcast()
+        t0 = time.perf_counter()
+        probe = torch.cuda.Event()
+        probe.record(torch.cuda.current_stream(dev))
+        diag = {"issue_s": t0 - ts, "steps": dict(steps), "stream_busy_after_issue": not probe.query(), "pending": len(C.watchdog()._pending),
+                "timeout_s": C.watchdog().timeout_s}
+        try:
+            h.wait()
+            comm.synchronize()
+            res["wait_point"] = {"raised": False, "sync_s": time.perf_counter() - t0, **diag}
+        except C.CommFailure as e:
+            res["wait_point"] = {"raised": True, "after_s": time.perf_counter() - t0, "msg": str(e)[:200],
+                                 "native_left": len(C._NATIVE)}
+        try:
+            comm.broadcast(t, 0)
+            res["wait_point"]["later_call_raised"] = False
+        except C.CommFailure:
+            res["wait_point"]["later_call_raised"] = True
+        torch.cuda.synchronize(dev)  # the spin kernel ends by itself
+        time.sleep(0.2)
+        res["wait_point"]["native_left_later"] = len(C._NATIVE)  # the watchdog thread aborted them
+        # fresh communicator + watchdog for the second case
+        wd = C.watchdog()
+        wd.stop()
+        C._WATCHDOG.clear()
+        comm._rccl = None
+        comm.key = "world-2"
+
+        # 2. no wait point: the watchdog thread raises in the main thread
+        h = stall_then_bcast()
+        t0 = time.perf_counter()
+        try:
+            for _ in range(500):  # 5 s of plain Python
+                time.sleep(0.01)
+            res["async"] = {"raised": False}
+        except C.CommFailure:
+            res["async"] = {"raised": True, "after_s": time.perf_counter() - t0}
+        torch.cuda.synchronize(dev)
+        time.sleep(0.2)
+        res["async"]["native_left_later"] = len(C._NATIVE)
+        C.destroy(abort=True)
+        res["ok"] = True
+    except Exception:
+        res["ok"] = False
+        res["traceback"] = traceback.format_exc()
+    (out / "res.json").write_text(json.dumps(res, indent=1, default=str))
+
+
+def dead_rank_rccl(rank, world, port, outdir):
+    """dead_rank over RCCL with libgelim's native communicators (one rank per
+    GPU): the last rank dies after the communicator exists; the survivors'
+    distributed solve must raise CommFailure within the watchdog timeout
+    (not hang in a device wait)."""
+    import time
+
+    import torch
+
+    from gelim.parallel import DistributedGauss
+    from gelim.parallel import comm as C
+
+    comm = _init(rank, world, port, "nccl", timeout_s=120)
+    C.start_watchdog(timeout_s=5.0, poll_s=0.05)
+    t = torch.ones(1024, dtype=torch.float64, device=comm.device)
+    comm.all_reduce(t)  # every rank's native communicator exists
+    comm.synchronize()
+    if rank == world - 1:
+        os._exit(3)
+    t0 = time.perf_counter()
+    try:
+        dg = DistributedGauss(comm, 4096, block=256)
+        dg.solve_(dg.generate_random(seed=1))
+        (Path(outdir) / f"ok{rank}.txt").write_text("finished")
+    except Exception as e:  # noqa: BLE001
+        (Path(outdir) / f"raised{rank}.txt").write_text(f"{time.perf_counter() - t0:.1f} {type(e).__name__}: {e}")
+    os._exit(0)
+
+
+def native_ops_multi(rank, world, port, outdir):
+    """libgelim's RCCL communicator across ranks (one per GPU): broadcasts
+    from every root, cross-rank sum / max / min, a rank-ordered all_gather
+    and a ring send/recv, each checked against its closed form; results to
+    ops{rank}.json."""
+    import json
+
+    import torch
+
+    from gelim.parallel import comm as C
+
+    res = {}
+    try:
+        comm = _init(rank, world, port, "nccl")
+        dev = comm.device
+        nc = comm.rccl()
+        cur = torch.cuda.current_stream(dev).cuda_stream
+        for dt in (torch.float64, torch.float32, torch.int32, torch.int64):
+            base = torch.arange(1, 257, device=dev).to(dt)
+            for root in range(world):
+                t = base * (rank + 1)
+                nc.bcast(t, root, cur)
+                res[f"bcast_root{root}_{dt}"] = bool(torch.equal(t, base * (root + 1)))
+            for op, want in (("sum", base * (world * (world + 1) // 2)), ("max", base * world), ("min", base)):
+                t = base * (rank + 1)
+                nc.allreduce(t, op, cur)
+                res[f"allreduce_{op}_{dt}"] = bool(torch.equal(t, want))
+            o = torch.zeros(256 * world, dtype=dt, device=dev)
+            nc.allgather(o, base * (rank + 1), cur)
+            want = torch.cat([base * (q + 1) for q in range(world)])
+            res[f"allgather_{dt}"] = bool(torch.equal(o, want))
+            o = torch.zeros(256, dtype=dt, device=dev)
+            nc.sendrecv(base * (rank + 1), (rank + 1) % world, o, (rank - 1) % world, cur)
+            res[f"sendrecv_{dt}"] = bool(torch.equal(o, base * ((rank - 1) % world + 1)))
+        # the asynchronous forms through the Communicator (communicator stream + events)
+        t = torch.full((1000,), float(rank), dtype=torch.float64, device=dev)
+        comm.broadcast_async(t, world - 1).wait()
+        res["bcast_async_last_root"] = bool((t == world - 1).all().item())
+        comm.synchronize()
+        res["unique_id_rank"] = rank
+        res["ok"] = all(v for k, v in res.items() if isinstance(v, bool))
+        C.destroy()
+    except Exception:
+        res["ok"] = False
+        res["traceback"] = traceback.format_exc()
+    (Path(outdir) / f"ops{rank}.json").write_text(json.dumps(res, indent=1))
+
+
+def rbt_timed(rank, world, port, outdir, n, seed):
+    """DistributedRBT over RCCL, graph-replayed: three solves (eager,
+    captured, replayed); x of the last to x{rank}.pt, [graph, steps, berr,
+    fallback, replay seconds] to meta{rank}.txt."""
+    import time
+
+    import torch
+
+    from gelim.parallel import DistributedRBT
+    from gelim.parallel import comm as C
+
+    try:
+        comm = _init(rank, world, port, "nccl")
+        d = DistributedRBT(comm, n, single_fast_path=False)
+        dt = None
+        for _ in range(3):
+            loc = d.generate_random(seed=seed)
+            comm.synchronize()
+            comm.barrier()
+            t0 = time.perf_counter()
+            x = d.solve_(loc)
+            comm.synchronize()
+            dt = time.perf_counter() - t0
+        torch.save(x.cpu(), Path(outdir) / f"x{rank}.pt")
+        (Path(outdir) / f"meta{rank}.txt").write_text(f"{d.graph} {d.last_steps} {d.last_berr} {d.last_fallback} {dt}")
+        d.close()
+        C.destroy()
+    except Exception:
+        (Path(outdir) / f"err{rank}.txt").write_text(traceback.format_exc())
+        raise

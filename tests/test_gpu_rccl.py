@@ -108,3 +108,42 @@ def test_native_rccl_ops(rccl_run, op, dtype):
     in each supported dtype, one rank, on the current stream."""
     _, res = rccl_run
     assert res["native_ops"][f"{op}_{dtype}"], res["native_ops"]
+
+
+@pytest.fixture(scope="module")
+def watchdog_run(tmp_path_factory, cuda):
+    out = tmp_path_factory.mktemp("rccl_wd")
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", MASTER_ADDR="127.0.0.1")
+    code = f"import dist_worker; dist_worker.rccl_watchdog({str(out)!r})"
+    proc = subprocess.run([sys.executable, "-u", "-c", code], cwd=HERE, env=env, capture_output=True, text=True,
+                          timeout=120)
+    resf = out / "res.json"
+    assert resf.exists(), f"rc={proc.returncode}\n{proc.stdout[-3000:]}\n{proc.stderr[-3000:]}"
+    res = json.loads(resf.read_text())
+    keep = HERE.parent / "gpurun_out"
+    if keep.is_dir():
+        (keep / "rccl_watchdog_res.json").write_text(resf.read_text())
+    assert res.get("ok"), res.get("traceback", res)
+    assert proc.returncode == 0, proc.stderr[-2000:]  # the process exits cleanly after the abort
+    return res
+
+
+def test_rccl_watchdog_wait_point(watchdog_run):
+    """A collective stuck behind a 2 s kernel, watchdog timeout 0.5 s: the
+    guarded host wait raises CommFailure within ~1 s, every native
+    communicator is aborted, and the next collective raises at once
+    (gauss_mpi/gauss_internal_input.c:289-297 has no handler)."""
+    r = watchdog_run["wait_point"]
+    assert watchdog_run["native"]
+    assert r["raised"], r
+    assert 0.4 <= r["after_s"] <= 1.5, r
+    assert r["later_call_raised"] and r["native_left_later"] == 0, r
+
+
+def test_rccl_watchdog_async(watchdog_run):
+    """The same stall with the main thread outside any wait point: the
+    watchdog thread raises CommFailure in it."""
+    r = watchdog_run["async"]
+    assert r["raised"], r
+    assert 0.4 <= r["after_s"] <= 1.5, r
+    assert r["native_left_later"] == 0, r

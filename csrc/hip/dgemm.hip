@@ -77,7 +77,23 @@ struct Args {
   double alpha;
   int acc;  // 1: C += alpha A B, 0: C = alpha A B (C is not read)
   int group;  // tile order: runs of `group` tile rows, column-major inside a run (<= 1: row-major)
+  // column-block-major B / C (0: plain row-major): columns [128 c, 128 c + 128)
+  // of the operand live in their own slab at +c * bbs (cbs) doubles, rows at
+  // ldb (ldc) inside it -- DistributedRBT's local storage, where every 128-
+  // column block is contiguous so its column goes out in one in-place broadcast
+  int64_t bbs, cbs;
 };
+
+// Column-block-major operands: shift B and C to the slab of the tile's
+// 128-column block (a 128- or 64-wide tile never straddles two), so the
+// row-major addressing below is unchanged.
+__device__ __forceinline__ Args slab_args(const Args& g, int n0) {
+  Args s = g;
+  const int64_t blk = n0 / 128;
+  if (g.bbs) s.B += blk * (g.bbs - 128);
+  if (g.cbs) s.C += blk * (g.cbs - 128);
+  return s;
+}
 
 // Tile index -> (tile row, tile column).  Grouped order: the 64 workgroups an
 // XCD runs at once (consecutive indices of its run) cover an 8 x 8 block of
@@ -163,7 +179,8 @@ __device__ __forceinline__ void store_stage(const Stage<T>& st, double* As, doub
 // double buffer at lds.  store = false: computed, not written (a persistent
 // workgroup's idle half, which still has to meet every barrier).
 template <bool FULL, int T = 128>
-__device__ __forceinline__ void tile_body(const Args& g, int m0, int n0, double* lds, int t, bool store = true) {
+__device__ __forceinline__ void tile_body(const Args& g0, int m0, int n0, double* lds, int t, bool store = true) {
+  const Args g = slab_args(g0, n0);
   using G = Geo<T>;
   constexpr int SA = G::SA, SB = G::SB, WM = G::WM, WN = G::WN, MB = G::MB, NB = G::NB;
   // stage b of the double buffer as offsets from lds (an array of the two
@@ -323,18 +340,24 @@ __global__ __launch_bounds__(kPThreads, 1) void dgemm_persist_kernel(Args g) {
 // noise of it, profiles/dgemm_r3_lds.txt), else that order.  C is stored
 // plainly (write-through stores were within noise, profiles/dgemm_wt_r4.txt).
 int dgemm_launch(double* C, int64_t ldc, const double* A, int64_t lda, const double* B, int64_t ldb, int64_t M,
-                 int64_t N, int64_t K, double alpha, int max_wg, hipStream_t s, int accumulate, int group_arg) {
+                 int64_t N, int64_t K, double alpha, int max_wg, hipStream_t s, int accumulate, int group_arg,
+                 int64_t bbs = 0, int64_t cbs = 0) {
   if (M <= 0 || N <= 0 || K <= 0) return GELIM_OK;
   if (M > INT32_MAX || N > INT32_MAX || K > INT32_MAX) return GELIM_FAIL(GELIM_E_ARG, "dgemm: dimension > 2^31");
+  // column-block-major operands: whole 128-column blocks, 128-wide slabs
+  if ((bbs || cbs) && (N % 128 || (bbs && (ldb < 128 || bbs < ldb * K || (bbs & 1))) ||
+                       (cbs && (ldc < 128 || cbs < ldc * M))))
+    return GELIM_FAIL(GELIM_E_ARG, "dgemm: column-block-major operands need N % 128 == 0 and 128-wide slabs");
+  const int64_t nb_row = bbs ? std::min<int64_t>(N, 128) : N, nc_row = cbs ? std::min<int64_t>(N, 128) : N;
   // 16-byte operand chunks: 16-byte aligned A and B, even leading dimensions
   // and K, and one double of row padding in B when N is odd
   if ((K & 1) || (lda & 1) || (ldb & 1) || (((uintptr_t)A | (uintptr_t)B) & 15) || ((N & 1) && ldb <= N) ||
-      lda < K || ldb < N || ldc < N)
+      lda < K || ldb < nb_row || ldc < nc_row)
     return GELIM_FAIL(GELIM_E_ARG, "dgemm: unsupported alignment / leading dimensions (K=" + std::to_string(K) +
                                        " lda=" + std::to_string(lda) + " ldb=" + std::to_string(ldb) + ")");
   const int tm = (int)((M + BM - 1) / BM), tn = (int)((N + BN - 1) / BN);
   const int group = group_arg >= 0 ? group_arg : 1;
-  Args g{C, ldc, A, lda, B, ldb, (int)M, (int)N, (int)K, tn, tm * tn, alpha, accumulate ? 1 : 0, group};
+  Args g{C, ldc, A, lda, B, ldb, (int)M, (int)N, (int)K, tn, tm * tn, alpha, accumulate ? 1 : 0, group, bbs, cbs};
   // max_wg > 0: at most max_wg CUs (rounded down to a multiple of 8)
   const int cap = max_wg > 0 ? std::max(8, max_wg / 8 * 8) : 0;
   // few tiles: one 256-thread workgroup per tile already stays within the
@@ -417,7 +440,7 @@ int dgemm_pair(const GemmOp& p1, const GemmOp& p2, double alpha, int accumulate,
   auto args = [&](const GemmOp& o, int T) {
     const int tm = (int)((o.M + T - 1) / T), tn = (int)((o.N + T - 1) / T);
     return Args{o.C, o.ldc, o.A, o.lda, o.B, o.ldb, (int)o.M, (int)o.N, (int)o.K, tn, tm * tn, alpha,
-                accumulate ? 1 : 0, 1};
+                accumulate ? 1 : 0, 1, 0, 0};
   };
   const Args a1 = args(p1, 128), a2 = args(p2, 128);
   if ((int64_t)a1.ntiles + a2.ntiles < (int64_t)ncu) {  // thin: 64-tiles, as dgemm_launch
@@ -443,6 +466,16 @@ extern "C" int gelim_gpu_dgemm_grouped(double* dC, int64_t ldc, const double* dA
                                        int group, void* stream) {
   return gelim::dgemm_launch(dC, ldc, dA, lda, dB, ldb, M, N, K, alpha, max_wg, (hipStream_t)stream, 1,
                              group < 0 ? 0 : group);
+}
+
+// Column-block-major B and / or C (bbs / cbs: doubles between consecutive
+// 128-column slabs; 0 = plain row-major): C (+)= alpha A B with N a multiple
+// of 128.  DistributedRBT's local storage (parallel/dist_rbt.py).
+extern "C" int gelim_gpu_dgemm_bm(double* dC, int64_t ldc, int64_t cbs, const double* dA, int64_t lda,
+                                  const double* dB, int64_t ldb, int64_t bbs, int64_t M, int64_t N, int64_t K,
+                                  double alpha, int accumulate, int max_wg, void* stream) {
+  return gelim::dgemm_launch(dC, ldc, dA, lda, dB, ldb, M, N, K, alpha, max_wg, (hipStream_t)stream, accumulate, -1,
+                             bbs, cbs);
 }
 
 // the persistent form on at most max_wg CUs (tests / benchmarks)

@@ -36,9 +36,11 @@ constexpr int NB = 128;  // block = the single-GPU engine's (lu_mixed.hip)
 // M_loc = (U^T A V) restricted to this rank's columns.  Thread (i, jl): row
 // group i (rows i + q h), local column group jl (local columns jl + p hl),
 // whose global group index is j = (jl / 128 * P + r) * 128 + jl % 128.
+// mbs > 0: M is column-block-major -- local block c (columns 128 c ..) is the
+// slab at M + c * mbs, rows at ldm (= 128) inside it.
 __global__ __launch_bounds__(256) void drbt_transform_kernel(const double* __restrict__ A, int64_t lda,
-                                                             double* __restrict__ M, int64_t ldm, int np, int nloc,
-                                                             int P, int r, const double* __restrict__ ud,
+                                                             double* __restrict__ M, int64_t ldm, int64_t mbs, int np,
+                                                             int nloc, int P, int r, const double* __restrict__ ud,
                                                              const double* __restrict__ vd) {
   const int h = np / 4, hl = nloc / 4;
   const int jl = blockIdx.x * 256 + threadIdx.x;
@@ -70,7 +72,10 @@ __global__ __launch_bounds__(256) void drbt_transform_kernel(const double* __res
       double v = 0.0;
 #pragma unroll
       for (int c = 0; c < 4; ++c) v += t[q][c] * V[c][p];
-      M[(int64_t)(i + q * h) * ldm + jl + p * hl] = v;
+      const int col = jl + p * hl;
+      const int64_t at = mbs ? (col / NB) * mbs + (int64_t)(i + q * h) * ldm + col % NB
+                             : (int64_t)(i + q * h) * ldm + col;
+      M[at] = v;
     }
 }
 
@@ -168,16 +173,17 @@ __global__ __launch_bounds__(256) void matvec_abs_kernel(const double* __restric
 
 // M (np x nloc, ldm) = this rank's columns of U^T A V, A (np x nloc, lda) the
 // rank's columns of the padded system.  np a multiple of 512 P, nloc = np / P.
-extern "C" int gelim_drbt_transform(const double* A, int64_t lda, double* M, int64_t ldm, int64_t np, int64_t nloc,
-                                    int P, int r, const double* ud, const double* vd, void* stream) {
+// mbs > 0: M column-block-major (128-column slabs mbs doubles apart, ldm = 128).
+extern "C" int gelim_drbt_transform(const double* A, int64_t lda, double* M, int64_t ldm, int64_t mbs, int64_t np,
+                                    int64_t nloc, int P, int r, const double* ud, const double* vd, void* stream) {
   if (!A || !M || !ud || !vd || P < 1 || r < 0 || r >= P || np % (512 * (int64_t)P) || nloc * P != np ||
-      lda < nloc || ldm < nloc || np > INT32_MAX)
+      lda < nloc || (mbs ? (ldm != gelim::NB || mbs < np * ldm) : ldm < nloc) || np > INT32_MAX)
     return GELIM_FAIL(GELIM_E_ARG, "drbt_transform: bad layout (np must be a multiple of 512 P, nloc = np / P)");
   const int64_t h = np / 4, hl = nloc / 4;
   if (h > 65535) return GELIM_FAIL(GELIM_E_ARG, "drbt_transform: order too large for the grid");
   const dim3 grid((unsigned)((hl + 255) / 256), (unsigned)h);
-  hipLaunchKernelGGL(gelim::drbt_transform_kernel, grid, dim3(256), 0, (hipStream_t)stream, A, lda, M, ldm, (int)np,
-                     (int)nloc, P, r, ud, vd);
+  hipLaunchKernelGGL(gelim::drbt_transform_kernel, grid, dim3(256), 0, (hipStream_t)stream, A, lda, M, ldm, mbs,
+                     (int)np, (int)nloc, P, r, ud, vd);
   HIP_TRY(hipGetLastError());
   return GELIM_OK;
 }

@@ -100,7 +100,9 @@ _PROTOS = {
     "gelim_mixed_reset_error": (_int, [_vp, _vp]),
     "gelim_rbt_block_inverse": (_int, [_vp, _i64, _i64, _vp, _vp, _vp]),
     "gelim_rbt_vec": (_int, [_vp, _i64, _i64, _i64, _vp, _int, _vp, _i64, _vp]),
-    "gelim_drbt_transform": (_int, [_vp, _i64, _vp, _i64, _i64, _i64, _int, _int, _vp, _vp, _vp]),
+    "gelim_drbt_transform": (_int, [_vp, _i64, _vp, _i64, _i64, _i64, _i64, _int, _int, _vp, _vp, _vp]),
+    "gelim_gpu_dgemm_bm": (_int, [_vp, _i64, _i64, _vp, _i64, _vp, _i64, _i64, _i64, _i64, _i64, _dbl, _int, _int,
+                                  _vp]),
     "gelim_drbt_super_solve": (_int, [_vp, _i64, _vp, _int, _vp, _vp, _vp, _int, _vp]),
     "gelim_rbt_block_solve": (_int, [_vp, _i64, _vp, _int, _vp, _vp, _vp, _int, _vp, _vp]),
     "gelim_drbt_gemv": (_int, [_vp, _i64, _i64, _i64, _vp, _vp, _dbl, _vp]),

@@ -19,19 +19,29 @@ is padded with an identity block to np, a multiple of 512 P: then every
 butterfly column group {j, j + np/4, j + np/2, j + 3np/4} lies on one rank
 and the transform M = U^T A V is local (csrc/hip/dist_rbt.hip).
 
-Factorisation (block k, owner o = k % P; the single-GPU factor_impl's steps):
-  owner:      broadcast M_{>=k,k}, its column from the diagonal block down
-              ((np - 128 k) x 128), as soon as it is up to date; THEN
-              Dinv_k = M_kk^-1 (Gauss-Jordan, one workgroup) and broadcast
-              the 128 x 128 inverse -- the big transfer runs under the inverse
-  every rank: W = Dinv_k M_{k, own cols > k};  M_{>k, own cols > k} -= M_{>k,k} W
+Storage: column-block-major -- local block lb is its own contiguous np x 128
+slab Mb[lb], so the column of block k from its diagonal block down is ONE
+contiguous buffer and goes out in an in-place broadcast (no pack copy).  The
+owner inverts the diagonal block IN PLACE: the slab's diagonal block holds
+Dinv_k afterwards (the block-LDU factor never needs A_kk again), so the column
+message is [Dinv_k; L_{k+1,k}; L_{k+2,k}; ...].
+
+Factorisation (block k, owner o = k % P), two messages per block:
+  small_k = [Dinv_k; L_{k+1,k}]   (256 x 128: all the next owner needs to
+                                   update and invert its diagonal block)
+  bulk_k  = L_{k+2.., k}          (the rest of the column, off the chain)
+  owner of k+1 (main stream): wait small_k; W = Dinv_k M[k, k+1];
+      M[k+1, k+1] -= L_{k+1,k} W; Dinv_{k+1} = M[k+1,k+1]^-1 in place (the
+      chain: it needs nothing of bulk_k); then wait bulk_k;
+      M[k+2.., k+1] -= L_{k+2..,k} W; broadcast small_{k+1}, bulk_{k+1}
+  every rank (side stream): wait small_k + bulk_k; W = Dinv_k M[k, own
+      cols]; M[>k, own cols] -= L_k W (its next block first, so the chain of
+      the next step never waits for the rest)
 The off-diagonal blocks stay in place as the block-LDU factor, the inverses
-with their owners.  Lookahead on two streams (DistributedGauss's scheme): the
-owner of k+1 applies panel k to block k+1 first on the main stream and ships
-block k+1, while the side stream applies panel k to the rest; broadcast
-buffers rotate over three slots.  Critical path per block: max(column
-transfer, inverse + one small broadcast) + the 128-wide update of the next
-block (profiles/dist_rbt_8rank_critical_path.md).
+on their diagonal blocks.  Three landing buffers rotate on the receivers.
+Critical path per block: small-message latency + two 128^3 GEMMs + the
+inverse (+ the column rest when the bulk is late)
+(profiles/dist_rbt_8rank_critical_path.md).
 
 Solves (every apply of (LU)^-1, replicated vectors): super-blocks of P
 blocks -- one block per rank, the same local block index s on every rank.
@@ -136,8 +146,12 @@ class DistributedRBT:
         # libgelim's native RCCL or no collective at all (gloo and the
         # emulated ranks meet on the host; torch's ProcessGroupNCCL watchdog
         # aborts on collectives recorded during a capture).
-        self.graph = graph and self.gpu and lookahead and (comm.backend == "none" or comm.native)
+        self.graph = graph and self.gpu and lookahead and (comm.backend == "none" or comm.native
+                                                           or getattr(comm, "capturable", False))
         self._graphs: dict[str, torch.cuda.CUDAGraph | None] = {}
+        # CUs the side stream's bulk trailing GEMM may take (0: all); a cap
+        # leaves CUs free for the chain's small kernels
+        self.side_cap = 0
         self.last_issue_s = None
         self._ud, self._vd = butterfly_diagonals(self.np, seed)
         lb = torch.arange(self.nloc) // NB
@@ -161,13 +175,14 @@ class DistributedRBT:
             return
         self.ud = torch.from_numpy(self._ud).to(dev)
         self.vd = torch.from_numpy(self._vd).to(dev)
-        self.M = torch.zeros((self.np, self.ld), **f64)
+        # column-block-major: slab lb = local block lb's np x 128 columns
+        self.Mb = torch.zeros((self.nbl, self.np, NB), **f64)
+        self.mbs = self.np * NB  # doubles between slabs
         self._Fs = self._Ds = None
         self._ain = torch.zeros(self.np, **f64)  # apply's input, captured by address
-        self.Dinv = torch.zeros((self.nbl, NB, NB), **f64)
         nbuf = NBUF if lookahead else 2
-        self._xbufs = [torch.zeros(self.np * NB, **f64) for _ in range(nbuf)]  # column k from the diagonal down
-        self._dbufs = [torch.zeros(NB * NB, **f64) for _ in range(nbuf)]       # its diagonal block's inverse
+        # landing buffers of the column messages [Dinv_k; L_k] (non-owners)
+        self._xbufs = [torch.zeros(self.np * NB, **f64) for _ in range(nbuf)]
         self._Wm = torch.zeros((NB, NB), **f64)
         self._Ws = torch.zeros((NB, self.nloc), **f64)
         self._info = torch.full((1,), 0x7F7F7F7F, dtype=torch.int32, device=dev)
@@ -234,70 +249,98 @@ class DistributedRBT:
 
     def _transform(self, loc: torch.Tensor) -> None:
         if self.gpu:
-            _native.check(_native.lib().gelim_drbt_transform(ptr(loc), self.ld, ptr(self.M), self.ld, self.np,
+            _native.check(_native.lib().gelim_drbt_transform(ptr(loc), self.ld, ptr(self.Mb), NB, self.mbs, self.np,
                                                              self.nloc, self.P, self.rank, ptr(self.ud), ptr(self.vd),
                                                              self._sh()), "drbt_transform")
         else:
-            self.M[:, :self.nloc] = self._Wu.T @ loc[:, :self.nloc] @ self._Wv_loc
+            Mc = self._Wu.T @ loc[:, :self.nloc] @ self._Wv_loc
+            self.Mb.copy_(Mc.view(self.np, self.nbl, NB).permute(1, 0, 2))
 
-    def _inverse(self, k: int, out: torch.Tensor) -> None:
-        lc = (k // self.P) * NB
-        blk = self.M[k * NB:(k + 1) * NB, lc:lc + NB]
+    def _col(self, k: int) -> torch.Tensor:
+        """Column k from its diagonal block down, (np - 128 k) x 128, on this
+        rank: the owner's slab, or the landing buffer of its message."""
+        m = self.np - k * NB
+        if k % self.P == self.rank:
+            return self.Mb[k // self.P, k * NB:]
+        return self._xbufs[k % len(self._xbufs)][:m * NB].view(m, NB)
+
+    def _invert(self, k: int) -> None:
+        """Owner of block k: Dinv_k = A_kk^-1 in place on the slab's diagonal
+        block (kept there for the solves and sent as the head of column k)."""
+        blk = self.Mb[k // self.P, k * NB:(k + 1) * NB]
         if self.gpu:
-            _native.check(_native.lib().gelim_rbt_block_inverse(ptr(blk), self.ld, k * NB, ptr(out),
-                                                                ptr(self._info), self._sh()), "rbt_block_inverse")
+            _native.check(_native.lib().gelim_rbt_block_inverse(ptr(blk), NB, k * NB, ptr(blk), ptr(self._info),
+                                                                self._sh()), "rbt_block_inverse")
         else:
             inv = torch.linalg.inv(blk)
             if not bool(torch.isfinite(inv).all()):
                 self._info.fill_(min(int(self._info.item()), k * NB + 1))
-            out.copy_(inv)
+            blk.copy_(inv)
 
-    def _gemm(self, C: torch.Tensor, A: torch.Tensor, B: torch.Tensor, alpha: float, acc: bool, stream=None) -> None:
-        """C (+)= alpha A B on 2-D row-major views."""
-        M_, N_ = C.shape
-        K_ = A.shape[1]
-        if M_ == 0 or N_ == 0:
+    def _gemm_bm(self, C: torch.Tensor, cbm: bool, A: torch.Tensor, B: torch.Tensor, bbm: bool, ncols: int,
+                 alpha: float, acc: bool, stream=None, cap: int = 0) -> None:
+        """C (+)= alpha A B over ncols columns.  bbm / cbm: B / C is a run of
+        column-block-major slabs starting at the given 2-D view (rows x 128
+        each, slab stride mbs); otherwise a plain row-major 2-D view."""
+        M_, K_ = A.shape[0], A.shape[1]
+        if M_ == 0 or ncols == 0:
             return
         if self.gpu:
-            _native.check(_native.lib().gelim_gpu_dgemm_ex(ptr(C), C.stride(0), ptr(A), A.stride(0), ptr(B),
-                                                           B.stride(0), M_, N_, K_, alpha, int(acc), 0,
-                                                           self._sh(stream)), "dgemm_ex")
-        elif acc:
-            C.add_(A @ B, alpha=alpha)
-        else:
-            torch.matmul(A, B, out=C)
-            if alpha != 1.0:
-                C.mul_(alpha)
-
-    def _apply_panel(self, k: int, xb: torch.Tensor, db: torch.Tensor, cb: int, ce: int, W: torch.Tensor,
-                     stream=None) -> None:
-        """Panel k (xb = column k from the diagonal block down, db = the
-        inverse of that diagonal block) applied to local columns [cb, ce):
-        W = Dinv_k M[k, cb:ce];  M[>k, cb:ce] -= L_k W."""
-        if ce <= cb:
+            _native.check(_native.lib().gelim_gpu_dgemm_bm(
+                ptr(C), C.stride(0), self.mbs if cbm else 0, ptr(A), A.stride(0), ptr(B), B.stride(0),
+                self.mbs if bbm else 0, M_, ncols, K_, alpha, int(acc), cap, self._sh(stream)), "dgemm_bm")
             return
-        m = self.np - (k + 1) * NB
-        Dk = db.view(NB, NB)
-        Wv = W[:, :ce - cb]
-        self._gemm(Wv, Dk, self.M[k * NB:(k + 1) * NB, cb:ce], 1.0, False, stream)
-        if m > 0:
-            L = xb[NB * NB:NB * NB + m * NB].view(m, NB)
-            self._gemm(self.M[(k + 1) * NB:, cb:ce], L, Wv, -1.0, True, stream)
+        nbk = ncols // NB
 
-    def _pack_col(self, k: int, xb: torch.Tensor) -> None:
-        """Owner of block k: its column from the diagonal block down, contiguous."""
-        lb = k // self.P
-        m = self.np - k * NB
-        xb[:m * NB].view(m, NB).copy_(self.M[k * NB:, lb * NB:(lb + 1) * NB])
+        def slab(T: torch.Tensor, j: int, rows: int) -> torch.Tensor:  # block j of a slab run
+            return T.as_strided((rows, NB), (T.stride(0), 1), T.storage_offset() + j * self.mbs)
 
-    def _invert(self, k: int, db: torch.Tensor) -> None:
-        """Owner of block k: Dinv_k (kept for the solves) into the broadcast buffer."""
-        lb = k // self.P
-        self._inverse(k, self.Dinv[lb])
-        db.copy_(self.Dinv[lb].view(-1))
+        Bc = torch.cat([slab(B, j, K_) for j in range(nbk)], dim=1) if bbm else B[:, :ncols]
+        prod = A @ Bc
+        if alpha != 1.0:
+            prod = prod * alpha
+        if cbm:
+            for j in range(nbk):
+                Cj = slab(C, j, M_)
+                if acc:
+                    Cj.add_(prod[:, j * NB:(j + 1) * NB])
+                else:
+                    Cj.copy_(prod[:, j * NB:(j + 1) * NB])
+        elif acc:
+            C[:, :ncols].add_(prod)
+        else:
+            C[:, :ncols].copy_(prod)
 
-    def _xsize(self, k: int) -> int:
-        return (self.np - k * NB) * NB
+    def _panel_w(self, k: int, col: torch.Tensor, lb0: int, lb1: int, W: torch.Tensor, stream=None,
+                 cap: int = 0) -> None:
+        """W[:, :128 (lb1 - lb0)] = Dinv_k M[k, local blocks lb0 .. lb1)."""
+        if lb1 > lb0:
+            self._gemm_bm(W, False, col[:NB], self.Mb[lb0, k * NB:(k + 1) * NB], True, (lb1 - lb0) * NB, 1.0,
+                          False, stream, cap)
+
+    def _panel_rows(self, k: int, col: torch.Tensor, lb0: int, lb1: int, r0: int, r1: int, W: torch.Tensor,
+                    stream=None, cap: int = 0) -> None:
+        """M[r0:r1, local blocks lb0 .. lb1) -= L_k[r0:r1] W (global rows
+        r0 > 128 k; col row 0 is global row 128 k)."""
+        if lb1 > lb0 and r1 > r0:
+            self._gemm_bm(self.Mb[lb0, r0:r1], True, col[r0 - k * NB:r1 - k * NB], W, False, (lb1 - lb0) * NB,
+                          -1.0, True, stream, cap)
+
+    def _apply_panel(self, k: int, col: torch.Tensor, lb0: int, lb1: int, W: torch.Tensor, stream=None,
+                     cap: int = 0) -> None:
+        """Panel k applied to local blocks [lb0, lb1), every row below block k
+        (cap > 0: the trailing GEMM on at most `cap` CUs)."""
+        if lb1 > lb0:
+            self._panel_w(k, col, lb0, lb1, W, stream)
+            self._panel_rows(k, col, lb0, lb1, (k + 1) * NB, self.np, W, stream, cap)
+
+    def _first_lb_after(self, k: int) -> int:
+        """This rank's first local block with global index > k."""
+        return min(self.nbl, max(0, -(-(k + 1 - self.rank) // self.P)))
+
+    def _small(self, k: int) -> int:
+        """Rows of the chain message of block k: Dinv_k and L_{k+1,k}."""
+        return min(2 * NB, self.np - k * NB)
 
     # -- factorisation --------------------------------------------------------
     def factor_(self, loc: torch.Tensor) -> int:
@@ -317,79 +360,101 @@ class DistributedRBT:
         return 0 if val == 0x7F7F7F7F else val
 
     def _factor_serial(self) -> None:
+        """One stream, one broadcast per block: the whole column message
+        [Dinv_k; L_k], then every rank applies panel k to its later blocks."""
         comm, r, P = self.comm, self.rank, self.P
         for k in range(self.nb):
-            xb, db = self._xbufs[k & 1], self._dbufs[k & 1]
             o = k % P
             if r == o:
-                self._pack_col(k, xb)
-                self._invert(k, db)
-            comm.broadcast(xb[:self._xsize(k)], src=o)
-            comm.broadcast(db, src=o)
-            self._apply_panel(k, xb, db, self._first_col_after(k), self.nloc, self._Ws)
-
-    def _first_col_after(self, k: int) -> int:
-        """Local column offset of this rank's first block with global index > k."""
-        q = max(0, -(-(k + 1 - self.rank) // self.P))
-        return min(q * NB, self.nloc)
+                self._invert(k)
+            col = self._col(k)
+            comm.broadcast(col.reshape(-1), src=o)
+            self._apply_panel(k, col, self._first_lb_after(k), self.nbl, self._Ws)
 
     def _factor_lookahead(self) -> None:
-        """Two streams and TWO broadcasts per block (module docstring).  The
-        owner of block k+1 ships its column (diagonal block down) as soon as
-        panel k has reached it, and only then inverts the diagonal block and
-        ships the 128 x 128 inverse: the big transfer runs under the inverse,
-        so a block costs max(transfer, inverse) on the critical path instead
-        of their sum.
-          main (owner of k+1): [wait column k, Dinv_k] [panel k -> block k+1]
-                               [pack column k+1, bcast] [invert k+1, bcast]
-          side (every rank):   [wait panel k] [panel k -> the next block this
-                               rank owns after k+1] (ev_first) [the rest] (ev_rest)"""
+        """Two streams, two broadcasts per block (module docstring).
+          main (owner of k+1): [wait small_k] W = Dinv_k M[k, k+1];
+               M[k+1, k+1] -= L_{k+1,k} W; invert it in place;
+               [wait bulk_k] M[k+2.., k+1] -= L_{k+2..,k} W;
+               broadcast small_{k+1}, bulk_{k+1}
+          side (every rank): [wait small_k + bulk_k] panel k -> the next block
+               this rank owns after k+1 (ev_first), then the rest (ev_rest)
+        The chain (small_k -> two 128^3 GEMMs -> inverse) never waits for a
+        bulk transfer unless that transfer is longer than the inverse."""
         comm, r, P, nb = self.comm, self.rank, self.P, self.nb
         main = torch.cuda.current_stream(self.device)
         side = self._side
-        side.wait_stream(main)  # M as the transform left it
-        X, D = self._xbufs, self._dbufs
-        nbuf = len(X)
-        ev_avail = [torch.cuda.Event() for _ in range(nb)]
+        side.wait_stream(main)  # Mb as the transform left it
+        nbuf = len(self._xbufs)
+        ev_issue = [torch.cuda.Event() for _ in range(nb)]
         ev_first = [torch.cuda.Event() for _ in range(nb)]
         ev_rest = [torch.cuda.Event() for _ in range(nb)]
-        hx, hd = {}, {}
+        hs, hb = {}, {}
 
-        def ship(k: int) -> None:  # every rank: the two broadcasts of block k, in this order
-            o = k % P
-            if r == o:
-                self._pack_col(k, X[k % nbuf])
-            hx[k] = comm.broadcast_async(X[k % nbuf][:self._xsize(k)], src=o)
-            if r == o:
-                self._invert(k, D[k % nbuf])
-            hd[k] = comm.broadcast_async(D[k % nbuf], src=o)
+        def ship(k: int) -> None:
+            hs[k], hb[k] = self._ship(k)
+            ev_issue[k].record(main)  # host-rendezvous transports land the data on main
 
+        if r == 0:
+            self._invert(0)
+        else:
+            self._foreign_chain(-1, None, None)
         ship(0)
         for k in range(nb):
-            xb, db = X[k % nbuf], D[k % nbuf]
-            hx.pop(k).wait()
-            hd.pop(k).wait()  # main waits for panel k
-            ev_avail[k].record(main)
-            c0 = self._first_col_after(k)
-            nxt = k + 1 < nb
-            o1 = (k + 1) % P if nxt else -1
-            cs = c0 + (NB if o1 == r else 0)  # block k+1 is main's
-            wf = NB if cs < self.nloc else 0
-            side.wait_event(ev_avail[k])
+            col = self._col(k)
+            hs[k].wait()  # main: the chain message of block k
+            side.wait_event(ev_issue[k])
             with torch.cuda.stream(side):
-                self._apply_panel(k, xb, db, cs, cs + wf, self._Ws, side)
+                hs[k].wait()  # side: all of column k
+                if hb[k] is not None:
+                    hb[k].wait()
+                lb0 = self._first_lb_after(k)
+                nxt = k + 1 < nb
+                o1 = (k + 1) % P if nxt else -1
+                ls = lb0 + (1 if o1 == r else 0)  # block k+1 is main's
+                lf = min(ls + 1, self.nbl)
+                self._apply_panel(k, col, ls, lf, self._Ws, side)
                 ev_first[k].record(side)
-                self._apply_panel(k, xb, db, cs + wf, self.nloc, self._Ws, side)
+                self._apply_panel(k, col, lf, self.nbl, self._Ws[:, (lf - ls) * NB:], side, self.side_cap)
                 ev_rest[k].record(side)
+            self._foreign_side(k, col, hs[k], hb[k])
+            if not nxt:
+                break
             if o1 == r:
+                lb = lb0  # local block of k+1
                 if k >= 1:
-                    main.wait_event(ev_first[k - 1])  # panel k-1 reached block k+1 on the side stream
-                self._apply_panel(k, xb, db, c0, c0 + NB, self._Wm)
-            if nxt:
-                if k + 1 >= nbuf:
-                    main.wait_event(ev_rest[k + 1 - nbuf])  # the buffer slots of k+1 are free again
-                ship(k + 1)
+                    main.wait_event(ev_first[k - 1])  # panel k-1 reached block k+1 (side stream)
+                self._panel_w(k, col, lb, lb + 1, self._Wm)
+                self._panel_rows(k, col, lb, lb + 1, (k + 1) * NB, (k + 2) * NB, self._Wm)  # its diagonal block
+                self._invert(k + 1)
+                if hb[k] is not None:
+                    hb[k].wait()  # main: L_{k+2.., k}
+                    self._panel_rows(k, col, lb, lb + 1, (k + 2) * NB, self.np, self._Wm)
+            else:
+                self._foreign_chain(k, col, hb[k])
+            if k + 1 >= nbuf:
+                main.wait_event(ev_rest[k + 1 - nbuf])  # the landing buffer of k+1 is free again
+            ship(k + 1)
         main.wait_event(ev_rest[nb - 1])
+
+    def _ship(self, k: int):
+        """Every rank: the two broadcasts of block k (the owner's slab in
+        place): (handle of small_k, handle of bulk_k or None)."""
+        o = k % self.P
+        col = self._col(k).reshape(-1)
+        sm = self._small(k) * NB
+        hs = self.comm.broadcast_async(col[:sm], src=o)
+        hb = self.comm.broadcast_async(col[sm:], src=o) if col.numel() > sm else None
+        return hs, hb
+
+    def _foreign_chain(self, k: int, col, hb) -> None:
+        """Hook: the chain step that produces block k+1 runs on ANOTHER rank
+        (nothing to do here; scripts/one_rank_of_p.py replays it on this GPU
+        to measure one rank of a P-rank run)."""
+
+    def _foreign_side(self, k: int, col, hs, hb) -> None:
+        """Hook: panel k applied to block k+2 by ITS owner's side stream, when
+        that owner is another rank (scripts/one_rank_of_p.py)."""
 
     # -- solves ----------------------------------------------------------------
     def _gather_solve_blocks(self) -> None:
@@ -397,8 +462,11 @@ class DistributedRBT:
         diagonal-block inverse (one all_gather each)."""
         P, S, ns = self.P, NB * self.P, self.nbl
         mine = torch.empty((ns, S, NB), dtype=torch.float64, device=self.device)
+        dmine = torch.empty((ns, NB, NB), dtype=torch.float64, device=self.device)
         for s in range(ns):
-            mine[s] = self.M[s * S:(s + 1) * S, s * NB:(s + 1) * NB]
+            mine[s] = self.Mb[s, s * S:(s + 1) * S]
+            gb = s * P + self.rank  # global block of local block s: its inverse sits on its diagonal block
+            dmine[s] = self.Mb[s, gb * NB:(gb + 1) * NB]
         g = torch.empty((P, ns, S, NB), dtype=torch.float64, device=self.device)
         self.comm.all_gather(g.view(-1), mine.view(-1))
         if getattr(self, "_Fs", None) is None:  # persistent: a captured apply reads them by address
@@ -406,9 +474,9 @@ class DistributedRBT:
             self._Ds = torch.empty((ns, P, NB, NB), dtype=torch.float64, device=self.device)
         self._Fs.copy_(g.permute(1, 2, 0, 3).reshape(ns, S, S))
         gd = torch.empty((P, ns, NB, NB), dtype=torch.float64, device=self.device)
-        self.comm.all_gather(gd.view(-1), self.Dinv.contiguous().view(-1))
+        self.comm.all_gather(gd.view(-1), dmine.view(-1))
         self._Ds.copy_(gd.permute(1, 0, 2, 3))  # (ns, P, 128, 128)
-        del mine, g, gd
+        del mine, dmine, g, gd
 
     def _super_solve(self, s: int, rhs: torch.Tensor, x: torch.Tensor, ysave: torch.Tensor | None,
                      upper: bool) -> None:
@@ -504,7 +572,7 @@ class DistributedRBT:
             self._super_solve(s, c[R] - t, z[R], y[R], False)
             if s + 1 < ns:
                 zb = z[s * S + r * NB:s * S + (r + 1) * NB]
-                self._gemv(self.M[(s + 1) * S:, s * NB:(s + 1) * NB], zb, acc[(s + 1) * S:])
+                self._gemv(self.Mb[s, (s + 1) * S:], zb, acc[(s + 1) * S:])
         xs = torch.empty_like(c)
         acc.zero_()
         for s in reversed(range(ns)):
@@ -514,7 +582,7 @@ class DistributedRBT:
             self._super_solve(s, y[R] - t, xs[R], None, True)
             if s > 0:
                 xb = xs[s * S + r * NB:s * S + (r + 1) * NB]
-                self._gemv(self.M[:s * S, s * NB:(s + 1) * NB], xb, acc[:s * S])
+                self._gemv(self.Mb[s, :s * S], xb, acc[:s * S])
         out = torch.empty_like(c)
         self._rbt_vec(xs, self.vd if self.gpu else None, False, out)
         return out

@@ -384,7 +384,9 @@ int dgemm_launch(double* C, int64_t ldc, const double* A, int64_t lda, const dou
     // at the block-LDU engine's K = 128 / 256 shapes, profiles/dgemm_thin_r4.txt;
     // it stays callable as gelim_gpu_dgemm_thin)
     const bool small = (int64_t)tm * tn < (int64_t)ncu;
-    if (small && cap == 0) {
+    // (capped: 64-tiles too when their grid stays within the cap)
+    const int64_t t64 = ((M + 63) / 64) * ((N + 63) / 64);
+    if (small && (cap == 0 || t64 <= cap)) {
       const int tm6 = (int)((M + 63) / 64), tn6 = (int)((N + 63) / 64);
       Args g6 = g;
       g6.tiles_n = tn6;

@@ -389,6 +389,7 @@ class Communicator:
     _cstream: object = field(default=None, repr=False, compare=False)
     key: str = "world"  # store key prefix of this communicator's native RCCL id
     _rccl: object = field(default=None, repr=False, compare=False)
+    _rccl_aux: object = field(default=None, repr=False, compare=False)
 
     # -- collectives ------------------------------------------------------
     @property
@@ -408,6 +409,19 @@ class Communicator:
         if self._rccl is None:
             self._rccl = NativeRccl(f"gelim_rccl/{self.key}", self.world_size, self.rank, self.device)
         return self._rccl
+
+    def rccl_aux(self, name: str) -> NativeRccl:
+        """A further native communicator over the same ranks (collective:
+        every rank asks for the same names in the same order).  Two
+        communicators progress independently, so a collective on one never
+        waits behind a long one on the other (DistributedRBT: the chain's
+        small messages beside the bulk columns)."""
+        if self._rccl_aux is None:
+            self._rccl_aux = {}
+        if name not in self._rccl_aux:
+            self._rccl_aux[name] = NativeRccl(f"gelim_rccl/{self.key}/{name}", self.world_size, self.rank,
+                                              self.device)
+        return self._rccl_aux[name]
 
     def comm_stream(self) -> torch.cuda.Stream:
         """The stream this rank's asynchronous collectives run on: a

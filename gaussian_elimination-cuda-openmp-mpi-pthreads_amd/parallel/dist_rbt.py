@@ -114,11 +114,24 @@ def butterfly_dense(d: np.ndarray, npad: int) -> torch.Tensor:
     return torch.from_numpy(W)
 
 
+import ctypes as _C
+
+
+class _ExecArgs(_C.Structure):
+    """gelim_drbt_args of csrc/hip/drbt_exec.hip (keep in sync)."""
+    _fields_ = [("np", _C.c_int64), ("nloc", _C.c_int64), ("P", _C.c_int32), ("rank", _C.c_int32),
+                ("Mb", _C.c_void_p), ("mbs", _C.c_int64), ("X", _C.c_void_p * 3), ("Wm", _C.c_void_p),
+                ("Ws", _C.c_void_p), ("info", _C.c_void_p), ("main", _C.c_void_p), ("side", _C.c_void_p),
+                ("comm", _C.c_void_p), ("rccl_small", _C.c_void_p), ("rccl_bulk", _C.c_void_p),
+                ("side_cap", _C.c_int32), ("replay", _C.c_int32), ("F", _C.c_void_p * 3), ("aux", _C.c_void_p),
+                ("Wf", _C.c_void_p), ("Wfs", _C.c_void_p), ("finfo", _C.c_void_p)]
+
+
 class DistributedRBT:
     """Randomised block-LDU solve of one n x n system over all ranks of comm."""
 
     def __init__(self, comm: Communicator, n: int, seed: int = SEED, lookahead: bool = True,
-                 single_fast_path: bool = True, max_steps: int = 6, graph: bool = True):
+                 single_fast_path: bool = True, max_steps: int = 6, graph: bool = True, native_exec: bool = True):
         self.comm, self.n = comm, n
         self.P, self.rank = comm.world_size, comm.rank
         self.device = comm.device
@@ -149,6 +162,13 @@ class DistributedRBT:
         self.graph = graph and self.gpu and lookahead and (comm.backend == "none" or comm.native
                                                            or getattr(comm, "capturable", False))
         self._graphs: dict[str, torch.cuda.CUDAGraph | None] = {}
+        # the lookahead factorisation issued natively (csrc/hip/drbt_exec.hip)
+        # wherever every collective is libgelim's own RCCL (or there is none):
+        # ~30 us of host time per block on the probed streams, instead of a
+        # Python loop or a hipGraph whose replay remaps the streams' queues
+        self.native_exec = (native_exec and self.gpu and lookahead
+                            and (comm.backend == "none" or comm.native or getattr(comm, "capturable", False)))
+        self._exec = None
         # CUs the side stream's bulk trailing GEMM may take (0: all); a cap
         # leaves CUs free for the chain's small kernels
         self.side_cap = 0
@@ -348,7 +368,11 @@ class DistributedRBT:
         column whose diagonal-block inverse is not finite (min over ranks)."""
         self._info.fill_(0x7F7F7F7F)
         self._transform(loc)
-        if self.lookahead and self.gpu:
+        if self.native_exec:
+            t0 = time.perf_counter()
+            self._factor_native()
+            self.last_issue_s = time.perf_counter() - t0
+        elif self.lookahead and self.gpu:
             t0 = time.perf_counter()
             self._replay("factor", self._factor_lookahead)
             self.last_issue_s = time.perf_counter() - t0  # host time to issue (or replay) the schedule
@@ -358,6 +382,37 @@ class DistributedRBT:
         self.comm.all_reduce(v, "min")
         val = int(self.comm.item(v))
         return 0 if val == 0x7F7F7F7F else val
+
+    def _exec_args(self) -> _ExecArgs:
+        a = _ExecArgs()
+        a.np, a.nloc, a.P, a.rank = self.np, self.nloc, self.P, self.rank
+        a.Mb, a.mbs = ptr(self.Mb), self.mbs
+        for i, x in enumerate(self._xbufs):
+            a.X[i] = ptr(x)
+        a.Wm, a.Ws, a.info = ptr(self._Wm), ptr(self._Ws), ptr(self._info)
+        a.main = torch.cuda.current_stream(self.device).cuda_stream
+        a.side = self._side.cuda_stream
+        a.comm = self.comm.comm_stream().cuda_stream
+        if self.comm.native:
+            a.rccl_small = self.comm.rccl_aux("small").handle
+            a.rccl_bulk = self.comm.rccl().handle
+        a.side_cap = self.side_cap
+        return a
+
+    def _factor_native(self) -> None:
+        """The lookahead schedule of _factor_lookahead, issued by
+        gelim_drbt_factor (csrc/hip/drbt_exec.hip): small messages on the
+        main stream through a communicator of their own, bulk columns on the
+        communicator stream through another."""
+        lib = _native.lib()
+        if self._exec is None:
+            self._exec = lib.gelim_drbt_exec_create()
+        a = self._exec_args()
+        self._patch_exec_args(a)
+        _native.check(lib.gelim_drbt_factor(self._exec, _C.byref(a)), "drbt_factor")
+
+    def _patch_exec_args(self, a: _ExecArgs) -> None:
+        """Hook (scripts/one_rank_of_p.py: the replay buffers)."""
 
     def _factor_serial(self) -> None:
         """One stream, one broadcast per block: the whole column message
@@ -710,3 +765,8 @@ class DistributedRBT:
         if self._plan:
             _native.lib().gelim_mixed_plan_destroy(self._plan)
             self._plan = None
+        if getattr(self, "_exec", None):
+            if self.gpu:
+                torch.cuda.synchronize(self.device)  # its events may still be in flight
+            _native.lib().gelim_drbt_exec_destroy(self._exec)
+            self._exec = None

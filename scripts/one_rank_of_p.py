@@ -102,8 +102,8 @@ class OneRankOfP(DistributedRBT):
     """DistributedRBT as rank r of P, with the other ranks' chain work
     replayed here (see the module docstring)."""
 
-    def __init__(self, comm: ReplayComm, n: int, graph: bool = True):
-        super().__init__(comm, n, single_fast_path=False, graph=graph)
+    def __init__(self, comm: ReplayComm, n: int, graph: bool = True, native_exec: bool = True):
+        super().__init__(comm, n, single_fast_path=False, graph=graph, native_exec=native_exec)
         dev = self.device
         self._fs = [torch.randn(self.np, NB, dtype=torch.float64, device=dev) for _ in range(3)]
         self._Wf = torch.zeros((NB, NB), dtype=torch.float64, device=dev)
@@ -112,6 +112,15 @@ class OneRankOfP(DistributedRBT):
         self._aux = dedicated_stream(dev, "aux")
         self._side_ev: dict[int, torch.cuda.Event] = {}
         self._ship_ev: dict[int, list] = {}
+
+    def _patch_exec_args(self, a) -> None:
+        """The native executor's replay mode (csrc/hip/drbt_exec.hip): the
+        same foreign chain steps and copies as the hooks below."""
+        a.replay = 1
+        for i, f in enumerate(self._fs):
+            a.F[i] = ptr(f)
+        a.aux = self._aux.cuda_stream
+        a.Wf, a.Wfs, a.finfo = ptr(self._Wf), ptr(self._Wfs), ptr(self._finfo)
 
     def _inv(self, blk: torch.Tensor, col: int) -> None:
         _native.check(_native.lib().gelim_rbt_block_inverse(ptr(blk), NB, col, ptr(blk), ptr(self._finfo),
@@ -215,7 +224,10 @@ def main() -> None:
     ap.add_argument("--json", default=None)
     ap.add_argument("--factor-only", action="store_true",
                     help="(profiling) after the timed factorisations, one more factorisation and nothing else")
-    ap.add_argument("--no-graph", action="store_true", help="issue the schedule eagerly (no hipGraph replay)")
+    ap.add_argument("--no-graph", action="store_true", help="Python schedule: issue eagerly (no hipGraph replay)")
+    ap.add_argument("--python-schedule", action="store_true",
+                    help="the Python lookahead loop (hipGraph-replayed unless --no-graph) instead of the native "
+                         "executor")
     ap.add_argument("--side-cap", type=int, default=None,
                     help="CUs the side stream's trailing GEMMs may use (default: the solver's choice)")
     a = ap.parse_args()
@@ -223,13 +235,14 @@ def main() -> None:
         raise SystemExit(f"--rank {a.rank} is not a rank of P = {a.P}")
     dev = torch.device("cuda:0")
     comm = ReplayComm(a.P, a.rank, dev)
-    d = OneRankOfP(comm, a.n, graph=not a.no_graph)
+    d = OneRankOfP(comm, a.n, graph=not a.no_graph, native_exec=not a.python_schedule)
     if a.side_cap is not None:
         d.side_cap = a.side_cap
     loc = d.generate_random(seed=5)
     for _ in range(3):  # eager, captured, replayed
         d.factor_(loc)
-    assert a.no_graph or (d.graph and d._graphs.get("factor") is not None), "the factorisation was not captured"
+    assert (not a.python_schedule or a.no_graph or (d.graph and d._graphs.get("factor") is not None)), \
+        "the factorisation was not captured"
     tf = time_it(lambda: d.factor_(loc), a.reps)
     if a.factor_only:
         time.sleep(0.05)
@@ -249,6 +262,7 @@ def main() -> None:
     tfm, tam, trm = min(tf), min(ta), min(tr)
     chain_step = tfm / d.nb
     res = {"n": a.n, "P": a.P, "rank": a.rank, "np": d.np, "blocks": d.nb, "graph": d.graph,
+           "schedule": "native executor" if d.native_exec else "python", "issue_ms": (d.last_issue_s or 0) * 1e3,
            "factor_ms": [round(t * 1e3, 3) for t in tf], "apply_ms": [round(t * 1e3, 3) for t in ta],
            "residual_ms": [round(t * 1e3, 3) for t in tr], "factor_min_ms": tfm * 1e3, "apply_min_ms": tam * 1e3,
            "residual_min_ms": trm * 1e3, "factor_per_block_us": chain_step * 1e6,

@@ -154,11 +154,16 @@ def test_graph_replay_matches_eager(gelim, cuda, n):
     from gelim.parallel.comm import Communicator
 
     comm = Communicator(0, 1, cuda, "none")
-    d = DistributedRBT(comm, n, single_fast_path=False)
+    d = DistributedRBT(comm, n, single_fast_path=False, native_exec=False)  # the Python loop, captured
     assert d.graph
     xs = [d.solve_(d.generate_random(seed=n)).cpu() for _ in range(4)]
     assert set(d._graphs) == {"factor", "apply"} and all(v is not None for v in d._graphs.values())
-    e = DistributedRBT(comm, n, single_fast_path=False, graph=False)
+    dn = DistributedRBT(comm, n, single_fast_path=False)  # the default: native factorisation, captured applies
+    assert dn.native_exec
+    xs += [dn.solve_(dn.generate_random(seed=n)).cpu() for _ in range(3)]
+    assert set(dn._graphs) == {"apply"}
+    dn.close()
+    e = DistributedRBT(comm, n, single_fast_path=False, graph=False, native_exec=False)
     xe = e.solve_(e.generate_random(seed=n)).cpu()
     for x in xs:
         assert torch.equal(x, xe)
@@ -227,3 +232,45 @@ def test_factor_bitwise_across_ranks_and_schedules(gelim, cuda):
     assert torch.isfinite(ref).all()
     for P, la in ((1, True), (2, True), (4, True), (8, True), (4, False)):
         assert torch.equal(_global_factor(gelim, cuda, P, n, la), ref), (P, la)
+
+
+@pytest.mark.parametrize("n", [2048, 4200])
+def test_native_executor_matches_python(gelim, cuda, n):
+    """The lookahead factorisation issued natively (csrc/hip/drbt_exec.hip)
+    and by the Python loop give the same factor bits and the same solution
+    (one rank; the RCCL form is tests/test_gpu_rccl.py)."""
+    comm = Communicator(0, 1, cuda, "none")
+    out = {}
+    for nat in (True, False):
+        d = DistributedRBT(comm, n, single_fast_path=False, native_exec=nat, graph=False)
+        assert d.native_exec == nat
+        loc = d.generate_random(seed=3)
+        assert d.factor_(loc) == 0
+        torch.cuda.synchronize()
+        M = d.Mb.clone()
+        x = d.solve_(loc)
+        out[nat] = (M, x)
+        d.close()
+    assert torch.equal(out[True][0], out[False][0])
+    assert torch.equal(out[True][1], out[False][1])
+
+
+@pytest.mark.parametrize("schedule", ["native", "python"])
+def test_one_rank_of_p_replay_runs(tmp_path, schedule):
+    """scripts/one_rank_of_p.py (rank 1 of a virtual 4-rank run, the other
+    ranks' chain steps replayed on this GPU) completes and reports times."""
+    import json
+    import os
+    import subprocess
+    import sys
+    from pathlib import Path
+
+    root = Path(__file__).resolve().parents[1]
+    out = tmp_path / "orp.json"
+    cmd = [sys.executable, str(root / "scripts" / "one_rank_of_p.py"), "--n", "4096", "--P", "4", "--rank", "1",
+           "--reps", "2", "--json", str(out)] + (["--python-schedule"] if schedule == "python" else [])
+    p = subprocess.run(cmd, cwd=root, env=dict(os.environ), capture_output=True, text=True, timeout=110)
+    assert p.returncode == 0, p.stderr[-3000:]
+    res = json.loads(out.read_text())
+    assert res["blocks"] == 32 and res["factor_min_ms"] > 0 and res["apply_min_ms"] > 0
+    assert res["schedule"] == ("native executor" if schedule == "native" else "python")

@@ -142,10 +142,12 @@ __global__ __launch_bounds__(256) void rbt_vec_kernel(const double* __restrict__
 // One workgroup of 512 threads (two waves per SIMD) inverts the 128 x 128
 // block in place in registers: thread (rg, cg) = (t >> 4, t & 15) holds the
 // 4 x 8 tile rows 4 rg.., columns 8 cg...  Step k of Gauss-Jordan is ONE
-// uniform rank-1 update of the whole block,
-//   a[i][j] -= g_i u_j,  g_i = a[i][k] - [i == k],  u_j = a[k][j] / a[k][k] (j != k),  u_k = 1 + 1 / a[k][k],
+// rank-1 update of the whole block from a base with row k and column k zeroed,
+//   a'[i][j] = b_ij - G_i U_j,  G_i = a[i][k] (G_k = -1),  U_j = a[k][j] / a[k][k] (U_k = 1 / a[k][k]),
 // which gives a'[k][k] = 1/a_kk, a'[k][j] = a_kj/a_kk, a'[i][k] = -a_ik/a_kk
-// and the Schur update elsewhere with no special cases.  Row k and column k
+// and the Schur update elsewhere with no cancellation (round 6: the earlier
+// uniform form a -= g u^T with g_k = a_kk - 1, u_k = 1 + 1/a_kk lost the low
+// bits of 1/a_kk in the pivot row and column).  Row k and column k
 // are published raw through parity-buffered LDS one step ahead (one barrier
 // per PAIR of steps, below), and the step loop is unrolled by 8 so every
 // in-tile index (k % 8) is static: publishing is a predicated store, not a
@@ -221,12 +223,20 @@ __device__ __forceinline__ void gj_pair(double (&a)[TR][kTl], GjPairLds<double>&
   }
   const bool kcol = cg == kg;                   // columns k, k+1 are in this thread's tile
   const bool krow = rg == RPG * kg + KK / TR;  // rows k, k+1 are
-  u[KK] = kcol ? 1.0 + pk : u[KK];
-  g[KK % TR] -= krow ? 1.0 : 0.0;
+  // step k without cancellation: a' = b - G U^T with U_j = a_kj p (U_k = p),
+  // G_i = a_ik (G_k = -1) and the base b = a with row k and column k zeroed
+  // (the uniform form's 1 + p and a_kk - 1 lost the low bits of p: |D A - I|
+  // 1.6e-10 instead of 1.8e-13 on a cond-1e4 Schur block, which cost the
+  // refinement up to 6 corrections, profiles/rbt_seeds_r6.txt)
+  u[KK] = kcol ? pk : u[KK];
+  g[KK % TR] = krow ? -1.0 : g[KK % TR];
   // step k applied to column k+1 (rows of this tile), row k+1 (columns of
-  // this tile) and the next pivot
+  // this tile) and the next pivot; a_k,k+1 and a_k+1,k sit in the zeroed
+  // row / column, so their bases are 0
   const double uk1 = ak1 * pk;  // u[k+1]
   const double gk1 = a1k;       // g[k+1]
+  g1[KK % TR] = krow ? 0.0 : g1[KK % TR];
+  u1[KK] = kcol ? 0.0 : u1[KK];
 #pragma unroll
   for (int i = 0; i < TR; ++i) g1[i] = fma(-g[i], uk1, g1[i]);
 #pragma unroll
@@ -234,8 +244,24 @@ __device__ __forceinline__ void gj_pair(double (&a)[TR][kTl], GjPairLds<double>&
   const double pk1 = gj_recip(fma(-gk1, uk1, a11));
 #pragma unroll
   for (int j = 0; j < kTl; ++j) u1[j] *= pk1;
-  u1[KK + 1] = kcol ? 1.0 + pk1 : u1[KK + 1];
-  g1[(KK + 1) % TR] -= krow ? 1.0 : 0.0;
+  u1[KK + 1] = kcol ? pk1 : u1[KK + 1];
+  g1[(KK + 1) % TR] = krow ? -1.0 : g1[(KK + 1) % TR];
+  // row k+1 and column k+1 are step k+1's alone (base 0, no step-k term);
+  // rows / columns k and k+1 of the tile start from 0
+  g[(KK + 1) % TR] = krow ? 0.0 : g[(KK + 1) % TR];
+  u[KK + 1] = kcol ? 0.0 : u[KK + 1];
+  if (krow) {  // one wave in eight holds rows k, k+1: the others branch past
+#pragma unroll
+    for (int j = 0; j < kTl; ++j) {
+      a[KK % TR][j] = 0.0;
+      a[KK % TR + 1][j] = 0.0;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < TR; ++i) {
+    a[i][KK] = kcol ? 0.0 : a[i][KK];
+    a[i][KK + 1] = kcol ? 0.0 : a[i][KK + 1];
+  }
   // the next pair's rows / columns first, published raw
   constexpr int KN = (KK + 2) % kTl;
   constexpr int rn = KN % TR;
@@ -284,213 +310,11 @@ __device__ __forceinline__ void gj_pairs(double (&a)[TR][kTl], GjPairLds<double>
   (gj_pair<TR, 2 * KK>(a, sh, kg, rg, cg), ...);
 }
 
-// ---- accuracy check + pivoted fallback ------------------------------------------
-// Gauss-Jordan WITHOUT pivoting loses accuracy on an ill-conditioned Schur
-// block (|D A - I| 1e-10 where a pivoted inverse gives ~cond eps,
-// profiles/gj_blocked_r4.txt), and the refinement then needs 4-6 corrections
-// or stalls into the partial-pivoting fallback: 6 % of random 8192 systems
-// (profiles/rbt_seeds_r6.txt; with pivoted block inverses the same systems
-// converge in 1-3 corrections).  So every inverse is checked on one probe
-// vector, e = |D (A x) - x|_inf / |x|_inf; past kGjTol the block is redone by
-// Gauss-Jordan WITH partial pivoting (logical: rows never move, the arg-max
-// over the unused rows of each column, two barriers per column), whose
-// result F satisfies Dinv[s(r)][p(j)] = F[r][j] (p(j): pivot row of column
-// j, s(r): the column row r was pivot of).  The probe costs ~2 us; the slow
-// path only runs on the blocks that need it.
-constexpr double kGjTol = 1.0 / (1ll << 37);  // ~7e-12
-
-__device__ __forceinline__ double gj_probe_x(int j) { return 1.0 + (double)((j * 37) % 29) / 29.0; }
-
-struct alignas(16) GjPivLds {
-  double col[NB];       // column k of the working matrix
-  double row[NB];       // the pivot row
-  double candv[16];     // per-wave candidate |value| (-1: none; NaN wins)
-  int candr[16];        // and its row
-  int piv[NB];          // pivot row of column k
-  int stepof[NB];       // the column whose pivot row r was
-  double red[16];       // probe reduction
-};
-
-// a[i][j] with a run-time column j (i static) / run-time row i (j static)
-template <int TR>
-__device__ __forceinline__ double tile_col(const double (&a)[TR][kTl], int i, int j) {
-  double v = a[i][0];
-#pragma unroll
-  for (int jj = 1; jj < kTl; ++jj) v = jj == j ? a[i][jj] : v;
-  return v;
-}
-template <int TR>
-__device__ __forceinline__ double tile_row(const double (&a)[TR][kTl], int i, int j) {
-  double v = a[0][j];
-#pragma unroll
-  for (int ii = 1; ii < TR; ++ii) v = ii == i ? a[ii][j] : v;
-  return v;
-}
-
-// e = |F (A x) - x|_inf / |x|_inf for the probe x, over the whole workgroup
-// (every thread gets the same value; NaN when F is not finite)
-template <int TR>
-__device__ double gj_probe(const double (&a)[TR][kTl], const double* __restrict__ Ablk, int64_t lda, GjPivLds& ps,
-                           int t, int rg, int cg) {
-  constexpr int kThreads = 16 * NB / TR;
-  constexpr int kPer = NB * kThreads / (NB * NB) > 0 ? NB / (kThreads / NB) : NB;  // columns per thread of A x
-  // y = A x: kThreads / NB threads per row
-  {
-    const int tpr = kThreads / NB, i = t / tpr, q = t % tpr;
-    const double* src = Ablk + (int64_t)i * lda + q * kPer;
-    double y = 0.0;
-    for (int j = 0; j < kPer; ++j) y = fma(src[j], gj_probe_x(q * kPer + j), y);
-    for (int off = 1; off < tpr; off <<= 1) y += __shfl_xor(y, off, 64);
-    if (q == 0) ps.col[i] = y;
-  }
-  __syncthreads();
-  double e = 0.0;
-#pragma unroll
-  for (int i = 0; i < TR; ++i) {
-    double z = 0.0;
-#pragma unroll
-    for (int j = 0; j < kTl; ++j) z = fma(a[i][j], ps.col[kTl * cg + j], z);
-    for (int off = 1; off < 16; off <<= 1) z += __shfl_xor(z, off, 64);  // the 16 column groups of the row
-    const double d = fabs(z - gj_probe_x(TR * rg + i));
-    e = (d > e || d != d) ? d : e;  // keeps a NaN
-  }
-  for (int off = 16; off < 64; off <<= 1) {
-    const double o = __shfl_xor(e, off, 64);
-    e = (o > e || o != o) ? o : e;
-  }
-  __syncthreads();  // ps.col is reused below
-  if ((t & 63) == 0) ps.red[t >> 6] = e;
-  __syncthreads();
-  double m = 0.0;
-  for (int w = 0; w < kThreads / 64; ++w) {
-    const double o = ps.red[w];
-    m = (o > m || o != o) ? o : m;
-  }
-  __syncthreads();
-  return m / 2.0;  // |x|_inf < 2
-}
-
-// pivot candidate (|value| ov, row orow; row NB = none) beats (bv, br): NaN
-// first, then the larger value, then the lower row
-__device__ __forceinline__ bool cand_better(double ov, int orow, double bv, int br) {
-  if (orow >= NB) return false;
-  if (br >= NB) return true;
-  const bool on = ov != ov, bn = bv != bv;
-  if (on != bn) return on;
-  if (on || ov == bv) return orow < br;
-  return ov > bv;
-}
-
-// Gauss-Jordan with logical partial pivoting on the tile a (reloaded from A),
-// written permuted to Dinv (see the comment above).  Per column: the owners
-// of column k (one lane in each row group of 16) take the arg-max |value|
-// over their unused rows, the four owner lanes of a wave merge by shuffles,
-// one candidate per wave goes through LDS (barrier), every thread picks the
-// winner of the 8 (NaN wins, ties to the lower row: every column always takes
-// an unused row, so the permutation is always complete), the pivot row's
-// owners publish it (barrier), rank-1 update.
-template <int TR>
-__device__ void gj_pivoted(double (&a)[TR][kTl], const double* __restrict__ Ablk, int64_t lda,
-                           double* __restrict__ Dinv, GjPivLds& ps, int t, int rg, int cg) {
-  constexpr int kWaves = 16 * NB / TR / 64;
-#pragma unroll
-  for (int i = 0; i < TR; ++i) {
-    const double* src = Ablk + (int64_t)(TR * rg + i) * lda + kTl * cg;
-#pragma unroll
-    for (int j = 0; j < kTl; ++j) a[i][j] = src[j];
-  }
-  bool used[TR];
-#pragma unroll
-  for (int i = 0; i < TR; ++i) used[i] = false;
-  if (t < NB) {
-    ps.piv[t] = t;
-    ps.stepof[t] = t;
-  }
-  __syncthreads();
-  const int lane = t & 63, wave = t >> 6;
-  for (int k = 0; k < NB; ++k) {
-    const int kc = k / kTl, kj = k % kTl;
-    double bv = -1.0;
-    int br = NB;
-    if (cg == kc) {  // this thread holds rows TR rg.. of column k
-#pragma unroll
-      for (int i = 0; i < TR; ++i) {
-        const double v = tile_col<TR>(a, i, kj);
-        ps.col[TR * rg + i] = v;
-        const double av = fabs(v);
-        if (!used[i] && cand_better(av, TR * rg + i, bv, br)) {
-          bv = av;
-          br = TR * rg + i;
-        }
-      }
-    }
-    // merge the wave's four owner lanes (lanes kc, kc + 16, kc + 32, kc + 48)
-#pragma unroll
-    for (int off = 16; off < 64; off <<= 1) {
-      const double ov = __shfl_xor(bv, off, 64);
-      const int orow = __shfl_xor(br, off, 64);
-      if (cand_better(ov, orow, bv, br)) {
-        bv = ov;
-        br = orow;
-      }
-    }
-    if (lane == kc) {
-      ps.candv[wave] = bv;
-      ps.candr[wave] = br;
-    }
-    __syncthreads();
-    double pv = -1.0;
-    int p = NB;
-#pragma unroll
-    for (int w = 0; w < kWaves; ++w) {
-      const double v = ps.candv[w];
-      const int r = ps.candr[w];
-      if (cand_better(v, r, pv, p)) {
-        pv = v;
-        p = r;
-      }
-    }
-    p &= NB - 1;
-    if (rg == p / TR) {
-#pragma unroll
-      for (int j = 0; j < kTl; ++j) ps.row[kTl * cg + j] = tile_row<TR>(a, p % TR, j);
-    }
-    if (t == 0) {
-      ps.piv[k] = p;
-      ps.stepof[p] = k;
-    }
-    double g[TR];
-#pragma unroll
-    for (int i = 0; i < TR; ++i) {
-      g[i] = ps.col[TR * rg + i] - (TR * rg + i == p ? 1.0 : 0.0);
-      used[i] = used[i] || (TR * rg + i == p);
-    }
-    __syncthreads();
-    const double pinv = 1.0 / ps.row[k];
-    double u[kTl];
-#pragma unroll
-    for (int j = 0; j < kTl; ++j) u[j] = (kTl * cg + j == k) ? 1.0 + pinv : ps.row[kTl * cg + j] * pinv;
-#pragma unroll
-    for (int i = 0; i < TR; ++i)
-#pragma unroll
-      for (int j = 0; j < kTl; ++j) a[i][j] = fma(-g[i], u[j], a[i][j]);
-  }
-  __syncthreads();
-#pragma unroll
-  for (int i = 0; i < TR; ++i) {
-    const int r = ps.stepof[TR * rg + i] & (NB - 1);
-#pragma unroll
-    for (int j = 0; j < kTl; ++j) Dinv[(int64_t)r * NB + (ps.piv[kTl * cg + j] & (NB - 1))] = a[i][j];
-  }
-}
-
 template <int TR>
 __global__ __launch_bounds__(16 * NB / TR) void diag_inv_pair_kernel(const double* __restrict__ Ablk, int64_t lda,
                                                                     int k0, double* __restrict__ Dinv,
-                                                                    int* __restrict__ info, double tol,
-                                                                    double* __restrict__ dbg) {
+                                                                    int* __restrict__ info) {
   __shared__ GjPairLds<double> sh;
-  __shared__ GjPivLds ps;
   const int t = threadIdx.x, rg = t >> 4, cg = t & 15;
   double a[TR][kTl];
 #pragma unroll
@@ -516,23 +340,16 @@ __global__ __launch_bounds__(16 * NB / TR) void diag_inv_pair_kernel(const doubl
   __syncthreads();
   for (int kg = 0; kg < NB / kTl; ++kg)
     gj_pairs<TR>(a, sh, kg, rg, cg, std::make_integer_sequence<int, kTl / 2>{});
-  const double e = gj_probe<TR>(a, Ablk, lda, ps, t, rg, cg);
-  if (dbg && t == 0) dbg[k0 / NB] = e;  // diagnostics: the probe error of every block
-  if (!(e <= tol)) {  // inaccurate (or not finite): pivoted Gauss-Jordan
-    gj_pivoted<TR>(a, Ablk, lda, Dinv, ps, t, rg, cg);
-  } else {
-#pragma unroll
-    for (int i = 0; i < TR; ++i) {
-      double* dst = Dinv + (int64_t)(TR * rg + i) * NB + kTl * cg;
-#pragma unroll
-      for (int j = 0; j < kTl; ++j) dst[j] = a[i][j];
-    }
-  }
   bool fin = true;
 #pragma unroll
-  for (int i = 0; i < TR; ++i)
+  for (int i = 0; i < TR; ++i) {
+    double* dst = Dinv + (int64_t)(TR * rg + i) * NB + kTl * cg;
 #pragma unroll
-    for (int j = 0; j < kTl; ++j) fin = fin && isfinite(a[i][j]);
+    for (int j = 0; j < kTl; ++j) {
+      fin = fin && isfinite(a[i][j]);
+      dst[j] = a[i][j];
+    }
+  }
   if (!fin) atomicMin(info, k0 + 1);
 }
 
@@ -542,12 +359,8 @@ __global__ __launch_bounds__(16 * NB / TR) void diag_inv_pair_kernel(const doubl
 // blocked MFMA form with 16- or 32-pivot blocks -- were slower or, blocked,
 // cost the refinement extra corrections, profiles/gj_blocked_r4.txt).  `col`
 // (its first global column) only labels a non-finite result in info.
-double g_gj_tol = __builtin_inf();  // probe threshold (kGjTol once validated); < 0: always pivoted, inf: never
-double* g_gj_dbg = nullptr;  // diagnostics: device array of per-block probe errors (indexed by column / 128)
-
 int block_inv(const double* Ablk, int64_t lda, int64_t col, double* Di, int* info, hipStream_t s) {
-  hipLaunchKernelGGL((diag_inv_pair_kernel<4>), dim3(1), dim3(16 * NB / 4), 0, s, Ablk, lda, (int)col, Di, info,
-                     g_gj_tol, g_gj_dbg);
+  hipLaunchKernelGGL((diag_inv_pair_kernel<4>), dim3(1), dim3(16 * NB / 4), 0, s, Ablk, lda, (int)col, Di, info);
   HIP_TRY(hipGetLastError());
   return GELIM_OK;
 }
@@ -1551,16 +1364,6 @@ extern "C" int gelim_mixed_debug_copy(void* dst, const void* src, int64_t bytes)
 // Dinv = inverse of the 128 x 128 fp64 block at Ablk (leading dimension lda)
 // by the Gauss-Jordan kernel above; *info (device) gets atomicMin'd with
 // 1 + col when the result is not finite.
-// tests / A-B: the probe tolerance of the block inverse (< 0: always the
-// pivoted Gauss-Jordan; +inf: never); returns the previous value
-extern "C" void gelim_debug_gj_errors(double* dev_errs) { gelim::g_gj_dbg = dev_errs; }
-
-extern "C" double gelim_debug_gj_tol(double tol) {
-  const double old = gelim::g_gj_tol;
-  gelim::g_gj_tol = tol;
-  return old;
-}
-
 extern "C" int gelim_rbt_block_inverse(const double* Ablk, int64_t lda, int64_t col, double* Dinv, int* info,
                                        void* stream) {
   if (!Ablk || !Dinv || !info || lda < gelim::NB) return GELIM_FAIL(GELIM_E_ARG, "rbt_block_inverse: bad argument");

@@ -116,8 +116,6 @@ _PROTOS = {
     "gelim_gpu_residual_cw": (_int, [_vp, _i64, _i64, _vp, _vp, _vp, _vp]),
     "gelim_mixed_plan_destroy": (None, [_vp]),
     "gelim_drbt_exec_create": (_vp, []),
-    "gelim_debug_gj_tol": (_dbl, [_dbl]),
-    "gelim_debug_gj_errors": (None, [_vp]),
     "gelim_drbt_exec_destroy": (None, [_vp]),
     "gelim_drbt_factor": (_int, [_vp, _vp]),
     "gelim_mixed_factor": (_int, [_vp, _vp, _i64, _vp]),

@@ -81,7 +81,7 @@ def test_rccl_dist_rbt_bitwise(rccl_run, gelim):
     assert r["graph_rccl"] and r["graph_none"] and not r["graph_torch_path"], r
     assert r["replay_equals_eager"], r
     assert r["fallback"] is None
-    assert r["berr"] <= 64 * torch.finfo(torch.float64).eps
+    assert r["berr"] <= 4 * torch.finfo(torch.float64).eps  # the strict rule (round 6: accurate block inverses)
     x = torch.load(out / "rbt.pt")
     aug = gelim.random_system(2048, seed=43, device="cuda:0").double().cpu()
     ref = torch.linalg.solve(aug[:, :2048], aug[:, 2048])

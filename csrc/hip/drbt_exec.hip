@@ -13,20 +13,25 @@
 // calls (~30 us of host time, under the GPU chain) and every stream keeps
 // the hardware queue it was probed onto.
 //
-// Per block k (owner o = k % P), messages [Dinv_k; L_{k+1,k}] ("small",
-// the chain's) and L_{k+2..,k} ("bulk"):
-//   small: on the MAIN stream through its own communicator -- the chain
-//          (wait small -> W -> diagonal update -> inverse -> column rest ->
-//          next small) then has no cross-stream hop besides the bulk's;
-//   bulk:  on the COMM stream through a second communicator, so it travels
-//          under the chain and never delays the next small message.
-// Owner of k+1, main: W = Dinv_k M[k, k+1]; M[k+1,k+1] -= L_{k+1,k} W;
-//   Dinv_{k+1} in place; [bulk_k] M[k+2..,k+1] -= L_{k+2..,k} W; ship k+1.
-// Every rank, side: [small_k, bulk_k] panel k -> its next block (ev_first),
-//   then the rest of its columns (ev_rest).
-// The GEMMs and inverses are the Python schedule's, with the same operands
-// and shapes, so both give the same factor bits
-// (tests/test_gpu_dist_rbt.py::test_native_executor_matches_python).
+// Per block k (owner o = k % P), column k goes out as three messages:
+//   small_k = [Dinv_k; L_{k+1,k}]: on the MAIN stream through its own
+//          communicator -- the chain is small_k -> W = Dinv_k M[k, k+1] ->
+//          M[k+1,k+1] -= L_{k+1,k} W -> Dinv_{k+1} -> small_{k+1}, with no
+//          cross-stream hop but the next-row product's (below);
+//   next_k = L_{k+2,k} and rest_k = L_{k+3..,k}: on the COMM stream through a
+//          second communicator.  The owner of k+1 computes the rows they
+//          carry there too, beside its inverse: the next block row
+//          M[k+2,k+1] -= L_{k+2,k} W (from next_k; small_{k+1} waits for it),
+//          then M[k+3,k+1] (from rest_k's first block) -> next_{k+1}, then the
+//          rest -> rest_{k+1}.  So the chain never waits on the bulk of a
+//          column: rest_k has the two block steps before small_{k+2} to land.
+// Every rank, side: [small_k, next_k, rest_k] panel k -> its next block
+//   (ev_first), then the rest of its columns (ev_rest).
+// Every product has dgemm.hip's per-element operation order (the 128-wide
+// ones run as drbt_tile_kernel, bit-identical) and the inverses are the same
+// kernel, so this schedule and the Python one (two messages per column) give
+// the same factor bits (tests/test_gpu_dist_rbt.py::
+// test_native_executor_matches_python, test_chain_products_match_dgemm).
 //
 // Replay (scripts/one_rank_of_p.py): rank r of a virtual P-rank run on one
 // GPU -- every other rank's chain step runs here on a rotating scratch slab
@@ -42,6 +47,7 @@
 #include <cstdint>
 #include <vector>
 
+#include "device_common.h"
 #include "gelim/internal.h"
 
 namespace gelim {
@@ -61,7 +67,7 @@ struct gelim_drbt_args {
   double* Mb;           // nloc / 128 slabs of np x 128, mbs doubles apart
   int64_t mbs;
   double* X[3];         // landing buffers, np x 128 each
-  double* Wm;           // 128 x 128 (main)
+  double* Wm;           // 2 x 128 x 128: the chain steps' W, a ring of two
   double* Ws;           // 128 x nloc (side)
   int32_t* info;        // device: 1 + first column of a non-finite inverse (atomicMin)
   void* main;           // hipStream_t (null: the default stream)
@@ -73,20 +79,105 @@ struct gelim_drbt_args {
   int32_t replay;       // 1: replay mode (module comment)
   double* F[3];         // replay: scratch slabs np x 128
   void* aux;            // replay: the virtual owners' side stream
-  double* Wf;           // replay: 128 x 128 (main) and 128 x 128 (aux)
-  double* Wfs;
+  double* Wfs;          // replay: 128 x 128, the virtual owners' side W
   int32_t* finfo;       // replay: the scratch inverses' info word
 };
 
+namespace {
+
+// The chain's 128-wide products, C (M x 128) (+)= alpha A (M x 128) B (128 x
+// 128), as one 64-thread workgroup per 16 x 16 tile of C: M = 128 is 64
+// workgroups on 64 CUs.  A CU pulls only ~32 KB (16 rows of A, a 16-column
+// strip of B) -- the load path of one CU, not its matrix core, is what bounds
+// these products: an 8-workgroup form (16-column strips, all of A per CU, 2 x
+// 128 KB streamed) spent 15.8 k cycles just issuing its loads and ran 21 us
+// for W + D (tools/microbench/chain_stamps.hip,
+// profiles/dist_rbt_replay_r6.md), dgemm.hip's 64-tiles 8.6 us per product.
+// The loads are coalesced (a wave instruction = one 1-KB row of A, or eight
+// 128-B rows of B), all in flight at once, and pass through LDS (A row
+// stride 132 doubles: the 16 x 4 fragment reads spread over the banks); then
+// 32 v_mfma_f64_16x16x4f64 over k = 0..127 in order, A scaled by alpha
+// (+-1) on its way in, C read first -- dgemm.hip's operation order, so the
+// products are its bits (tests/test_gpu_dist_rbt.py).
+constexpr int kTileSA = 132;
+
+template <bool kAcc>
+__global__ __launch_bounds__(64) void drbt_tile_kernel(double* __restrict__ C, int64_t ldc, const double* __restrict__ A,
+                                                       int64_t lda, const double* __restrict__ B, int64_t ldb,
+                                                       double alpha) {
+  __shared__ __attribute__((aligned(16))) double as[16 * kTileSA];
+  __shared__ __attribute__((aligned(16))) double bs[128 * 16];
+  const int lane = threadIdx.x, r16 = lane & 15, q = lane >> 4;
+  const int tm = blockIdx.x >> 3, tn = blockIdx.x & 7;  // B strip tn stays on XCD blockIdx % 8
+  const double* Ab = A + (int64_t)(16 * tm) * lda;
+  const double* Bb = B + 16 * tn;
+  double2 av[16], bv[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) av[i] = *reinterpret_cast<const double2*>(Ab + (int64_t)i * lda + 2 * lane);
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int e = lane + 64 * i;
+    bv[i] = *reinterpret_cast<const double2*>(Bb + (int64_t)(e >> 3) * ldb + 2 * (e & 7));
+  }
+  double* Ct = C + (int64_t)(16 * tm) * ldc + 16 * tn;
+  gelim::dev::d4 acc = {0.0, 0.0, 0.0, 0.0};
+  if (kAcc) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) acc[r] = Ct[(int64_t)(q + 4 * r) * ldc + r16];
+  }
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int i = 0; i < 16; ++i) *reinterpret_cast<double2*>(as + i * kTileSA + 2 * lane) = av[i];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int e = lane + 64 * i;
+    *reinterpret_cast<double2*>(bs + (e >> 3) * 16 + 2 * (e & 7)) = bv[i];
+  }
+  __syncthreads();
+  const double* a_s = as + r16 * kTileSA + q;
+  const double* b_s = bs + q * 16 + r16;
+#pragma unroll
+  for (int s = 0; s < 32; ++s)
+    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(alpha * a_s[4 * s], b_s[64 * s], acc, 0, 0, 0);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) Ct[(int64_t)(q + 4 * r) * ldc + r16] = acc[r];
+}
+
+// C (M x 128, ldc) = A B (accumulate 0) or C -= A B (accumulate 1); M a
+// multiple of 16, every operand 16-byte aligned with even leading dimensions
+int tile_gemm(double* C, int64_t ldc, const double* A, int64_t lda, const double* B, int64_t ldb, int64_t M,
+              int accumulate, hipStream_t s) {
+  if (M <= 0) return GELIM_OK;
+  if (M % 16 || (lda | ldb | ldc) & 1 || ((uintptr_t)A | (uintptr_t)B | (uintptr_t)C) & 15)
+    return GELIM_FAIL(GELIM_E_ARG, "drbt tile_gemm: shape / alignment");
+  const dim3 grid((unsigned)(M / 16 * 8));
+  if (accumulate)
+    hipLaunchKernelGGL(drbt_tile_kernel<true>, grid, dim3(64), 0, s, C, ldc, A, lda, B, ldb, -1.0);
+  else
+    hipLaunchKernelGGL(drbt_tile_kernel<false>, grid, dim3(64), 0, s, C, ldc, A, lda, B, ldb, 1.0);
+  HIP_TRY(hipGetLastError());
+  return GELIM_OK;
+}
+
+}  // namespace
+
 struct gelim_drbt_exec {
   int nb = 0;
-  std::vector<hipEvent_t> ev;  // 7 per block
+  std::vector<hipEvent_t> ev;  // kNev per block
 };
 
 namespace {
 
 constexpr int NB = 128;
-enum { kSmall, kBulk, kShip, kFirst, kRest, kAuxSide, kShipDone, kNev };
+// per block k: kSmall (main: small_k in place), kBulk (comm: next_k and rest_k
+// in place, and the comm stream's reads of column k-1 done), kW (main: step
+// k's W and diagonal update, or its receive), kNR (comm: block k+1's next
+// block row), kFirst / kRest (side: panel k applied to the next local block /
+// to every local block), kAuxSide (replay: the virtual owner of block k has
+// applied panel k-2), kShipDone (replay: rest_k copied out of its scratch slab)
+// kTop / kAuxTop: the same applies' first two block rows below k (all that
+// the next chain step's main-stream products read).
+enum { kSmall, kBulk, kW, kNR, kTop, kFirst, kRest, kAuxTop, kAuxSide, kShipDone, kNev };
 
 int mk_events(gelim_drbt_exec* ex, int nb) {
   if (ex->nb >= nb) return GELIM_OK;
@@ -103,12 +194,12 @@ struct Exec {
   hipStream_t main, side, comm, aux;
   int64_t nb, nbl;
 
-  hipEvent_t ev(int k, int which) const { return ex->ev[(size_t)k * kNev + which]; }
+  hipEvent_t ev(int64_t k, int which) const { return ex->ev[(size_t)k * kNev + which]; }
   bool owns(int64_t k) const { return k % a.P == a.rank; }
   double* col(int64_t k) const {  // column k from its diagonal block down (ld 128)
     return owns(k) ? a.Mb + (k / a.P) * a.mbs + k * NB * NB : a.X[k % 3];
   }
-  int64_t small(int64_t k) const { return std::min<int64_t>(2 * NB, a.np - k * NB); }
+  double* wbuf(int64_t k) const { return a.Wm + (k & 1) * NB * NB; }  // step k's W (a ring of two)
   int64_t first_lb_after(int64_t k) const {
     const int64_t q = (k + 1 - a.rank + a.P - 1) / a.P;  // ceil((k + 1 - rank) / P), >= 0 here
     return std::min(nbl, std::max<int64_t>(0, k + 1 - a.rank > 0 ? q : 0));
@@ -131,73 +222,98 @@ struct Exec {
     return gemm(a.Mb + lb0 * a.mbs + r0 * NB, NB, a.mbs, c + (r0 - k * NB) * NB, NB, W, ldw, 0, r1 - r0,
                 (lb1 - lb0) * NB, NB, -1.0, 1, cap, s);
   }
+  // panel k applied to local blocks lb0 .. lb1; with top, rows k+1 .. k+2
+  // first, then the event top, then the rows below
   int apply_panel(int64_t k, const double* c, int64_t lb0, int64_t lb1, double* W, int64_t ldw, int cap,
-                  hipStream_t s) const {
-    if (lb1 <= lb0) return GELIM_OK;
-    GELIM_TRY(panel_w(k, c, lb0, lb1, W, ldw, s));
-    return panel_rows(k, c, lb0, lb1, (k + 1) * NB, a.np, W, ldw, cap, s);
+                  hipStream_t s, hipEvent_t top = nullptr) const {
+    if (lb1 > lb0) {
+      GELIM_TRY(panel_w(k, c, lb0, lb1, W, ldw, s));
+      const int64_t r1 = top ? std::min(a.np, (k + 3) * NB) : (k + 1) * NB;
+      GELIM_TRY(panel_rows(k, c, lb0, lb1, (k + 1) * NB, r1, W, ldw, cap, s));
+      if (top) HIP_TRY(hipEventRecord(top, s));
+      return panel_rows(k, c, lb0, lb1, r1, a.np, W, ldw, cap, s);
+    }
+    if (top) HIP_TRY(hipEventRecord(top, s));
+    return GELIM_OK;
   }
   int invert(double* blk, int64_t colidx, int32_t* info, hipStream_t s) const {
     return gelim_rbt_block_inverse(blk, NB, colidx, blk, info, s);
   }
 
-  // the chain message of block k, [Dinv_k; L_{k+1,k}], on the main stream
-  // (the owner's slab in place; receivers into their landing buffer)
-  int ship_small(int64_t k) {
-    double* c = col(k);
-    const int64_t sm = small(k) * NB;
+  // Row blocks [b0, b1) of column k to every rank, on stream s: the owner's
+  // slab in place, receivers into their landing buffer (replay: a copy out
+  // of the virtual owner's scratch slab)
+  int ship(int64_t k, int64_t b0, int64_t b1, void* rccl, hipStream_t s) const {
+    b1 = std::min(b1, nb);
+    if (b1 <= b0) return GELIM_OK;
+    double* c = col(k) + (b0 - k) * NB * NB;
+    const int64_t n = (b1 - b0) * NB * NB;
     if (a.replay && !owns(k)) {
-      HIP_TRY(hipMemcpyAsync(c, a.F[k % 3] + k * NB * NB, sm * sizeof(double), hipMemcpyDeviceToDevice, main));
-    } else if (a.rccl_small) {
-      GELIM_TRY(gelim_rccl_bcast(a.rccl_small, c, sm, 0, (int)(k % a.P), main));
+      HIP_TRY(hipMemcpyAsync(c, a.F[k % 3] + b0 * NB * NB, n * sizeof(double), hipMemcpyDeviceToDevice, s));
+    } else if (rccl) {
+      GELIM_TRY(gelim_rccl_bcast(rccl, c, n, 0, (int)(k % a.P), s));
     }
-    HIP_TRY(hipEventRecord(ev(k, kSmall), main));
     return GELIM_OK;
   }
-  // the rest of column k, L_{k+2..,k}, on the communicator stream after
-  // what main has produced (owner) or freed (receivers) so far
-  int ship_bulk(int64_t k) {
-    double* c = col(k);
-    const int64_t n = (a.np - k * NB) * NB, sm = small(k) * NB;
-    HIP_TRY(hipEventRecord(ev(k, kShip), main));
-    HIP_TRY(hipStreamWaitEvent(comm, ev(k, kShip), 0));
-    if (n > sm) {
-      if (a.replay && !owns(k)) {
-        const double* src = a.F[k % 3] + k * NB * NB;
-        HIP_TRY(hipMemcpyAsync(c + sm, src + sm, (n - sm) * sizeof(double), hipMemcpyDeviceToDevice, comm));
-      } else if (a.rccl_bulk) {
-        GELIM_TRY(gelim_rccl_bcast(a.rccl_bulk, c + sm, n - sm, 0, (int)(k % a.P), comm));
-      }
-    }
-    HIP_TRY(hipEventRecord(ev(k, kBulk), comm));
-    if (a.replay && !owns(k)) HIP_TRY(hipEventRecord(ev(k, kShipDone), comm));
+  // A receiver's landing buffer X[t % 3] held column t-3: the side stream
+  // (panel t-3), main (chain step t-3 reads it) and comm (its step t-3 reads
+  // it; that step ends with kBulk(t-2)) must be done with it
+  int land(int64_t t, hipStream_t s, bool on_main) const {
+    if (owns(t) || t < 3) return GELIM_OK;
+    HIP_TRY(hipStreamWaitEvent(s, ev(t - 3, kRest), 0));
+    HIP_TRY(hipStreamWaitEvent(s, on_main ? ev(t - 2, kBulk) : ev(t - 3, kW), 0));
+    return GELIM_OK;
+  }
+  // small_t = [Dinv_t; L_{t+1,t}], the chain message, on main
+  int ship_small(int64_t t) {
+    GELIM_TRY(land(t, main, true));
+    GELIM_TRY(ship(t, t, t + 2, a.rccl_small, main));
+    HIP_TRY(hipEventRecord(ev(t, kSmall), main));
+    return GELIM_OK;
+  }
+  // next_t = L_{t+2,t} and rest_t = L_{t+3..,t} on comm; with f (the slab
+  // of column t, owner's view) and k = t - 1, the rows they hold are first
+  // updated there: f[t+2] -= L_{t+2,k} W, ship next, f[t+3..] -= L_{t+3..,k} W,
+  // ship rest.  The rows beyond small_k come from next_k / rest_k, which
+  // precede these on comm.
+  int ship_below(int64_t t, double* f, const double* c, const double* W) {
+    if (f && t + 2 < nb) GELIM_TRY(tile_gemm(f + (t + 2) * NB * NB, NB, c + 3 * NB * NB, NB, W, NB, NB, 1, comm));
+    GELIM_TRY(land(t, comm, false));
+    GELIM_TRY(ship(t, t + 2, t + 3, a.rccl_bulk, comm));
+    if (f && t + 3 < nb)
+      GELIM_TRY(gemm(f + (t + 3) * NB * NB, NB, 0, c + 4 * NB * NB, NB, W, NB, 0, (nb - t - 3) * NB, NB, NB, -1.0, 1,
+                     a.side_cap, comm));
+    GELIM_TRY(ship(t, t + 3, nb, a.rccl_bulk, comm));
+    HIP_TRY(hipEventRecord(ev(t, kBulk), comm));
+    if (a.replay && !owns(t)) HIP_TRY(hipEventRecord(ev(t, kShipDone), comm));
     return GELIM_OK;
   }
 
   // The chain step that produces block t = k+1 on its slab f (ld 128, the
-  // column from row 0): W = Dinv_k f[k]; f[t] -= L_{t,k} W; the next block
-  // row f[t+1] -= L_{t+1,k} W (needs bulk_k's first block); Dinv_t = f[t]^-1
-  // in place; ship small_t; the rest f[t+2..] -= L_{t+2..,k} W; ship bulk_t.
-  // Only W, the diagonal update, the next-block row and the inverse are on
-  // the chain: the next owner needs nothing else.
-  int chain(int64_t k, double* f, int64_t fbs, double* W, int32_t* info) {
+  // column from row 0).  Main: W = Dinv_k f[k]; f[t] -= L_{t,k} W (both from
+  // small_k alone); Dinv_t = f[t]^-1 in place; ship small_t once comm has
+  // updated f[t+1].  Comm, beside the inverse: f[t+1] -= L_{t+1,k} W (next_k),
+  // then the rows below with their messages (ship_below).  So the chain is
+  // small_k -> W -> diagonal -> inverse -> small_t, and neither it nor the
+  // next-row product waits on the bulk of a column.
+  // below: the event of the apply of panel k-1 to the whole of block t (the
+  // caller made main wait for its top rows only)
+  int chain(int64_t k, double* f, int32_t* info, hipEvent_t below) {
     const int64_t t = k + 1;
     const double* c = col(k);
-    GELIM_TRY(gemm(W, NB, 0, c, NB, f + k * NB * NB, NB, fbs, NB, NB, NB, 1.0, 0, 0, main));
-    GELIM_TRY(gemm(f + t * NB * NB, NB, fbs, c + NB * NB, NB, W, NB, 0, NB, NB, NB, -1.0, 1, 0, main));
-    const bool more = (t + 1) * NB < a.np;
-    if (more) {
-      HIP_TRY(hipStreamWaitEvent(main, ev(k, kBulk), 0));
-      GELIM_TRY(gemm(f + (t + 1) * NB * NB, NB, fbs, c + 2 * NB * NB, NB, W, NB, 0, NB, NB, NB, -1.0, 1, 0, main));
-    }
+    double* W = wbuf(k);
+    if (k >= 2) HIP_TRY(hipStreamWaitEvent(main, ev(k - 1, kBulk), 0));  // comm's step k-2 is done with this W
+    GELIM_TRY(tile_gemm(W, NB, c, NB, f + k * NB * NB, NB, NB, 0, main));
+    GELIM_TRY(tile_gemm(f + t * NB * NB, NB, c + NB * NB, NB, W, NB, NB, 1, main));
+    HIP_TRY(hipEventRecord(ev(k, kW), main));
     GELIM_TRY(invert(f + t * NB * NB, t * NB, info, main));
-    // a receiver's landing buffer of t is free once its side stream is done with t - 3
-    if (t >= 3 && !owns(t)) HIP_TRY(hipStreamWaitEvent(main, ev(t - 3, kRest), 0));
-    GELIM_TRY(ship_small(t));
-    if ((t + 2) * NB < a.np)
-      GELIM_TRY(gemm(f + (t + 2) * NB * NB, NB, fbs, c + 3 * NB * NB, NB, W, NB, 0, a.np - (t + 2) * NB, NB, NB, -1.0,
-                     1, 0, main));
-    return ship_bulk(t);
+    HIP_TRY(hipStreamWaitEvent(comm, ev(k, kW), 0));
+    if (below) HIP_TRY(hipStreamWaitEvent(comm, below, 0));
+    if (t + 1 < nb) GELIM_TRY(tile_gemm(f + (t + 1) * NB * NB, NB, c + 2 * NB * NB, NB, W, NB, NB, 1, comm));
+    HIP_TRY(hipEventRecord(ev(k, kNR), comm));
+    GELIM_TRY(ship_below(t, f, c, W));
+    HIP_TRY(hipStreamWaitEvent(main, ev(k, kNR), 0));
+    return ship_small(t);
   }
 
   // replay: the virtual owner of block k+2 applies panel k to it first
@@ -209,53 +325,49 @@ struct Exec {
     HIP_TRY(hipStreamWaitEvent(aux, ev(k, kSmall), 0));
     HIP_TRY(hipStreamWaitEvent(aux, ev(k, kBulk), 0));
     if (t >= 3) HIP_TRY(hipStreamWaitEvent(aux, ev(t - 3, kShipDone), 0));  // the slab's previous column shipped
-    GELIM_TRY(gemm(a.Wfs, NB, 0, c, NB, f + k * NB * NB, NB, 0, NB, NB, NB, 1.0, 0, 0, aux));
-    GELIM_TRY(gemm(f + (k + 1) * NB * NB, NB, 0, c + NB * NB, NB, a.Wfs, NB, 0, a.np - (k + 1) * NB, NB, NB, -1.0, 1,
-                   a.side_cap, aux));
+    GELIM_TRY(tile_gemm(a.Wfs, NB, c, NB, f + k * NB * NB, NB, NB, 0, aux));
+    const int64_t top = std::min<int64_t>(2, nb - k - 1);  // block rows k+1, k+2: what the chain's main reads
+    GELIM_TRY(tile_gemm(f + (k + 1) * NB * NB, NB, c + NB * NB, NB, a.Wfs, NB, top * NB, 1, aux));
+    HIP_TRY(hipEventRecord(ev(t, kAuxTop), aux));
+    GELIM_TRY(gemm(f + (k + 1 + top) * NB * NB, NB, 0, c + (1 + top) * NB * NB, NB, a.Wfs, NB, 0,
+                   a.np - (k + 1 + top) * NB, NB, NB, -1.0, 1, a.side_cap, aux));
     HIP_TRY(hipEventRecord(ev(t, kAuxSide), aux));
     return GELIM_OK;
-  }
-
-  // replay: the virtual owner of block k+1 (k = -1: block 0's inverse)
-  int foreign_chain(int64_t k) {
-    const int64_t t = k + 1;
-    double* f = a.F[t % 3];
-    if (k < 0) return invert(f, 0, a.finfo, main);
-    if (t >= 2) HIP_TRY(hipStreamWaitEvent(main, ev(t, kAuxSide), 0));
-    return chain(k, f, 0, a.Wf, a.finfo);
   }
 
   int run() {
     HIP_TRY(hipEventRecord(ev(0, kRest), main));  // Mb as the transform left it
     HIP_TRY(hipStreamWaitEvent(side, ev(0, kRest), 0));
+    HIP_TRY(hipStreamWaitEvent(comm, ev(0, kRest), 0));
     if (a.rank == 0)
       GELIM_TRY(invert(a.Mb, 0, a.info, main));
     else if (a.replay)
-      GELIM_TRY(foreign_chain(-1));
+      GELIM_TRY(invert(a.F[0], 0, a.finfo, main));
     GELIM_TRY(ship_small(0));
-    GELIM_TRY(ship_bulk(0));
+    GELIM_TRY(ship_below(0, nullptr, nullptr, nullptr));
     for (int64_t k = 0; k < nb; ++k) {
       const double* c = col(k);
-      const int64_t lb0 = first_lb_after(k);
-      const bool nxt = k + 1 < nb;
-      const bool mine1 = nxt && owns(k + 1);
+      const int64_t t = k + 1, lb0 = first_lb_after(k);
+      const bool nxt = t < nb;
+      const bool mine1 = nxt && owns(t);
       // main first: the chain step of block k+1 depends only on the previous
       // steps' side / aux work, so it is queued before this step's
       if (mine1) {
-        if (k >= 1) HIP_TRY(hipStreamWaitEvent(main, ev(k - 1, kFirst), 0));  // panel k-1 reached block k+1
-        GELIM_TRY(chain(k, a.Mb + lb0 * a.mbs, a.mbs, a.Wm, a.info));
-      } else if (nxt && a.replay) {
-        GELIM_TRY(foreign_chain(k));
+        if (k >= 1) HIP_TRY(hipStreamWaitEvent(main, ev(k - 1, kTop), 0));  // panel k-1 reached block k+1's top
+        GELIM_TRY(chain(k, a.Mb + lb0 * a.mbs, a.info, k >= 1 ? ev(k - 1, kFirst) : nullptr));
+      } else if (nxt && a.replay) {  // the virtual owner of block k+1, on this GPU
+        if (t >= 2) HIP_TRY(hipStreamWaitEvent(main, ev(t, kAuxTop), 0));
+        GELIM_TRY(chain(k, a.F[t % 3], a.finfo, t >= 2 ? ev(t, kAuxSide) : nullptr));
       } else if (nxt) {
-        if (k + 1 >= 3) HIP_TRY(hipStreamWaitEvent(main, ev(k + 1 - 3, kRest), 0));  // landing buffer free again
-        GELIM_TRY(ship_small(k + 1));
-        GELIM_TRY(ship_bulk(k + 1));
+        GELIM_TRY(ship_small(t));
+        HIP_TRY(hipEventRecord(ev(k, kW), main));
+        GELIM_TRY(ship_below(t, nullptr, nullptr, nullptr));
       }
       HIP_TRY(hipStreamWaitEvent(side, ev(k, kSmall), 0));
       HIP_TRY(hipStreamWaitEvent(side, ev(k, kBulk), 0));
       const int64_t ls = lb0 + (mine1 ? 1 : 0);  // block k+1 is main's
       const int64_t lf = std::min(ls + 1, nbl);
-      GELIM_TRY(apply_panel(k, c, ls, lf, a.Ws, a.nloc, a.side_cap, side));
+      GELIM_TRY(apply_panel(k, c, ls, lf, a.Ws, a.nloc, a.side_cap, side, ev(k, kTop)));
       HIP_TRY(hipEventRecord(ev(k, kFirst), side));
       GELIM_TRY(apply_panel(k, c, lf, nbl, a.Ws + (lf - ls) * NB, a.nloc, a.side_cap, side));
       HIP_TRY(hipEventRecord(ev(k, kRest), side));
@@ -273,6 +385,16 @@ struct Exec {
 
 }  // namespace
 
+// The chain step's small products alone (tests and micro-benchmarks):
+// with_w = 1: W = Dk B, then D -= L W; with_w = 0: D -= L W (W given).
+// Every operand is 128 x 128, row-major, ld 128.
+extern "C" int gelim_drbt_chain_products(const double* Dk, const double* B, double* W, const double* L, double* D,
+                                         int32_t with_w, void* stream) {
+  if (!W || !L || !D || (with_w && (!Dk || !B))) return GELIM_FAIL(GELIM_E_ARG, "drbt_chain_products: null operand");
+  if (with_w) GELIM_TRY(tile_gemm(W, NB, Dk, NB, B, NB, NB, 0, (hipStream_t)stream));
+  return tile_gemm(D, NB, L, NB, W, NB, NB, 1, (hipStream_t)stream);
+}
+
 extern "C" gelim_drbt_exec* gelim_drbt_exec_create(void) { return new gelim_drbt_exec(); }
 
 extern "C" void gelim_drbt_exec_destroy(gelim_drbt_exec* ex) {
@@ -287,7 +409,7 @@ extern "C" int gelim_drbt_factor(gelim_drbt_exec* ex, const gelim_drbt_args* a) 
   if (!ex || !a || !a->Mb || !a->Wm || !a->Ws || !a->info || a->P < 1 || a->rank < 0 || a->rank >= a->P ||
       a->np % (512 * (int64_t)a->P) || a->nloc * a->P != a->np || a->mbs < a->np * NB || !a->side ||
       !a->comm || (a->P > 1 && !a->replay && (!a->rccl_small || !a->rccl_bulk)) ||
-      (a->replay && (!a->aux || !a->F[0] || !a->F[1] || !a->F[2] || !a->Wf || !a->Wfs || !a->finfo)) ||
+      (a->replay && (!a->aux || !a->F[0] || !a->F[1] || !a->F[2] || !a->Wfs || !a->finfo)) ||
       !a->X[0] || !a->X[1] || !a->X[2])
     return GELIM_FAIL(GELIM_E_ARG, "drbt_factor: bad arguments");
   const int64_t nb = a->np / NB;

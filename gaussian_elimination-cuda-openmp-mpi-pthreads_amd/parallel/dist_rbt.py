@@ -124,7 +124,7 @@ class _ExecArgs(_C.Structure):
                 ("Ws", _C.c_void_p), ("info", _C.c_void_p), ("main", _C.c_void_p), ("side", _C.c_void_p),
                 ("comm", _C.c_void_p), ("rccl_small", _C.c_void_p), ("rccl_bulk", _C.c_void_p),
                 ("side_cap", _C.c_int32), ("replay", _C.c_int32), ("F", _C.c_void_p * 3), ("aux", _C.c_void_p),
-                ("Wf", _C.c_void_p), ("Wfs", _C.c_void_p), ("finfo", _C.c_void_p)]
+                ("Wfs", _C.c_void_p), ("finfo", _C.c_void_p)]
 
 
 class DistributedRBT:
@@ -203,7 +203,7 @@ class DistributedRBT:
         nbuf = NBUF if lookahead else 2
         # landing buffers of the column messages [Dinv_k; L_k] (non-owners)
         self._xbufs = [torch.zeros(self.np * NB, **f64) for _ in range(nbuf)]
-        self._Wm = torch.zeros((NB, NB), **f64)
+        self._Wm = torch.zeros((2, NB, NB), **f64)  # the native executor's W ring; the Python schedule uses [0]
         self._Ws = torch.zeros((NB, self.nloc), **f64)
         self._info = torch.full((1,), 0x7F7F7F7F, dtype=torch.int32, device=dev)
         self._serr = torch.zeros(1, dtype=torch.int32, device=dev)  # block solves: hand-off timeout word
@@ -479,12 +479,12 @@ class DistributedRBT:
                 lb = lb0  # local block of k+1
                 if k >= 1:
                     main.wait_event(ev_first[k - 1])  # panel k-1 reached block k+1 (side stream)
-                self._panel_w(k, col, lb, lb + 1, self._Wm)
-                self._panel_rows(k, col, lb, lb + 1, (k + 1) * NB, (k + 2) * NB, self._Wm)  # its diagonal block
+                self._panel_w(k, col, lb, lb + 1, self._Wm[0])
+                self._panel_rows(k, col, lb, lb + 1, (k + 1) * NB, (k + 2) * NB, self._Wm[0])  # its diagonal block
                 self._invert(k + 1)
                 if hb[k] is not None:
                     hb[k].wait()  # main: L_{k+2.., k}
-                    self._panel_rows(k, col, lb, lb + 1, (k + 2) * NB, self.np, self._Wm)
+                    self._panel_rows(k, col, lb, lb + 1, (k + 2) * NB, self.np, self._Wm[0])
             else:
                 self._foreign_chain(k, col, hb[k])
             if k + 1 >= nbuf:

@@ -120,7 +120,7 @@ class OneRankOfP(DistributedRBT):
         for i, f in enumerate(self._fs):
             a.F[i] = ptr(f)
         a.aux = self._aux.cuda_stream
-        a.Wf, a.Wfs, a.finfo = ptr(self._Wf), ptr(self._Wfs), ptr(self._finfo)
+        a.Wfs, a.finfo = ptr(self._Wfs), ptr(self._finfo)
 
     def _inv(self, blk: torch.Tensor, col: int) -> None:
         _native.check(_native.lib().gelim_rbt_block_inverse(ptr(blk), NB, col, ptr(blk), ptr(self._finfo),

@@ -201,6 +201,38 @@ def test_dgemm_block_major(gelim, cuda, acc, M, nblk, K):
     assert torch.equal(slabs[:, :K + 32], orig[:, :K + 32]) and torch.equal(slabs[:, K + 32 + M:], orig[:, K + 32 + M:])
 
 
+def test_chain_products_match_dgemm(gelim, cuda):
+    """drbt_exec.hip's chain kernels (W = Dk B with D -= L W in one launch;
+    D -= L W alone) give dgemm.hip's bits, and the fp64 products."""
+    from gelim import _native
+
+    lib = _native.lib()
+    torch.manual_seed(5)
+    Dk, B, L, D0 = (torch.randn(128, 128, dtype=torch.float64, device=cuda) for _ in range(4))
+    s = torch.cuda.current_stream(cuda).cuda_stream
+    W, D = torch.empty_like(B), D0.clone()
+    _native.check(lib.gelim_drbt_chain_products(Dk.data_ptr(), B.data_ptr(), W.data_ptr(), L.data_ptr(), D.data_ptr(),
+                                                1, s), "chain_products")
+    W2, D2 = torch.empty_like(B), D0.clone()
+    _native.check(lib.gelim_gpu_dgemm_ex(W2.data_ptr(), 128, Dk.data_ptr(), 128, B.data_ptr(), 128, 128, 128, 128,
+                                         1.0, 0, 0, s), "dgemm W")
+    _native.check(lib.gelim_gpu_dgemm_ex(D2.data_ptr(), 128, L.data_ptr(), 128, W2.data_ptr(), 128, 128, 128, 128,
+                                         -1.0, 1, 0, s), "dgemm D")
+    torch.cuda.synchronize()
+    assert torch.equal(W, W2) and torch.equal(D, D2)
+    want_w = Dk @ B
+    assert ((W - want_w).abs().max() / want_w.abs().max()).item() < 1e-14
+    want_d = D0 - L @ want_w
+    assert ((D - want_d).abs().max() / want_d.abs().max()).item() < 1e-13
+    # the next-row form: D -= L W with W given
+    D3, D4 = D0.clone(), D0.clone()
+    _native.check(lib.gelim_drbt_chain_products(None, None, W.data_ptr(), L.data_ptr(), D3.data_ptr(), 0, s), "nr")
+    _native.check(lib.gelim_gpu_dgemm_ex(D4.data_ptr(), 128, L.data_ptr(), 128, W.data_ptr(), 128, 128, 128, 128,
+                                         -1.0, 1, 0, s), "dgemm nr")
+    torch.cuda.synchronize()
+    assert torch.equal(D3, D4)
+
+
 def _global_factor(gelim, cuda, P, n, lookahead):
     """The factor of DistributedRBT on P emulated ranks, assembled from the
     ranks' column-block-major slabs into one np x np matrix."""

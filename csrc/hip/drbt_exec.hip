@@ -93,31 +93,26 @@ namespace {
 // 128 KB streamed) spent 15.8 k cycles just issuing its loads and ran 21 us
 // for W + D (tools/microbench/chain_stamps.hip,
 // profiles/dist_rbt_replay_r6.md), dgemm.hip's 64-tiles 8.6 us per product.
-// The loads are coalesced (a wave instruction = one 1-KB row of A, or eight
-// 128-B rows of B), all in flight at once, and pass through LDS (A row
-// stride 132 doubles: the 16 x 4 fragment reads spread over the banks); then
-// 32 v_mfma_f64_16x16x4f64 over k = 0..127 in order, A scaled by alpha
-// (+-1) on its way in, C read first -- dgemm.hip's operation order, so the
-// products are its bits (tests/test_gpu_dist_rbt.py).
-constexpr int kTileSA = 132;
-
+// No LDS: the kernel must find a slot on CUs that the side stream's GEMMs
+// fill (40 KB of LDS per dgemm workgroup), so each lane loads its own MFMA
+// fragments (A: 16 rows x 4 k per instruction; B: 4 rows x 128 B), all of
+// them in flight before the first MFMA; then 32 v_mfma_f64_16x16x4f64 over
+// k = 0..127 in order, A scaled by alpha (+-1) on its way in, C read first
+// -- dgemm.hip's operation order, so the products are its bits
+// (tests/test_gpu_dist_rbt.py).
 template <bool kAcc>
 __global__ __launch_bounds__(64) void drbt_tile_kernel(double* __restrict__ C, int64_t ldc, const double* __restrict__ A,
                                                        int64_t lda, const double* __restrict__ B, int64_t ldb,
                                                        double alpha) {
-  __shared__ __attribute__((aligned(16))) double as[16 * kTileSA];
-  __shared__ __attribute__((aligned(16))) double bs[128 * 16];
   const int lane = threadIdx.x, r16 = lane & 15, q = lane >> 4;
   const int tm = blockIdx.x >> 3, tn = blockIdx.x & 7;  // B strip tn stays on XCD blockIdx % 8
-  const double* Ab = A + (int64_t)(16 * tm) * lda;
-  const double* Bb = B + 16 * tn;
-  double2 av[16], bv[16];
+  const double* Ab = A + (int64_t)(16 * tm + r16) * lda + q;
+  const double* Bb = B + (int64_t)q * ldb + 16 * tn + r16;
+  double av[32], bv[32];
 #pragma unroll
-  for (int i = 0; i < 16; ++i) av[i] = *reinterpret_cast<const double2*>(Ab + (int64_t)i * lda + 2 * lane);
-#pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    const int e = lane + 64 * i;
-    bv[i] = *reinterpret_cast<const double2*>(Bb + (int64_t)(e >> 3) * ldb + 2 * (e & 7));
+  for (int s = 0; s < 32; ++s) {
+    av[s] = Ab[4 * s];
+    bv[s] = Bb[(int64_t)(4 * s) * ldb];
   }
   double* Ct = C + (int64_t)(16 * tm) * ldc + 16 * tn;
   gelim::dev::d4 acc = {0.0, 0.0, 0.0, 0.0};
@@ -127,29 +122,17 @@ __global__ __launch_bounds__(64) void drbt_tile_kernel(double* __restrict__ C, i
   }
   __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-  for (int i = 0; i < 16; ++i) *reinterpret_cast<double2*>(as + i * kTileSA + 2 * lane) = av[i];
-#pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    const int e = lane + 64 * i;
-    *reinterpret_cast<double2*>(bs + (e >> 3) * 16 + 2 * (e & 7)) = bv[i];
-  }
-  __syncthreads();
-  const double* a_s = as + r16 * kTileSA + q;
-  const double* b_s = bs + q * 16 + r16;
-#pragma unroll
-  for (int s = 0; s < 32; ++s)
-    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(alpha * a_s[4 * s], b_s[64 * s], acc, 0, 0, 0);
+  for (int s = 0; s < 32; ++s) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(alpha * av[s], bv[s], acc, 0, 0, 0);
 #pragma unroll
   for (int r = 0; r < 4; ++r) Ct[(int64_t)(q + 4 * r) * ldc + r16] = acc[r];
 }
 
 // C (M x 128, ldc) = A B (accumulate 0) or C -= A B (accumulate 1); M a
-// multiple of 16, every operand 16-byte aligned with even leading dimensions
+// multiple of 16
 int tile_gemm(double* C, int64_t ldc, const double* A, int64_t lda, const double* B, int64_t ldb, int64_t M,
               int accumulate, hipStream_t s) {
   if (M <= 0) return GELIM_OK;
-  if (M % 16 || (lda | ldb | ldc) & 1 || ((uintptr_t)A | (uintptr_t)B | (uintptr_t)C) & 15)
-    return GELIM_FAIL(GELIM_E_ARG, "drbt tile_gemm: shape / alignment");
+  if (M % 16) return GELIM_FAIL(GELIM_E_ARG, "drbt tile_gemm: M not a multiple of 16");
   const dim3 grid((unsigned)(M / 16 * 8));
   if (accumulate)
     hipLaunchKernelGGL(drbt_tile_kernel<true>, grid, dim3(64), 0, s, C, ldc, A, lda, B, ldb, -1.0);
@@ -177,7 +160,8 @@ constexpr int NB = 128;
 // applied panel k-2), kShipDone (replay: rest_k copied out of its scratch slab)
 // kTop / kAuxTop: the same applies' first two block rows below k (all that
 // the next chain step's main-stream products read).
-enum { kSmall, kBulk, kW, kNR, kTop, kFirst, kRest, kAuxTop, kAuxSide, kShipDone, kNev };
+// kNext: next_k in place (comm), all that the top rows' applies need besides small_k.
+enum { kSmall, kNext, kBulk, kW, kNR, kTop, kFirst, kRest, kAuxTop, kAuxSide, kShipDone, kNev };
 
 int mk_events(gelim_drbt_exec* ex, int nb) {
   if (ex->nb >= nb) return GELIM_OK;
@@ -224,17 +208,18 @@ struct Exec {
   }
   // panel k applied to local blocks lb0 .. lb1; with top, rows k+1 .. k+2
   // first, then the event top, then the rows below
+  // (the caller has made s wait for small_k and next_k; the rows below
+  // k+2 wait here for rest_k)
   int apply_panel(int64_t k, const double* c, int64_t lb0, int64_t lb1, double* W, int64_t ldw, int cap,
                   hipStream_t s, hipEvent_t top = nullptr) const {
+    const int64_t r1 = top ? std::min(a.np, (k + 3) * NB) : (k + 1) * NB;
     if (lb1 > lb0) {
       GELIM_TRY(panel_w(k, c, lb0, lb1, W, ldw, s));
-      const int64_t r1 = top ? std::min(a.np, (k + 3) * NB) : (k + 1) * NB;
       GELIM_TRY(panel_rows(k, c, lb0, lb1, (k + 1) * NB, r1, W, ldw, cap, s));
-      if (top) HIP_TRY(hipEventRecord(top, s));
-      return panel_rows(k, c, lb0, lb1, r1, a.np, W, ldw, cap, s);
     }
     if (top) HIP_TRY(hipEventRecord(top, s));
-    return GELIM_OK;
+    HIP_TRY(hipStreamWaitEvent(s, ev(k, kBulk), 0));
+    return lb1 > lb0 ? panel_rows(k, c, lb0, lb1, r1, a.np, W, ldw, cap, s) : GELIM_OK;
   }
   int invert(double* blk, int64_t colidx, int32_t* info, hipStream_t s) const {
     return gelim_rbt_block_inverse(blk, NB, colidx, blk, info, s);
@@ -280,6 +265,7 @@ struct Exec {
     if (f && t + 2 < nb) GELIM_TRY(tile_gemm(f + (t + 2) * NB * NB, NB, c + 3 * NB * NB, NB, W, NB, NB, 1, comm));
     GELIM_TRY(land(t, comm, false));
     GELIM_TRY(ship(t, t + 2, t + 3, a.rccl_bulk, comm));
+    HIP_TRY(hipEventRecord(ev(t, kNext), comm));
     if (f && t + 3 < nb)
       GELIM_TRY(gemm(f + (t + 3) * NB * NB, NB, 0, c + 4 * NB * NB, NB, W, NB, 0, (nb - t - 3) * NB, NB, NB, -1.0, 1,
                      a.side_cap, comm));
@@ -323,12 +309,13 @@ struct Exec {
     double* f = a.F[t % 3];
     const double* c = col(k);
     HIP_TRY(hipStreamWaitEvent(aux, ev(k, kSmall), 0));
-    HIP_TRY(hipStreamWaitEvent(aux, ev(k, kBulk), 0));
+    HIP_TRY(hipStreamWaitEvent(aux, ev(k, kNext), 0));
     if (t >= 3) HIP_TRY(hipStreamWaitEvent(aux, ev(t - 3, kShipDone), 0));  // the slab's previous column shipped
     GELIM_TRY(tile_gemm(a.Wfs, NB, c, NB, f + k * NB * NB, NB, NB, 0, aux));
     const int64_t top = std::min<int64_t>(2, nb - k - 1);  // block rows k+1, k+2: what the chain's main reads
     GELIM_TRY(tile_gemm(f + (k + 1) * NB * NB, NB, c + NB * NB, NB, a.Wfs, NB, top * NB, 1, aux));
     HIP_TRY(hipEventRecord(ev(t, kAuxTop), aux));
+    HIP_TRY(hipStreamWaitEvent(aux, ev(k, kBulk), 0));
     GELIM_TRY(gemm(f + (k + 1 + top) * NB * NB, NB, 0, c + (1 + top) * NB * NB, NB, a.Wfs, NB, 0,
                    a.np - (k + 1 + top) * NB, NB, NB, -1.0, 1, a.side_cap, aux));
     HIP_TRY(hipEventRecord(ev(t, kAuxSide), aux));
@@ -364,7 +351,7 @@ struct Exec {
         GELIM_TRY(ship_below(t, nullptr, nullptr, nullptr));
       }
       HIP_TRY(hipStreamWaitEvent(side, ev(k, kSmall), 0));
-      HIP_TRY(hipStreamWaitEvent(side, ev(k, kBulk), 0));
+      HIP_TRY(hipStreamWaitEvent(side, ev(k, kNext), 0));
       const int64_t ls = lb0 + (mine1 ? 1 : 0);  // block k+1 is main's
       const int64_t lf = std::min(ls + 1, nbl);
       GELIM_TRY(apply_panel(k, c, ls, lf, a.Ws, a.nloc, a.side_cap, side, ev(k, kTop)));
@@ -393,6 +380,16 @@ extern "C" int gelim_drbt_chain_products(const double* Dk, const double* B, doub
   if (!W || !L || !D || (with_w && (!Dk || !B))) return GELIM_FAIL(GELIM_E_ARG, "drbt_chain_products: null operand");
   if (with_w) GELIM_TRY(tile_gemm(W, NB, Dk, NB, B, NB, NB, 0, (hipStream_t)stream));
   return tile_gemm(D, NB, L, NB, W, NB, NB, 1, (hipStream_t)stream);
+}
+
+// The grid cap (CUs) of the bulk GEMMs beside the chain: all CUs but 32,
+// which the chain's inverse and tile products then always find free
+// (parallel/dist_rbt.py side_cap).
+extern "C" int gelim_drbt_side_cap(void) {
+  int dev = 0, ncu = 0;
+  (void)hipGetDevice(&dev);
+  (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+  return ncu > 64 ? ncu - 32 : 0;
 }
 
 extern "C" gelim_drbt_exec* gelim_drbt_exec_create(void) { return new gelim_drbt_exec(); }

@@ -119,6 +119,7 @@ _PROTOS = {
     "gelim_drbt_exec_destroy": (None, [_vp]),
     "gelim_drbt_factor": (_int, [_vp, _vp]),
     "gelim_drbt_chain_products": (_int, [_vp, _vp, _vp, _vp, _vp, _int, _vp]),
+    "gelim_drbt_side_cap": (_int, []),
     "gelim_mixed_factor": (_int, [_vp, _vp, _i64, _vp]),
     "gelim_mixed_apply": (_int, [_vp, _vp, _i64, _vp, _vp]),
     "gelim_gpu_leaf_max_rows": (_i64, []),

@@ -169,9 +169,14 @@ class DistributedRBT:
         self.native_exec = (native_exec and self.gpu and lookahead
                             and (comm.backend == "none" or comm.native or getattr(comm, "capturable", False)))
         self._exec = None
-        # CUs the side stream's bulk trailing GEMM may take (0: all); a cap
-        # leaves CUs free for the chain's small kernels
-        self.side_cap = 0
+        # CUs the bulk GEMMs beside the chain (side stream; the native
+        # executor's rows below the chain, on the communicator stream) may
+        # take, 0: all.  Uncapped they fill every CU's LDS (dgemm 64-tiles: 4
+        # x 40 KB) and the chain's next kernel -- the inverse, a W product --
+        # waits for the whole grid to be dispatched: 40-120 us per block in the
+        # one-rank-of-8 replay (profiles/dist_rbt_replay_r6.md).  Capped, the
+        # persistent form leaves 32 CUs free.
+        self.side_cap = int(_native.lib().gelim_drbt_side_cap()) if self.gpu and self.P > 1 else 0
         self.last_issue_s = None
         self._ud, self._vd = butterfly_diagonals(self.np, seed)
         lb = torch.arange(self.nloc) // NB

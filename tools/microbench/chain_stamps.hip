@@ -1,3 +1,13 @@
+// Where the time of an 8-workgroup fused chain kernel went (round 6): the
+// first form of DistributedRBT's W = Dinv B; D -= L W kernel (16-column
+// strips, 512 threads, every workgroup streaming all of Dinv and L through
+// LDS), with s_memtime stamps per wave, plus a dependent-accumulator
+// v_mfma_f64_16x16x4f64 chain.  Result (profiles/dist_rbt_replay_r6.md):
+// 15.8 k cycles to ISSUE the loads, 20.8 k in the chunk loop -- the load path
+// of one CU, not its matrix core, bound it; the executor now runs these
+// products as one wave per 16 x 16 tile (csrc/hip/drbt_exec.hip).
+//
+//   hipcc -O3 --offload-arch=gfx950 -std=c++17 tools/microbench/chain_stamps.hip -o /tmp/chain_stamps
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdlib>

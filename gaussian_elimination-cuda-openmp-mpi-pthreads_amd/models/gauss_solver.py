@@ -17,9 +17,12 @@ Backends
 
 fp32 elimination + fp64 refinement is `hip-pivot` with
 dtype=float32 and `solve_refined` (stored fp32 factors, O(n^2) per
-correction).  The round-3/4 "hip-mixed" engine (fp32 trailing products +
-GMRES-IR) was removed in round 5: slower than hip-rbt at every n and not
-convergent at 16384 (profiles/trsv_split_r5.txt).
+correction).  It is NOT a fast path: the per-pivot loop is latency-bound, so
+fp32 saves no time (2048: 11.9 vs 11.4 ms); it serves the reference's fp32
+programs and fp32 inputs.  The fast paths are fp64 (`hip`, `hip-rbt`).  The
+round-3/4 "hip-mixed" engine (fp32 trailing products + GMRES-IR) was removed
+in round 5: slower than hip-rbt at every n and not convergent at 16384
+(profiles/trsv_split_r5.txt).
   seq / omp / pthreads-v1 / pthreads-v2 / pthreads-v3 : the reference CPU
                       strategies (csrc/cpu/gauss_cpu.cpp), fp64
 

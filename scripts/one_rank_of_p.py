@@ -199,13 +199,15 @@ def model(n: int, P: int, t_factor: float, t_apply: float, t_resid: float, corre
     link = 0.0
     for k in range(1, nb):
         small = min(2 * NB, npad - k * NB) * NB * 8
-        bulk = max(0, npad - k * NB - 2 * NB) * NB * 8
+        rest = max(0, npad - k * NB - 3 * NB) * NB * 8
         t_small = lat_us * 1e-6 + small / (bw_gbs * 1e9)
-        t_bulk = lat_us * 1e-6 + bulk / (bw_gbs * 1e9)
-        # the chain waits for the small message; the column rest (and so the
-        # next small message) waits for the bulk when it is longer than the
-        # inverse + the two small GEMMs
-        link += t_small + max(0.0, t_bulk - t_chain_step)
+        t_rest = lat_us * 1e-6 + rest / (bw_gbs * 1e9)
+        # the chain waits for the small message [Dinv_k; L_{k+1,k}]; the
+        # next-row message (one block, shipped beside the owner's inverse)
+        # lands under the next owner's inverse; the column rest is first
+        # needed two chain steps later (its first block feeds next_{k+1},
+        # csrc/hip/drbt_exec.hip), so it costs only what it takes beyond that
+        link += t_small + max(0.0, t_rest - 2 * t_chain_step)
     ns = npad // (NB * P)
     solve_lat = 2 * ns * (lat_us * 1e-6 + NB * P * 8 / (bw_gbs * 1e9))  # one all_reduce per super-block, 2 directions
     applies = 1 + corrections

@@ -416,6 +416,90 @@ int dgemm_ex(double* C, int64_t ldc, const double* A, int64_t lda, const double*
   return dgemm_capped(C, ldc, A, lda, B, ldb, M, N, K, alpha, 0, s, accumulate);
 }
 
+// K = 128 products as one 64-thread workgroup per 16 x 16 tile of C: for
+// the 128-wide products on a latency-bound chain (the randomised engines'
+// W = Dinv A_k,rest and block-column / block-row updates).  Those have few
+// 64-tiles, so a 64-tile grid leaves most CUs idle, and each of its
+// workgroups needs 40 KB of LDS -- beside a bulk GEMM whose 128-tiles hold
+// 2 x 72 KB of every CU's LDS it cannot start until side workgroups retire
+// (28.8 us for 128 x 8064 x 128 under the hip-rbt side update,
+// profiles/rbt_trace_8192_r6.txt).  A tile workgroup pulls ~32 KB (16 rows of
+// A, a 16-column strip of B) and uses no LDS: each lane loads its own MFMA
+// fragments, all in flight before the first MFMA (A: 16 rows x 4 k per
+// instruction; B: 4 rows x 128 B), then 32 v_mfma_f64_16x16x4f64 over k =
+// 0..127 in order, A scaled by alpha on its way in, C read first -- the tile
+// kernel's per-element operation order, so the bits are dgemm's
+// (tests/test_gpu_dist_rbt.py::test_chain_products_match_dgemm).  128 x 128
+// x 128: 3.9 us against 8.6 for the 64-tile grid
+// (profiles/dist_rbt_replay_r6.md).
+struct Tile16 {
+  double* C;
+  int64_t ldc;
+  const double* A;
+  int64_t lda;
+  const double* B;
+  int64_t ldb;
+  int nt;  // 16-column tiles of C
+};
+
+template <bool kAcc>
+__global__ __launch_bounds__(64) void tile16_kernel(Tile16 o0, Tile16 o1, int n0, double alpha) {
+  const int lane = threadIdx.x, r16 = lane & 15, q = lane >> 4;
+  int b = blockIdx.x;
+  const Tile16 o = b < n0 ? o0 : o1;
+  b = b < n0 ? b : b - n0;
+  const int tm = b / o.nt, tn = b % o.nt;
+  const double* Ab = o.A + (int64_t)(16 * tm + r16) * o.lda + q;
+  const double* Bb = o.B + (int64_t)q * o.ldb + 16 * tn + r16;
+  double av[32], bv[32];
+#pragma unroll
+  for (int s = 0; s < 32; ++s) {
+    av[s] = Ab[4 * s];
+    bv[s] = Bb[(int64_t)(4 * s) * o.ldb];
+  }
+  double* Ct = o.C + (int64_t)(16 * tm) * o.ldc + 16 * tn;
+  dev::d4 acc = {0.0, 0.0, 0.0, 0.0};
+  if (kAcc) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) acc[r] = Ct[(int64_t)(q + 4 * r) * o.ldc + r16];
+  }
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int s = 0; s < 32; ++s) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(alpha * av[s], bv[s], acc, 0, 0, 0);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) Ct[(int64_t)(q + 4 * r) * o.ldc + r16] = acc[r];
+}
+
+// Up to two independent K = 128 products C (+)= alpha A B in one launch of
+// 16 x 16 tiles (M, N multiples of 16; an op with M or N <= 0 is skipped).
+int dgemm_tiles(const GemmOp& p1, const GemmOp& p2, double alpha, int accumulate, hipStream_t s) {
+  const GemmOp* ops[2] = {&p1, &p2};
+  Tile16 t[2] = {};
+  int n[2] = {0, 0};
+  for (int i = 0; i < 2; ++i) {
+    const GemmOp& o = *ops[i];
+    if (o.M <= 0 || o.N <= 0) continue;
+    if (o.K != 128 || o.M % 16 || o.N % 16 || o.lda < 128 || o.ldb < o.N || o.ldc < o.N ||
+        (o.M / 16) * (o.N / 16) > INT32_MAX / 2)
+      return GELIM_FAIL(GELIM_E_ARG, "dgemm_tiles: K must be 128, M and N multiples of 16");
+    t[i] = Tile16{o.C, o.ldc, o.A, o.lda, o.B, o.ldb, (int)(o.N / 16)};
+    n[i] = (int)((o.M / 16) * (o.N / 16));
+  }
+  if (n[0] + n[1] == 0) return GELIM_OK;
+  if (n[0] == 0) {  // op 0 empty: op 1 alone
+    t[0] = t[1];
+    n[0] = n[1];
+    n[1] = 0;
+  }
+  const dim3 grid((unsigned)(n[0] + n[1]));
+  if (accumulate)
+    hipLaunchKernelGGL(tile16_kernel<true>, grid, dim3(64), 0, s, t[0], t[1], n[0], alpha);
+  else
+    hipLaunchKernelGGL(tile16_kernel<false>, grid, dim3(64), 0, s, t[0], t[1], n[0], alpha);
+  HIP_TRY(hipGetLastError());
+  return GELIM_OK;
+}
+
 // Two independent C += alpha A B products (same alpha / accumulate) in one
 // launch (dgemm2_kernel); either may be empty.  Same operand contract as
 // dgemm_launch.

@@ -28,7 +28,7 @@
 // Every rank, side: [small_k, next_k, rest_k] panel k -> its next block
 //   (ev_first), then the rest of its columns (ev_rest).
 // Every product has dgemm.hip's per-element operation order (the 128-wide
-// ones run as drbt_tile_kernel, bit-identical) and the inverses are the same
+// ones run as dgemm.hip tile16_kernel, bit-identical) and the inverses are the same
 // kernel, so this schedule and the Python one (two messages per column) give
 // the same factor bits (tests/test_gpu_dist_rbt.py::
 // test_native_executor_matches_python, test_chain_products_match_dgemm).
@@ -85,61 +85,15 @@ struct gelim_drbt_args {
 
 namespace {
 
-// The chain's 128-wide products, C (M x 128) (+)= alpha A (M x 128) B (128 x
-// 128), as one 64-thread workgroup per 16 x 16 tile of C: M = 128 is 64
-// workgroups on 64 CUs.  A CU pulls only ~32 KB (16 rows of A, a 16-column
-// strip of B) -- the load path of one CU, not its matrix core, is what bounds
-// these products: an 8-workgroup form (16-column strips, all of A per CU, 2 x
-// 128 KB streamed) spent 15.8 k cycles just issuing its loads and ran 21 us
-// for W + D (tools/microbench/chain_stamps.hip,
-// profiles/dist_rbt_replay_r6.md), dgemm.hip's 64-tiles 8.6 us per product.
-// No LDS: the kernel must find a slot on CUs that the side stream's GEMMs
-// fill (40 KB of LDS per dgemm workgroup), so each lane loads its own MFMA
-// fragments (A: 16 rows x 4 k per instruction; B: 4 rows x 128 B), all of
-// them in flight before the first MFMA; then 32 v_mfma_f64_16x16x4f64 over
-// k = 0..127 in order, A scaled by alpha (+-1) on its way in, C read first
-// -- dgemm.hip's operation order, so the products are its bits
-// (tests/test_gpu_dist_rbt.py).
-template <bool kAcc>
-__global__ __launch_bounds__(64) void drbt_tile_kernel(double* __restrict__ C, int64_t ldc, const double* __restrict__ A,
-                                                       int64_t lda, const double* __restrict__ B, int64_t ldb,
-                                                       double alpha) {
-  const int lane = threadIdx.x, r16 = lane & 15, q = lane >> 4;
-  const int tm = blockIdx.x >> 3, tn = blockIdx.x & 7;  // B strip tn stays on XCD blockIdx % 8
-  const double* Ab = A + (int64_t)(16 * tm + r16) * lda + q;
-  const double* Bb = B + (int64_t)q * ldb + 16 * tn + r16;
-  double av[32], bv[32];
-#pragma unroll
-  for (int s = 0; s < 32; ++s) {
-    av[s] = Ab[4 * s];
-    bv[s] = Bb[(int64_t)(4 * s) * ldb];
-  }
-  double* Ct = C + (int64_t)(16 * tm) * ldc + 16 * tn;
-  gelim::dev::d4 acc = {0.0, 0.0, 0.0, 0.0};
-  if (kAcc) {
-#pragma unroll
-    for (int r = 0; r < 4; ++r) acc[r] = Ct[(int64_t)(q + 4 * r) * ldc + r16];
-  }
-  __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-  for (int s = 0; s < 32; ++s) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(alpha * av[s], bv[s], acc, 0, 0, 0);
-#pragma unroll
-  for (int r = 0; r < 4; ++r) Ct[(int64_t)(q + 4 * r) * ldc + r16] = acc[r];
-}
-
-// C (M x 128, ldc) = A B (accumulate 0) or C -= A B (accumulate 1); M a
-// multiple of 16
+// The chain's 128-wide products: C (M x 128, ldc) = A B (accumulate 0) or
+// C -= A B (accumulate 1), K = 128, as dgemm.hip's 16 x 16 tiles (one
+// 64-thread workgroup each, no LDS; bit-identical to dgemm): 64 workgroups
+// for M = 128, 3.9 us against 8.6 for dgemm's 64-tile grid
+// (profiles/dist_rbt_replay_r6.md).
 int tile_gemm(double* C, int64_t ldc, const double* A, int64_t lda, const double* B, int64_t ldb, int64_t M,
               int accumulate, hipStream_t s) {
-  if (M <= 0) return GELIM_OK;
-  if (M % 16) return GELIM_FAIL(GELIM_E_ARG, "drbt tile_gemm: M not a multiple of 16");
-  const dim3 grid((unsigned)(M / 16 * 8));
-  if (accumulate)
-    hipLaunchKernelGGL(drbt_tile_kernel<true>, grid, dim3(64), 0, s, C, ldc, A, lda, B, ldb, -1.0);
-  else
-    hipLaunchKernelGGL(drbt_tile_kernel<false>, grid, dim3(64), 0, s, C, ldc, A, lda, B, ldb, 1.0);
-  HIP_TRY(hipGetLastError());
-  return GELIM_OK;
+  return gelim::dgemm_tiles(gelim::GemmOp{C, ldc, A, lda, B, ldb, M, 128, 128}, gelim::GemmOp{}, accumulate ? -1.0 : 1.0,
+                            accumulate, s);
 }
 
 }  // namespace

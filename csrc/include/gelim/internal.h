@@ -51,6 +51,10 @@ struct GemmOp {
   int64_t M, N, K;
 };
 int dgemm_pair(const GemmOp& p1, const GemmOp& p2, double alpha, int accumulate, struct ihipStream_t* s);
+// The same for K = 128 as 16 x 16 tiles, one 64-thread workgroup each, no LDS
+// (dgemm.hip tile16_kernel): bit-identical to dgemm, for 128-wide products on
+// a latency-bound chain.  M and N multiples of 16.
+int dgemm_tiles(const GemmOp& p1, const GemmOp& p2, double alpha, int accumulate, struct ihipStream_t* s);
 int fill_words_async(const WordFill* f, int nf, struct ihipStream_t* s);
 
 }  // namespace gelim

@@ -431,7 +431,9 @@ int dgemm_ex(double* C, int64_t ldc, const double* A, int64_t lda, const double*
 // kernel's per-element operation order, so the bits are dgemm's
 // (tests/test_gpu_dist_rbt.py::test_chain_products_match_dgemm).  128 x 128
 // x 128: 3.9 us against 8.6 for the 64-tile grid
-// (profiles/dist_rbt_replay_r6.md).
+// (profiles/dist_rbt_replay_r6.md).  At 128 x 8000 the tiles' operand
+// traffic (4x the 64-tiles') lost more than the LDS wait cost: hip-rbt keeps
+// dgemm there (profiles/rbt_trace_8192_r6.txt).
 struct Tile16 {
   double* C;
   int64_t ldc;

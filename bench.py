@@ -277,6 +277,9 @@ def main() -> None:
         "gflops_per_gpu": (2.0 / 3.0) * n ** 3 / step_s * 1e-9,
         "max_error": err.item(),
         "singular": info != 0,
+        # build provenance: the digest of the sources libgelim.so was compiled from, and whether it is this tree's
+        "libgelim_source_digest": gelim._native.build_digest(),
+        "libgelim_built_from_tree": gelim._native.build_digest() == gelim._native.source_digest(),
     })
     timer = threading.Timer(args.budget, watchdog)
     timer.daemon = True

@@ -40,6 +40,7 @@ _u64 = C.c_uint64
 _PROTOS = {
     "gelim_last_error": (C.c_char_p, []),
     "gelim_version": (C.c_char_p, []),
+    "gelim_build_digest": (C.c_char_p, []),
     "gelim_dat_size": (_i64, [C.c_char_p]),
     "gelim_dat_read": (_int, [C.c_char_p, _vp, _i64, _i64]),
     "gelim_matrix_gen": (_int, [_i64, C.c_char_p]),
@@ -194,3 +195,25 @@ def check(rc: int, what: str = "") -> int:
 
 def version() -> str:
     return lib().gelim_version().decode()
+
+
+# the files csrc/cmake/source_digest.cmake hashes (relative to csrc/)
+_DIGEST_GLOBS = ("core/**/*.cpp", "cpu/**/*.cpp", "comm/**/*.hip", "hip/**/*.hip", "hip/**/*.h", "include/**/*.h",
+                 "tools/**/*.cpp")
+
+
+def build_digest() -> str:
+    """The source digest compiled into the loaded libgelim.so."""
+    return lib().gelim_build_digest().decode()
+
+
+def source_digest(csrc: Path | None = None) -> str:
+    """The same digest (csrc/cmake/source_digest.cmake) of the sources in the
+    tree beside this package: equal to build_digest() when the loaded
+    library was built from them."""
+    import hashlib
+
+    root = Path(csrc) if csrc is not None else Path(__file__).resolve().parents[1] / "csrc"
+    files = sorted({p.relative_to(root).as_posix() for g in _DIGEST_GLOBS for p in root.glob(g) if p.is_file()})
+    lines = "".join(f"{f} {hashlib.sha256((root / f).read_bytes()).hexdigest()}\n" for f in files)
+    return hashlib.sha256(lines.encode()).hexdigest()

@@ -79,7 +79,7 @@ struct gelim_drbt_args {
   int32_t replay;       // 1: replay mode (module comment)
   double* F[3];         // replay: scratch slabs np x 128
   void* aux;            // replay: the virtual owners' side stream
-  double* Wfs;          // replay: 128 x 128, the virtual owners' side W
+  double* Wfs;          // replay: 2 x 128 x 128, the virtual owners' side W (a ring of two)
   int32_t* finfo;       // replay: the scratch inverses' info word
 };
 
@@ -256,21 +256,36 @@ struct Exec {
     return ship_small(t);
   }
 
-  // replay: the virtual owner of block k+2 applies panel k to it first
-  int foreign_side(int64_t k) {
+  // replay: the virtual owner of block k+2 applies panel k to it first --
+  // its top rows (what that owner's chain step reads on main) ...
+  int foreign_top(int64_t k) {
     const int64_t t = k + 2;
     if (!a.replay || t >= nb || owns(t)) return GELIM_OK;
     double* f = a.F[t % 3];
     const double* c = col(k);
+    double* W = a.Wfs + (k & 1) * NB * NB;  // a ring of two: foreign_rest(k - 1) still reads the other
     HIP_TRY(hipStreamWaitEvent(aux, ev(k, kSmall), 0));
     HIP_TRY(hipStreamWaitEvent(aux, ev(k, kNext), 0));
     if (t >= 3) HIP_TRY(hipStreamWaitEvent(aux, ev(t - 3, kShipDone), 0));  // the slab's previous column shipped
-    GELIM_TRY(tile_gemm(a.Wfs, NB, c, NB, f + k * NB * NB, NB, NB, 0, aux));
-    const int64_t top = std::min<int64_t>(2, nb - k - 1);  // block rows k+1, k+2: what the chain's main reads
-    GELIM_TRY(tile_gemm(f + (k + 1) * NB * NB, NB, c + NB * NB, NB, a.Wfs, NB, top * NB, 1, aux));
+    GELIM_TRY(tile_gemm(W, NB, c, NB, f + k * NB * NB, NB, NB, 0, aux));
+    const int64_t top = std::min<int64_t>(2, nb - k - 1);  // block rows k+1, k+2
+    GELIM_TRY(tile_gemm(f + (k + 1) * NB * NB, NB, c + NB * NB, NB, W, NB, top * NB, 1, aux));
     HIP_TRY(hipEventRecord(ev(t, kAuxTop), aux));
+    return GELIM_OK;
+  }
+  // ... and the rows below, once rest_k has landed.  Issued AFTER the next
+  // step's foreign_top: on the real run these are different owners' side
+  // streams, so one owner's top rows never queue behind another's bulk (a
+  // single replay stream in plain step order serialised them)
+  int foreign_rest(int64_t k) {
+    const int64_t t = k + 2;
+    if (!a.replay || t >= nb || owns(t)) return GELIM_OK;
+    double* f = a.F[t % 3];
+    const double* c = col(k);
+    const double* W = a.Wfs + (k & 1) * NB * NB;
+    const int64_t top = std::min<int64_t>(2, nb - k - 1);
     HIP_TRY(hipStreamWaitEvent(aux, ev(k, kBulk), 0));
-    GELIM_TRY(gemm(f + (k + 1 + top) * NB * NB, NB, 0, c + (1 + top) * NB * NB, NB, a.Wfs, NB, 0,
+    GELIM_TRY(gemm(f + (k + 1 + top) * NB * NB, NB, 0, c + (1 + top) * NB * NB, NB, W, NB, 0,
                    a.np - (k + 1 + top) * NB, NB, NB, -1.0, 1, a.side_cap, aux));
     HIP_TRY(hipEventRecord(ev(t, kAuxSide), aux));
     return GELIM_OK;
@@ -312,8 +327,10 @@ struct Exec {
       HIP_TRY(hipEventRecord(ev(k, kFirst), side));
       GELIM_TRY(apply_panel(k, c, lf, nbl, a.Ws + (lf - ls) * NB, a.nloc, a.side_cap, side));
       HIP_TRY(hipEventRecord(ev(k, kRest), side));
-      GELIM_TRY(foreign_side(k));
+      GELIM_TRY(foreign_top(k));
+      if (k >= 1) GELIM_TRY(foreign_rest(k - 1));
     }
+    GELIM_TRY(foreign_rest(nb - 1));
     HIP_TRY(hipStreamWaitEvent(main, ev(nb - 1, kRest), 0));
     HIP_TRY(hipStreamWaitEvent(main, ev(nb - 1, kBulk), 0));
     if (a.replay) {

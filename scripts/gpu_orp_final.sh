@@ -1,6 +1,8 @@
 # DistributedRBT one-rank-of-P replays for profiles/dist_rbt_replay_r6.md:
-# 8192 at P = 8 (three processes), 4, 2; 16384 at P = 8
+# the replay / executor tests, then 8192 at P = 8 (three processes), 4, 2; 16384 at P = 8
 set -o pipefail
+timeout -k 10 300 python -u -m pytest tests/test_gpu_dist_rbt.py -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_orp.log 2>&1; rc=$?; tail -1 gpurun_out/pytest_orp.log
+[ $rc -eq 0 ] || { grep -E "Error|assert|FAILED" gpurun_out/pytest_orp.log | head -20; exit $rc; }
 run() {  # n P tag
   timeout -k 10 150 python -u scripts/one_rank_of_p.py --n $1 --P $2 --rank 1 --json gpurun_out/orp_$3.json > gpurun_out/orp_$3.log 2>&1 || { tail -20 gpurun_out/orp_$3.log; exit 1; }
   python3 -c "

@@ -107,7 +107,7 @@ class OneRankOfP(DistributedRBT):
         dev = self.device
         self._fs = [torch.randn(self.np, NB, dtype=torch.float64, device=dev) for _ in range(3)]
         self._Wf = torch.zeros((NB, NB), dtype=torch.float64, device=dev)
-        self._Wfs = torch.zeros((NB, NB), dtype=torch.float64, device=dev)
+        self._Wfs = torch.zeros((2, NB, NB), dtype=torch.float64, device=dev)  # the native replay's W ring
         self._finfo = torch.zeros(1, dtype=torch.int32, device=dev)
         self._aux = dedicated_stream(dev, "aux")
         self._side_ev: dict[int, torch.cuda.Event] = {}
@@ -139,8 +139,8 @@ class OneRankOfP(DistributedRBT):
                 hb.wait()
             for h in self._ship_ev.pop(t - 3, []):  # the scratch slab's previous column has been shipped
                 h.wait()
-            self._gemm_bm(self._Wfs, False, col[:NB], f[k * NB:(k + 1) * NB], False, NB, 1.0, False, aux)
-            self._gemm_bm(f[(k + 1) * NB:], False, col[NB:], self._Wfs, False, NB, -1.0, True, aux)
+            self._gemm_bm(self._Wfs[0], False, col[:NB], f[k * NB:(k + 1) * NB], False, NB, 1.0, False, aux)
+            self._gemm_bm(f[(k + 1) * NB:], False, col[NB:], self._Wfs[0], False, NB, -1.0, True, aux)
             ev = torch.cuda.Event()
             ev.record(aux)
         self._side_ev[t] = ev

@@ -75,7 +75,7 @@ struct gelim_drbt_args {
   void* comm;
   void* rccl_small;     // communicators (null: no collective -- one rank, or the replay)
   void* rccl_bulk;
-  int32_t side_cap;     // CUs for the side stream's bulk GEMMs (0 = all)
+  int32_t side_cap;     // CUs for the bulk GEMMs beside the chain: side, and the rows below on comm (0 = all)
   int32_t replay;       // 1: replay mode (module comment)
   double* F[3];         // replay: scratch slabs np x 128
   void* aux;            // replay: the virtual owners' side stream

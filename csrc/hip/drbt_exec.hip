@@ -44,6 +44,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstddef>
 #include <cstdint>
 #include <vector>
 
@@ -351,6 +352,20 @@ extern "C" int gelim_drbt_chain_products(const double* Dk, const double* B, doub
   if (!W || !L || !D || (with_w && (!Dk || !B))) return GELIM_FAIL(GELIM_E_ARG, "drbt_chain_products: null operand");
   if (with_w) GELIM_TRY(tile_gemm(W, NB, Dk, NB, B, NB, NB, 0, (hipStream_t)stream));
   return tile_gemm(D, NB, L, NB, W, NB, NB, 1, (hipStream_t)stream);
+}
+
+// sizeof / offsetof of the argument block, for the Python mirror's layout test
+// (tests/test_dist_rbt_cpu.py): which = 0 size, 1 offset of Wm, 2 of side_cap,
+// 3 of Wfs, 4 of finfo.
+extern "C" int64_t gelim_drbt_args_layout(int32_t which) {
+  switch (which) {
+    case 0: return (int64_t)sizeof(gelim_drbt_args);
+    case 1: return (int64_t)offsetof(gelim_drbt_args, Wm);
+    case 2: return (int64_t)offsetof(gelim_drbt_args, side_cap);
+    case 3: return (int64_t)offsetof(gelim_drbt_args, Wfs);
+    case 4: return (int64_t)offsetof(gelim_drbt_args, finfo);
+    default: return -1;
+  }
 }
 
 // The grid cap (CUs) of the bulk GEMMs beside the chain: all CUs but 32,

@@ -121,6 +121,7 @@ _PROTOS = {
     "gelim_drbt_factor": (_int, [_vp, _vp]),
     "gelim_drbt_chain_products": (_int, [_vp, _vp, _vp, _vp, _vp, _int, _vp]),
     "gelim_drbt_side_cap": (_int, []),
+    "gelim_drbt_args_layout": (_i64, [_i32]),
     "gelim_mixed_factor": (_int, [_vp, _vp, _i64, _vp]),
     "gelim_mixed_apply": (_int, [_vp, _vp, _i64, _vp, _vp]),
     "gelim_gpu_leaf_max_rows": (_i64, []),

@@ -158,3 +158,18 @@ def test_dist_rbt_pad_warning():
     with pytest.warns(RuntimeWarning, match="padded to 4096"):
         d = DistributedRBT(c, 2048, single_fast_path=False)
     assert d.pad_ratio == 2.0
+
+
+def test_native_executor_args_layout_matches_python_mirror(gelim):
+    """parallel/dist_rbt.py _ExecArgs mirrors csrc/hip/drbt_exec.hip's
+    gelim_drbt_args field for field; a drift would hand the executor shifted
+    pointers, so size and the offsets of fields late in the block are pinned."""
+    import ctypes
+
+    from gelim import _native
+    from gelim.parallel.dist_rbt import _ExecArgs
+
+    lay = _native.lib().gelim_drbt_args_layout
+    assert lay(0) == ctypes.sizeof(_ExecArgs)
+    for which, field in ((1, "Wm"), (2, "side_cap"), (3, "Wfs"), (4, "finfo")):
+        assert lay(which) == getattr(_ExecArgs, field).offset, field

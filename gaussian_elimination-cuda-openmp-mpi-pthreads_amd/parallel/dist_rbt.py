@@ -175,11 +175,11 @@ class DistributedRBT:
         # x 40 KB) and the chain's next kernel -- the inverse, a W product --
         # waits for the whole grid to be dispatched: 40-120 us per block in the
         # one-rank-of-8 replay (profiles/dist_rbt_replay_r6.md).  Capped, the
-        # persistent form leaves 32 CUs free.  Only from 8 ranks: at 2 and 4 the
+        # persistent form leaves 16 CUs free.  Only from 8 ranks: at 2 and 4 the
         # side share (1/P of the trailing update) is large enough that the cap
         # costs more than it saves -- one-rank-of-P replay, same box, two rounds:
         # P = 2 10.3-10.5 ms uncapped vs 11.5-11.8 capped, P = 4 8.1-8.7 vs 9.3,
-        # P = 8 8.4-8.5 vs 6.9-8.4 (scripts/gpu_cap_by_p.sh).
+        # P = 8 6.9-8.5 uncapped vs 6.8-7.1 at CUs - 16 (scripts/gpu_cap_by_p.sh, gpu_cap_p8.sh).
         self.side_cap = int(_native.lib().gelim_drbt_side_cap()) if self.gpu and self.P >= 8 else 0
         self.last_issue_s = None
         self._ud, self._vd = butterfly_diagonals(self.np, seed)

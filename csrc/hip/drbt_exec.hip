@@ -371,8 +371,9 @@ extern "C" int64_t gelim_drbt_args_layout(int32_t which) {
 // The grid cap (CUs) of the bulk GEMMs beside the chain: all CUs but 16,
 // which the chain's inverse and tile products then always find free
 // (parallel/dist_rbt.py side_cap; one-rank-of-8 replay, four alternating
-// rounds: factor 6.8-7.1 ms at CUs - 16 in 4 of 4 processes, 7.0-8.4 at
-// CUs - 32, 6.9-8.5 uncapped, profiles/dist_rbt_replay_r6.md).
+// rounds on one box: factor 6.8-7.1 ms at CUs - 16 in 4 of 4 processes,
+// 7.0-8.4 at CUs - 32, 6.9-8.5 uncapped; another box ran 7.1-8.3 at every
+// cap, profiles/dist_rbt_replay_r6.md).
 extern "C" int gelim_drbt_side_cap(void) {
   int dev = 0, ncu = 0;
   (void)hipGetDevice(&dev);

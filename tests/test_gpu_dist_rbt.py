@@ -287,10 +287,11 @@ def test_native_executor_matches_python(gelim, cuda, n):
     assert torch.equal(out[True][1], out[False][1])
 
 
-@pytest.mark.parametrize("schedule", ["native", "python"])
-def test_one_rank_of_p_replay_runs(tmp_path, schedule):
-    """scripts/one_rank_of_p.py (rank 1 of a virtual 4-rank run, the other
-    ranks' chain steps replayed on this GPU) completes and reports times."""
+@pytest.mark.parametrize("schedule,P", [("native", 4), ("python", 4), ("native", 8)])
+def test_one_rank_of_p_replay_runs(tmp_path, schedule, P):
+    """scripts/one_rank_of_p.py (rank 1 of a virtual P-rank run, the other
+    ranks' chain steps replayed on this GPU) completes and reports times; at
+    P = 8 the bulk GEMMs beside the chain run capped (persistent dgemm)."""
     import json
     import os
     import subprocess
@@ -299,7 +300,7 @@ def test_one_rank_of_p_replay_runs(tmp_path, schedule):
 
     root = Path(__file__).resolve().parents[1]
     out = tmp_path / "orp.json"
-    cmd = [sys.executable, str(root / "scripts" / "one_rank_of_p.py"), "--n", "4096", "--P", "4", "--rank", "1",
+    cmd = [sys.executable, str(root / "scripts" / "one_rank_of_p.py"), "--n", "4096", "--P", str(P), "--rank", "1",
            "--reps", "2", "--json", str(out)] + (["--python-schedule"] if schedule == "python" else [])
     p = subprocess.run(cmd, cwd=root, env=dict(os.environ), capture_output=True, text=True, timeout=110)
     assert p.returncode == 0, p.stderr[-3000:]
